@@ -1,0 +1,199 @@
+/*
+ * mpccbf.h — C ABI of the MI355X-native batched MPC-CBF QP solver (libmpccbf.so).
+ *
+ * This is the drop-in boundary that replaces the CPLEX call of the reference hot path:
+ *
+ *   qpcpp::Solver<double>::solve(Problem&)          workspace/lib/qpcpp/include/qpcpp/solvers/Solver.h:27-37
+ *   qpcpp::CPLEXSolver<double>::solve(Problem&)     workspace/lib/qpcpp/src/solvers/CPLEX.cpp:35-177
+ *   called from ConnectivityIMPCCBF::optimize        workspace/lib/mpc_cbf/src/controller/ConnectivityIMPCCBF.cpp:199-211
+ *
+ * Two entry families:
+ *   (1) mpccbf_qp_solve_dense*: one generic dense QP in the flattened CPLEX form (what
+ *       CPLEXSolver::solve builds from a qpcpp::Problem, CPLEX.cpp:52-147). The C++ adapter
+ *       qpcpp::HIPSolver<double> (mpc-cbf_amd/csrc/qpcpp/) flattens a Problem into this.
+ *   (2) mpccbf_create / mpccbf_impc_solve: the structured, batched path. The parameter-only
+ *       operators of the MPC-CBF QP (PiecewiseBezierMPCQPOperations ctor, :9-38) are built once
+ *       per context; each call runs ConnectivityIMPCCBF::optimize (ConnectivityIMPCCBF.cpp:47-215)
+ *       for a whole batch of agents on the GPU: both IMPC iterations, the closed-form safety-CBF
+ *       rows (ConnectivityCBF.cpp:152-198, in place of GiNaC substitution), and the QP solves.
+ *
+ * Conventions
+ *   - All numbers are FP64 (the reference instantiates <double, 3U>).
+ *   - A state is 6 doubles [px, py, yaw, vx, vy, vyaw] (model::State, DIM = 3).
+ *   - Infinite bounds: any value <= -1e300 / >= 1e300 (numeric_limits<double>::lowest()/max()
+ *     as used by qpcpp::Problem, Problem.h:366-372).
+ *   - Solve statuses are qpcpp::SolveStatus indices (Solver.h:13-21): MPCCBF_OPTIMAL == 0 ...
+ *   - Functions return MPCCBF_OK (0) or a negative error code; they never throw. The last
+ *     error message of the calling thread is available from mpccbf_last_error().
+ *   - Pointers in mpccbf_batch are DEVICE pointers; work is enqueued on the given hipStream_t
+ *     (passed as void*; NULL = default stream) and is asynchronous. The dense-QP functions take
+ *     HOST pointers and are synchronous.
+ *   - One context per host thread/stream (contexts hold device buffers; not thread-safe).
+ */
+#ifndef MPCCBF_H
+#define MPCCBF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCCBF_ABI_VERSION 1
+
+/* qpcpp::SolveStatus (Solver.h:13-21) */
+enum {
+    MPCCBF_OPTIMAL = 0,
+    MPCCBF_FEASIBLE = 1,
+    MPCCBF_UNBOUNDED = 2,
+    MPCCBF_INFEASIBLE = 3,
+    MPCCBF_ERROR = 4,
+    MPCCBF_UNKNOWN = 5, /* also: IMPC iteration not attempted (reference `break`, :208-211) */
+    MPCCBF_INFEASIBLEORUNBOUNDED = 6
+};
+
+/* API return codes */
+enum {
+    MPCCBF_OK = 0,
+    MPCCBF_ERR_INVALID_ARGUMENT = -1, /* std::invalid_argument / runtime_error in the reference */
+    MPCCBF_ERR_HIP = -2,
+    MPCCBF_ERR_CAPACITY = -3,
+    MPCCBF_ERR_NO_DEVICE = -4,
+    MPCCBF_ERR_INTERNAL = -5
+};
+
+/* Parameters: the JSON keys of experiments/config/base_config.json as parsed and validated by
+ * common/include/common/parsing.hpp:20-214 (mpc_params, physical_limits, cbf_params, bezier_params). */
+typedef struct mpccbf_params {
+    double h, Ts;
+    int32_t k_hor;
+    double w_pos_err, w_u_eff;
+    int32_t spd_f;
+    double v_min[3], v_max[3], a_min[3], a_max[3];
+    double d_min;
+    int32_t cbf_horizon, impc_iter, slack_mode;
+    double slack_cost, slack_decay_rate;
+    int32_t num_pieces, num_control_points;
+    double piece_max_parameter;
+    int32_t continuity_upto_degree;
+} mpccbf_params;
+
+typedef struct mpccbf_ctx mpccbf_ctx;
+
+/* Context options (all optional; zero-initialise for defaults). */
+typedef struct mpccbf_options {
+    int32_t device;            /* HIP device ordinal (default 0) */
+    int32_t keep_redundant;    /* 1: keep every box row (no exact host-side redundancy removal) */
+    int32_t no_cbf_filter;     /* 1: keep every CBF row (no exact in-kernel redundancy filter) */
+    int32_t max_pdip_iters;    /* default 60 */
+    double tolerance;          /* PDIP relative tolerance, default 1e-9 */
+} mpccbf_options;
+
+/* Validates p like parsing.hpp:37-135,182-214, builds the parameter-only operators on the host
+ * and uploads them. Returns MPCCBF_ERR_INVALID_ARGUMENT with the reference's message on bad
+ * parameters. */
+int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx** out);
+void mpccbf_destroy(mpccbf_ctx* ctx);
+
+/* Sizes: n = num_pieces * 3 * num_control_points decision variables (curve control points,
+ * layout [piece][dim][control point], BezierQPOperations.cpp:180-204); nz = free dimension
+ * after the equality constraints; rows = shared inequality rows kept after exact reduction. */
+int mpccbf_num_vars(const mpccbf_ctx* ctx);
+int mpccbf_reduced_dim(const mpccbf_ctx* ctx);
+int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
+
+/* One IMPC control step for a batch of agents (ConnectivityIMPCCBF::optimize per agent).
+ * Inputs (device):
+ *   states      num_states x 6, every agent visible to this batch (local + gathered)
+ *   agent_first the batch solves agents [agent_first, agent_first + num_agents) of `states`
+ *   targets     num_agents x 3: reference position replicated over the horizon
+ *               (MPCCBFFormationControl_example.cpp:143-144); or NULL and give `refs`
+ *   refs        num_agents x 3*k_hor full reference trajectory (ref_positions); or NULL
+ *   nb_row_ptr  num_agents + 1 CSR offsets (nb_row_ptr[0] may be nonzero)
+ *   nb_col      neighbour indices into `states` (the reference uses all N-1 others, :59-67)
+ * Outputs (device, any may be NULL):
+ *   x           num_agents x n: control points of the last OPTIMAL iteration (the curve the
+ *               driver keeps, example :160-164); NaN if no iteration was OPTIMAL
+ *   status      num_agents x impc_iter SolveStatus per IMPC iteration (UNKNOWN = not attempted)
+ *   obj         num_agents x impc_iter optimal objective x^T H x + c^T x (CPLEX.cpp:144-146)
+ *   iters       num_agents x impc_iter interior-point iterations
+ *   next_states num_agents x 6: position/velocity of the kept curve at t = h (Jacobi update of
+ *               the closed-loop driver, example :188-207, without noise); unchanged input if no
+ *               curve was found. */
+typedef struct mpccbf_batch {
+    int32_t num_states;
+    const double* states;
+    int32_t agent_first;
+    int32_t num_agents;
+    const double* targets;
+    const double* refs;
+    const int32_t* nb_row_ptr;
+    const int32_t* nb_col;
+    double* x;
+    int32_t* status;
+    double* obj;
+    int32_t* iters;
+    double* next_states;
+} mpccbf_batch;
+
+int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);
+
+/* Tuning knob: kernel geometry for mpccbf_impc_solve. 0 (default): 16 lanes per agent,
+ * 4 row slots per lane; 1: 64 lanes per agent, 1 slot; 2: 64 lanes, 4 slots (wide rows). */
+int mpccbf_set_variant(mpccbf_ctx* ctx, int variant);
+
+/* Neighbour lists on the device: for each agent of [agent_first, agent_first+num_agents) the
+ * (at most) k nearest other agents of `states` (planar distance) within `radius`, sorted by
+ * index; k <= 0 means all N-1 others (reference semantics, radius ignored). row_ptr gets
+ * num_agents + 1 entries, col capacity num_agents * (k > 0 ? k : num_states - 1). */
+int mpccbf_build_neighbors(mpccbf_ctx* ctx, const double* states, int32_t num_states,
+                           int32_t agent_first, int32_t num_agents, int32_t k, double radius,
+                           int32_t* row_ptr, int32_t* col, void* hip_stream);
+
+/* Generic dense QP in the flattened CPLEX form (host pointers; synchronous):
+ *   minimise  x^T H x + c^T x + c0        (H symmetric: sum_{i<=j} q_ij x_i x_j, CPLEX.cpp:122-147)
+ *   s.t.      lo_r <= A_r x <= hi_r       (rows; lo == hi is an equality)
+ *             vlo_i <= x_i <= vhi_i
+ * Equalities are eliminated on the host (null space), the reduced problem is solved by the GPU
+ * interior-point kernel. x_out is written only if *status_out is OPTIMAL (Solver.h:33-35). */
+typedef struct mpccbf_dense_qp {
+    int32_t n, m;
+    const double* H;  /* n x n row-major */
+    const double* c;  /* n */
+    double c0;
+    const double* A;  /* m x n row-major */
+    const double* lo;
+    const double* hi;
+    const double* vlo; /* n, or NULL = free */
+    const double* vhi;
+} mpccbf_dense_qp;
+
+int mpccbf_qp_solve_dense(const mpccbf_dense_qp* qp, double* x_out, double* obj_out,
+                          int32_t* status_out);
+/* Batched form: count independent QPs solved in one launch. */
+int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, double* const* x_out,
+                                double* obj_out, int32_t* status_out);
+
+/* Host-only inspection of the condensed operators (no device needed; used by the CPU tests).
+ * Call once with capacity_ok = 0 to get the sizes, then again with every pointer sized:
+ *   H n*n, Z n*nz, Xs n*6, Pr nz*nz, Qs nz*6, Qt nz*3, Ks 6*6, Kt 3*6,
+ *   G m*nz, Gs m*6, lo/hi m, Cs mc*6, clo/chi mc, UZ0 3*nz, US0 3*6 (any pointer may be NULL).
+ * Objective of the condensed QP: 1/2 y^T Pr y + (Qs s0 + Qt t)^T y + s0^T Ks s0 + t^T Kt s0,
+ * full decision vector x = Xs s0 + Z y. */
+typedef struct mpccbf_host_ops {
+    int32_t n, nz, m, mc, rows_total, rows_removed;
+    int32_t capacity_ok;
+    double *H, *Z, *Xs, *Pr, *Qs, *Qt, *Ks, *Kt, *G, *Gs, *lo, *hi, *Cs, *clo, *chi, *UZ0, *US0;
+} mpccbf_host_ops;
+int mpccbf_host_operators(const mpccbf_params* p, int32_t keep_redundant, mpccbf_host_ops* out);
+const char* mpccbf_host_last_error(void);
+
+/* Diagnostics */
+const char* mpccbf_last_error(void);
+const char* mpccbf_status_string(int32_t status); /* SolveStatusToStr, Solver.cpp:4-28 */
+int mpccbf_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCCBF_H */

@@ -1,0 +1,245 @@
+// capi.hip — the C ABI of include/mpccbf.h: context lifetime, operator upload, launches.
+// No exception crosses this boundary (the reference's std::invalid_argument / runtime_error
+// become MPCCBF_ERR_INVALID_ARGUMENT plus a thread-local message).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mpccbf.h"
+#include "host/operators.hpp"
+#include "kernels/impc.hpp"
+
+namespace mpccbf {
+
+hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
+                       hipStream_t s);
+int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
+                     double radius, int32_t* row_ptr, int32_t* col, void* scratch,
+                     size_t scratch_bytes, hipStream_t s);
+size_t neighbors_scratch_bytes(int num_states, int num_agents, int k);
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) return fail(MPCCBF_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+}  // namespace mpccbf
+
+struct mpccbf_ctx {
+    mpccbf_params p;
+    mpccbf_options opt;
+    mpccbf::Operators ops;
+    mpccbf::DevOps dev;
+    int device = 0;
+    double* dbuf = nullptr;
+    size_t dbuf_elems = 0;
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    int variant = 0;
+};
+
+using namespace mpccbf;
+
+static void pack(std::vector<double>& v, int32_t& off, const Mat& m) {
+    off = (int32_t)v.size();
+    v.insert(v.end(), m.a.begin(), m.a.end());
+}
+static void pack(std::vector<double>& v, int32_t& off, const std::vector<double>& m) {
+    off = (int32_t)v.size();
+    v.insert(v.end(), m.begin(), m.end());
+}
+static void pack(std::vector<double>& v, int32_t& off, const std::vector<Mat>& ms) {
+    off = (int32_t)v.size();
+    for (const Mat& m : ms) v.insert(v.end(), m.a.begin(), m.a.end());
+}
+
+extern "C" {
+
+int mpccbf_abi_version(void) { return MPCCBF_ABI_VERSION; }
+
+const char* mpccbf_last_error(void) { return g_err.c_str(); }
+
+const char* mpccbf_status_string(int32_t s) {
+    switch (s) {
+        case MPCCBF_OPTIMAL: return "OPTIMAL";
+        case MPCCBF_FEASIBLE: return "FEASIBLE";
+        case MPCCBF_UNBOUNDED: return "UNBOUNDED";
+        case MPCCBF_INFEASIBLE: return "INFEASIBLE";
+        case MPCCBF_ERROR: return "ERROR";
+        case MPCCBF_UNKNOWN: return "UNKNOWN";
+        case MPCCBF_INFEASIBLEORUNBOUNDED: return "INFEASIBLEORUNBOUNDED";
+        default: return "";
+    }
+}
+
+int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx** out) {
+    if (!p || !out) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    const std::string verr = validate_params(*p);
+    if (!verr.empty()) return fail(MPCCBF_ERR_INVALID_ARGUMENT, verr);
+    if (p->cbf_horizon > MAX_CBF_H) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "cbf_horizon > 8 not supported");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
+    mpccbf_ctx* c = new mpccbf_ctx();
+    c->p = *p;
+    if (opt) c->opt = *opt; else std::memset(&c->opt, 0, sizeof(c->opt));
+    c->device = c->opt.device;
+    try {
+        c->ops = build_operators(*p, c->opt.keep_redundant != 0);
+    } catch (const std::exception& e) {
+        delete c;
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, e.what());
+    }
+    const Operators& o = c->ops;
+    DevOps& d = c->dev;
+    std::memset(&d, 0, sizeof(d));
+    d.n = o.n;
+    d.nz = o.nz;
+    d.m = o.G.r;
+    d.mc = o.Cs.r;
+    d.K = o.K;
+    d.spd_f = o.spd_f;
+    d.cbf_h = o.cbf_h;
+    d.impc_iter = p->impc_iter;
+    std::vector<double> v;
+    pack(v, d.o_Z, o.Z);
+    pack(v, d.o_Xs, o.Xs);
+    pack(v, d.o_Pr, o.Pr);
+    pack(v, d.o_LPr, o.LPr);
+    pack(v, d.o_Qs, o.Qs);
+    pack(v, d.o_Qt, o.Qt);
+    pack(v, d.o_Qr, o.Qr);
+    pack(v, d.o_Ks, o.Ks);
+    pack(v, d.o_Kt, o.Kt);
+    pack(v, d.o_Kr, o.Kr);
+    pack(v, d.o_G, o.G);
+    pack(v, d.o_Gs, o.Gs);
+    pack(v, d.o_lo, o.lo);
+    pack(v, d.o_hi, o.hi);
+    pack(v, d.o_Cs, o.Cs);
+    pack(v, d.o_clo, o.clo);
+    pack(v, d.o_chi, o.chi);
+    pack(v, d.o_UZ, o.UZ);
+    pack(v, d.o_US, o.US);
+    pack(v, d.o_PZ, o.PZ);
+    pack(v, d.o_PS, o.PS);
+    pack(v, d.o_AZ, o.AZ);
+    pack(v, d.o_AS, o.AS);
+    v.push_back(0.0);  // keep every offset addressable even for empty operators
+    for (int i = 0; i < 3; i++) {
+        d.a_lo[i] = o.a_lo[i];
+        d.a_hi[i] = o.a_hi[i];
+    }
+    d.d_min = p->d_min;
+    d.cbf_filter = c->opt.no_cbf_filter ? 0 : 1;
+    d.maxit = c->opt.max_pdip_iters > 0 ? c->opt.max_pdip_iters : 60;
+    d.tol = c->opt.tolerance > 0 ? c->opt.tolerance : 1e-9;
+    d.feas_tol = 1e-6;  // CPLEX default feasibility tolerance
+    c->variant = 0;
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipMalloc(&c->dbuf, v.size() * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(c->dbuf, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (c->dbuf) (void)hipFree(c->dbuf);
+        delete c;
+        return fail(MPCCBF_ERR_HIP, std::string("operator upload: ") + hipGetErrorString(e));
+    }
+    c->dbuf_elems = v.size();
+    *out = c;
+    return MPCCBF_OK;
+}
+
+void mpccbf_destroy(mpccbf_ctx* c) {
+    if (!c) return;
+    if (c->dbuf) (void)hipFree(c->dbuf);
+    if (c->scratch) (void)hipFree(c->scratch);
+    delete c;
+}
+
+int mpccbf_num_vars(const mpccbf_ctx* c) { return c ? c->ops.n : -1; }
+int mpccbf_reduced_dim(const mpccbf_ctx* c) { return c ? c->ops.nz : -1; }
+int mpccbf_num_shared_rows(const mpccbf_ctx* c) { return c ? c->ops.G.r : -1; }
+
+int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
+    if (!c || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    if (b->num_agents < 0 || b->agent_first < 0 || b->agent_first + b->num_agents > b->num_states)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
+    if (b->num_agents == 0) return MPCCBF_OK;
+    if (!b->states || !b->nb_row_ptr || (!b->nb_col && b->num_states > 1))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "states / neighbour CSR missing");
+    if (!b->targets && !b->refs) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "targets or refs required");
+    ImpcArgs a;
+    a.num_states = b->num_states;
+    a.states = b->states;
+    a.agent_first = b->agent_first;
+    a.num_agents = b->num_agents;
+    a.targets = b->targets;
+    a.refs = b->targets ? nullptr : b->refs;
+    a.nb_row_ptr = b->nb_row_ptr;
+    a.nb_col = b->nb_col;
+    a.x = b->x;
+    a.status = b->status;
+    a.obj = b->obj;
+    a.iters = b->iters;
+    a.next_states = b->next_states;
+    HIP_TRY(hipSetDevice(c->device));
+    hipError_t e = launch_impc(c->dev, c->dbuf, a, c->variant, (hipStream_t)stream);
+    if (e == hipErrorInvalidValue)
+        return fail(MPCCBF_ERR_CAPACITY, "no kernel instantiation for this reduced dimension / row count");
+    HIP_TRY(e);
+    return MPCCBF_OK;
+}
+
+int mpccbf_set_variant(mpccbf_ctx* c, int variant) {
+    if (!c) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    c->variant = variant;
+    return MPCCBF_OK;
+}
+
+int mpccbf_build_neighbors(mpccbf_ctx* c, const double* states, int32_t num_states,
+                           int32_t first, int32_t num_agents, int32_t k, double radius,
+                           int32_t* row_ptr, int32_t* col, void* stream) {
+    if (!c || !states || !row_ptr) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    if (first < 0 || num_agents < 0 || first + num_agents > num_states)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
+    if (k > 16) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "k > 16 not supported (use k <= 0 for all)");
+    if (k > 0 && !(radius > 0)) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "radius must be positive");
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t need = neighbors_scratch_bytes(num_states, num_agents, k);
+    if (need > c->scratch_bytes) {
+        if (c->scratch) (void)hipFree(c->scratch);
+        c->scratch = nullptr;
+        c->scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&c->scratch, need));
+        c->scratch_bytes = need;
+    }
+    const int rc = launch_neighbors(states, num_states, first, num_agents, k, radius, row_ptr, col,
+                                    c->scratch, c->scratch_bytes, (hipStream_t)stream);
+    if (rc != 0) return fail(MPCCBF_ERR_HIP, std::string("neighbour kernels: ") + hipGetErrorString((hipError_t)rc));
+    return MPCCBF_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+// Implemented in dense_qp.hip (generic flattened-CPLEX QP path); placeholders until then.
+int mpccbf_qp_solve_dense(const mpccbf_dense_qp*, double*, double*, int32_t*) {
+    return fail(MPCCBF_ERR_INTERNAL, "dense path not built");
+}
+int mpccbf_qp_solve_dense_batch(int32_t, const mpccbf_dense_qp*, double* const*, double*, int32_t*) {
+    return fail(MPCCBF_ERR_INTERNAL, "dense path not built");
+}
+}

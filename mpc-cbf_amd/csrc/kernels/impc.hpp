@@ -1,0 +1,40 @@
+// impc.hpp — device-side layout of the condensed MPC-CBF operators and kernel arguments.
+#pragma once
+
+#include <stdint.h>
+
+namespace mpccbf {
+
+constexpr int MAX_CBF_H = 8;
+
+// Offsets (in doubles) of each operator inside one device buffer (see operators.hpp).
+struct DevOps {
+    int32_t n, nz, m, mc, K, spd_f, cbf_h, impc_iter;
+    int32_t o_Z, o_Xs, o_Pr, o_LPr, o_Qs, o_Qt, o_Qr, o_Ks, o_Kt, o_Kr;
+    int32_t o_G, o_Gs, o_lo, o_hi, o_Cs, o_clo, o_chi;
+    int32_t o_UZ, o_US, o_PZ, o_PS, o_AZ, o_AS;
+    double a_lo[3], a_hi[3];
+    double d_min;
+    int32_t cbf_filter;
+    int32_t maxit;
+    double tol;
+    double feas_tol;  // absolute row-violation tolerance for constant rows / single-row checks
+};
+
+struct ImpcArgs {
+    int32_t num_states;
+    const double* states;
+    int32_t agent_first;
+    int32_t num_agents;
+    const double* targets;
+    const double* refs;  // full 3K per agent (tail used)
+    const int32_t* nb_row_ptr;
+    const int32_t* nb_col;
+    double* x;
+    int32_t* status;
+    double* obj;
+    int32_t* iters;
+    double* next_states;
+};
+
+}  // namespace mpccbf

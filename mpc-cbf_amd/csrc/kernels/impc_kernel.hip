@@ -1,0 +1,382 @@
+// impc_kernel.hip — one fused launch per control step: ConnectivityIMPCCBF::optimize for a
+// batch of agents (mpc_cbf/src/controller/ConnectivityIMPCCBF.cpp:47-215).
+//
+// Mapping (gfx950, wave64): one agent per group of G lanes (G = 64 or 16). Per agent:
+//   1. state-dependent parts of the condensed QP: q = Qs s0 + Qt t, shared row bounds shifted by
+//      Gs s0, constant-row feasibility (e.g. the k = 0 velocity bound, which the initial-state
+//      equality pins);
+//   2. IMPC iteration 0: closed-form safety-CBF rows at the current state
+//      (ConnectivityCBF.cpp:152-198 via ConnectivityMPCCBFQPOperations.cpp:192-205), exact
+//      redundancy filter, compaction into the group's LDS staging area, PDIP solve;
+//   3. IMPC iteration 1 (only after OPTIMAL, :158): predicted ego states from iteration 0's curve
+//      at h_samples(k), k < cbf_horizon (:161-168), CBF rows per (neighbour, k) (:252-272), solve;
+//   4. outputs: per-iteration status/objective/iterations, control points of the kept curve
+//      (x = Xs s0 + Z y), and the closed-loop next state (curve at t = h).
+// Shared operators are read through the scalar/L1/L2 path (uniform addresses); per-agent inputs
+// are a 48-byte state, a 24-byte target and the neighbour states (gathered, L2-resident).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "impc.hpp"
+#include "pdip.hpp"
+
+namespace mpccbf {
+namespace dev {
+
+__device__ __forceinline__ const double* opp(const double* buf, int off) { return buf + off; }
+
+// Safety HOCBF row of ConnectivityCBF::initSafetyCBF (cbf/src/detail/ConnectivityCBF.cpp:152-198)
+// evaluated at (ego e, neighbour nb): a = L_g L_f h = (2dx, 2dy, 0),
+// b = L_f^2 h + L_f alpha(h) + alpha(L_f h + alpha(h)), alpha(x) = 5 x^3 (gamma = 5, :62, :19-21),
+// where L_f alpha differentiates the ego position only (f = A x, :171-184).
+__device__ __forceinline__ void safety_cbf(const double e[6], double npx, double npy, double nvx,
+                                           double nvy, double dmin, double a[3], double& b) {
+    constexpr double gamma = 5.0;
+    const double dx = e[0] - npx, dy = e[1] - npy;
+    const double dvx = e[3] - nvx, dvy = e[4] - nvy;
+    const double hh = dx * dx + dy * dy - dmin * dmin;
+    const double lfh = 2.0 * (dx * dvx + dy * dvy);
+    const double lf2h = 2.0 * (dvx * dvx + dvy * dvy);
+    const double alpha_h = gamma * hh * hh * hh;
+    const double lf_alpha = 3.0 * gamma * hh * hh * (2.0 * dx * e[3] + 2.0 * dy * e[4]);
+    const double psi = lfh + alpha_h;
+    b = lf2h + lf_alpha + gamma * psi * psi * psi;
+    a[0] = 2.0 * dx;
+    a[1] = 2.0 * dy;
+    a[2] = 0.0;
+}
+
+template <int NZ, int G, int R>
+__global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double* __restrict__ buf,
+                                                    const ImpcArgs args) {
+    constexpr int GPB = 256 / G;
+    const int gl = threadIdx.x & (G - 1);
+    const int gib = threadIdx.x / G;
+    const int ai = blockIdx.x * GPB + gib;  // agent index within the batch
+    if (ai >= args.num_agents) return;      // whole group leaves together
+
+    extern __shared__ double lds_stage[];
+    const int cap = R * G - op.m;  // CBF row slots per agent
+    double* stage = lds_stage + (size_t)gib * cap * (NZ + 1);
+
+    const int self = args.agent_first + ai;
+    double s0[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) s0[i] = args.states[(size_t)self * 6 + i];
+
+    // ---- linear term q and objective constant
+    double q[NZ];
+    double kconst = 0.0;
+    {
+        const double* Qs = opp(buf, op.o_Qs);
+        const double* Ks = opp(buf, op.o_Ks);
+#pragma unroll
+        for (int i = 0; i < NZ; i++) {
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) v = fma(Qs[i * 6 + s], s0[s], v);
+            q[i] = v;
+        }
+#pragma unroll
+        for (int s = 0; s < 6; s++) {
+            double v = 0.0;
+#pragma unroll
+            for (int u = 0; u < 6; u++) v = fma(Ks[s * 6 + u], s0[u], v);
+            kconst = fma(s0[s], v, kconst);
+        }
+        if (args.targets) {
+            const double* Qt = opp(buf, op.o_Qt);
+            const double* Kt = opp(buf, op.o_Kt);
+            double t[3];
+#pragma unroll
+            for (int d = 0; d < 3; d++) t[d] = args.targets[(size_t)ai * 3 + d];
+#pragma unroll
+            for (int i = 0; i < NZ; i++)
+#pragma unroll
+                for (int d = 0; d < 3; d++) q[i] = fma(Qt[i * 3 + d], t[d], q[i]);
+#pragma unroll
+            for (int d = 0; d < 3; d++) {
+                double v = 0.0;
+#pragma unroll
+                for (int s = 0; s < 6; s++) v = fma(Kt[d * 6 + s], s0[s], v);
+                kconst = fma(t[d], v, kconst);
+            }
+        } else {
+            const double* Qr = opp(buf, op.o_Qr);
+            const double* Kr = opp(buf, op.o_Kr);
+            const int nr = 3 * op.spd_f;
+            const double* rt = args.refs + (size_t)ai * 3 * op.K + 3 * (op.K - op.spd_f);
+            for (int j = 0; j < nr; j++) {
+                const double rv = rt[j];
+#pragma unroll
+                for (int i = 0; i < NZ; i++) q[i] = fma(Qr[i * nr + j], rv, q[i]);
+                double v = 0.0;
+#pragma unroll
+                for (int s = 0; s < 6; s++) v = fma(Kr[j * 6 + s], s0[s], v);
+                kconst = fma(rv, v, kconst);
+            }
+        }
+    }
+
+    // ---- shared rows into register slots
+    Rows<NZ, R> rw;
+    {
+        const double* Gm = opp(buf, op.o_G);
+        const double* Gs = opp(buf, op.o_Gs);
+        const double* lo = opp(buf, op.o_lo);
+        const double* hi = opp(buf, op.o_hi);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int slot = r * G + gl;
+            const bool on = slot < op.m;
+            const int si = on ? slot : 0;
+            double sh = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) sh = fma(Gs[si * 6 + s], s0[s], sh);
+#pragma unroll
+            for (int j = 0; j < NZ; j++) rw.g[r][j] = on ? Gm[si * NZ + j] : 0.0;
+            const double l = lo[si], h = hi[si];
+            rw.hl[r] = on && l > -1e300;
+            rw.hu[r] = on && h < 1e300;
+            rw.lo[r] = rw.hl[r] ? l - sh : 0.0;
+            rw.hi[r] = rw.hu[r] ? h - sh : 0.0;
+        }
+    }
+    // ---- constant rows: pure feasibility checks on s0
+    bool infeasible = false;
+    {
+        const double* Cs = opp(buf, op.o_Cs);
+        const double* clo = opp(buf, op.o_clo);
+        const double* chi = opp(buf, op.o_chi);
+        for (int i = gl; i < op.mc; i += G) {
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) v = fma(Cs[i * 6 + s], s0[s], v);
+            if (v < clo[i] - op.feas_tol || v > chi[i] + op.feas_tol) infeasible = true;
+        }
+        infeasible = grp_ballot<G>(infeasible) != 0ull;
+    }
+
+    const int nb0 = args.nb_row_ptr[ai], nb1 = args.nb_row_ptr[ai + 1];
+    const int nnb = nb1 - nb0;
+    const double* UZ = opp(buf, op.o_UZ);
+    const double* US = opp(buf, op.o_US);
+
+    double y[NZ], ykeep[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; i++) {
+        y[i] = 0.0;
+        ykeep[i] = 0.0;
+    }
+    bool have_curve = false;
+    bool success = true;
+    const PdipCfg cfg{op.maxit, op.tol};
+
+    for (int it = 0; it < op.impc_iter; it++) {
+        const size_t oi = (size_t)ai * op.impc_iter + it;
+        if (!success) {  // the reference breaks out of the IMPC loop (:208-211)
+            if (gl == 0) {
+                if (args.status) args.status[oi] = ST_UNKNOWN;
+                if (args.obj) args.obj[oi] = __builtin_nan("");
+                if (args.iters) args.iters[oi] = 0;
+            }
+            continue;
+        }
+        // ---- CBF rows -> LDS staging (compacted)
+        const int nk = (it == 0) ? 1 : op.cbf_h;
+        int count = 0;
+        bool row_infeasible = false;
+        for (int k = 0; k < nk; k++) {
+            double e[6];
+            if (it == 0) {
+#pragma unroll
+                for (int s = 0; s < 6; s++) e[s] = s0[s];
+            } else {
+                const double* PZ = opp(buf, op.o_PZ) + (size_t)k * 6 * NZ;
+                const double* PS = opp(buf, op.o_PS) + (size_t)k * 36;
+#pragma unroll
+                for (int s = 0; s < 6; s++) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int u = 0; u < 6; u++) v = fma(PS[s * 6 + u], s0[u], v);
+#pragma unroll
+                    for (int j = 0; j < NZ; j++) v = fma(PZ[s * NZ + j], y[j], v);
+                    e[s] = v;
+                }
+            }
+            // U_k s0 part of the acceleration at sample k
+            const double* UZk = UZ + (size_t)k * 3 * NZ;
+            const double* USk = US + (size_t)k * 18;
+            double us[3];
+#pragma unroll
+            for (int d = 0; d < 3; d++) {
+                double v = 0.0;
+#pragma unroll
+                for (int s = 0; s < 6; s++) v = fma(USk[d * 6 + s], s0[s], v);
+                us[d] = v;
+            }
+            for (int base = 0; base < nnb; base += G) {
+                const int j = base + gl;
+                bool keep = false;
+                double a[3] = {0.0, 0.0, 0.0}, b = 0.0;
+                if (j < nnb) {
+                    const int nbi = args.nb_col[nb0 + j];
+                    const double* ns = args.states + (size_t)nbi * 6;
+                    safety_cbf(e, ns[0], ns[1], ns[3], ns[4], op.d_min, a, b);
+                    // max / min of -a^T u over the acceleration box at sample k (those box rows
+                    // are part of every QP): b >= max  -> the row is implied (exactly redundant);
+                    // b < min - tol -> no acceleration satisfies it (infeasible).
+                    double bmax = 0.0, bmin = 0.0;
+#pragma unroll
+                    for (int d = 0; d < 3; d++) {
+                        const double v1 = -a[d] * op.a_lo[d], v2 = -a[d] * op.a_hi[d];
+                        bmax += fmax(v1, v2);
+                        bmin += fmin(v1, v2);
+                    }
+                    keep = !(op.cbf_filter && b >= bmax);
+                    if (b < bmin - op.feas_tol) row_infeasible = true;
+                }
+                const unsigned long long msk = grp_ballot<G>(keep);
+                const int pre = __popcll(msk & ((1ull << gl) - 1ull));
+                const int slot = count + pre;
+                if (keep && slot < cap) {
+                    double* dst = stage + (size_t)slot * (NZ + 1);
+                    // row: -a^T (US_k s0 + UZ_k y) <= b
+#pragma unroll
+                    for (int jz = 0; jz < NZ; jz++)
+                        dst[jz] = -(a[0] * UZk[jz] + a[1] * UZk[NZ + jz] + a[2] * UZk[2 * NZ + jz]);
+                    dst[NZ] = b + (a[0] * us[0] + a[1] * us[1] + a[2] * us[2]);
+                }
+                count += __popcll(msk);
+            }
+        }
+        row_infeasible = grp_ballot<G>(row_infeasible) != 0ull;
+        wave_lds_sync();
+        // ---- CBF rows into the free slots (previous iteration's CBF rows are replaced)
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const int slot = r * G + gl;
+            if (slot >= op.m) {
+                const int ci = slot - op.m;
+                const bool on = ci < count && ci < cap;
+                const double* src = stage + (size_t)(on ? ci : 0) * (NZ + 1);
+#pragma unroll
+                for (int jz = 0; jz < NZ; jz++) rw.g[r][jz] = on ? src[jz] : 0.0;
+                rw.hl[r] = false;
+                rw.hu[r] = on;
+                rw.lo[r] = 0.0;
+                rw.hi[r] = on ? src[NZ] : 0.0;
+            }
+        }
+        int st;
+        int nit = 0;
+        if (count > cap) {
+            st = ST_ERROR;  // capacity: caller re-runs with a wider instantiation
+        } else if (infeasible || row_infeasible) {
+            st = ST_INFEASIBLE;
+        } else {
+            const PdipOut po =
+                pdip_solve<NZ, G, R>(rw, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y, cfg);
+            st = po.status;
+            nit = po.iters;
+            if (st != ST_OPTIMAL) {
+                // certify: minimal uniform row violation above the feasibility tolerance
+                const double tstar = pdip_phase1<NZ, G, R>(rw, cfg);
+                if (tstar > op.feas_tol) st = ST_INFEASIBLE;
+            }
+        }
+        double objv = __builtin_nan("");
+        if (st == ST_OPTIMAL) {
+            const double* Pr = opp(buf, op.o_Pr);
+            double v = kconst;
+#pragma unroll
+            for (int i = 0; i < NZ; i++) {
+                double pyi = 0.0;
+#pragma unroll
+                for (int j = 0; j < NZ; j++) pyi = fma(Pr[i * NZ + j], y[j], pyi);
+                v = fma(y[i], 0.5 * pyi + q[i], v);
+            }
+            objv = v;
+#pragma unroll
+            for (int i = 0; i < NZ; i++) ykeep[i] = y[i];
+            have_curve = true;
+        } else {
+            success = false;
+        }
+        if (gl == 0) {
+            if (args.status) args.status[oi] = st;
+            if (args.obj) args.obj[oi] = objv;
+            if (args.iters) args.iters[oi] = nit;
+        }
+        wave_lds_sync();  // staging is rewritten by the next iteration
+    }
+
+    // ---- outputs: control points of the kept curve and the closed-loop next state
+    if (args.x) {
+        const double* Z = opp(buf, op.o_Z);
+        const double* Xs = opp(buf, op.o_Xs);
+        for (int i = gl; i < op.n; i += G) {
+            double v = 0.0;
+            if (have_curve) {
+#pragma unroll
+                for (int s = 0; s < 6; s++) v = fma(Xs[i * 6 + s], s0[s], v);
+#pragma unroll
+                for (int j = 0; j < NZ; j++) v = fma(Z[i * NZ + j], ykeep[j], v);
+            } else {
+                v = __builtin_nan("");
+            }
+            args.x[(size_t)ai * op.n + i] = v;
+        }
+    }
+    if (args.next_states && gl < 6) {
+        double v = s0[0];
+        if (have_curve) {
+            const double* AZ = opp(buf, op.o_AZ);
+            const double* AS = opp(buf, op.o_AS);
+            v = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) v = fma(AS[gl * 6 + s], s0[s], v);
+#pragma unroll
+            for (int j = 0; j < NZ; j++) v = fma(AZ[gl * NZ + j], ykeep[j], v);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 6; s++)
+                if (s == gl) v = s0[s];
+        }
+        args.next_states[(size_t)ai * 6 + gl] = v;
+    }
+}
+
+}  // namespace dev
+
+// Host-side launcher table (instantiations).
+struct ImpcLaunch {
+    int nz, G, R;
+    void (*fn)(const DevOps, const double*, const ImpcArgs);
+};
+
+template <int NZ, int G, int R>
+static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcArgs& a,
+                                hipStream_t s) {
+    constexpr int GPB = 256 / G;
+    const int blocks = (a.num_agents + GPB - 1) / GPB;
+    const size_t lds = (size_t)GPB * (R * G - op.m) * (NZ + 1) * sizeof(double);
+    hipLaunchKernelGGL((dev::impc_kernel<NZ, G, R>), dim3(blocks), dim3(256), lds, s, op, buf, a);
+    return hipGetLastError();
+}
+
+// Returns hipErrorInvalidValue if no instantiation fits (nz, m).
+hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
+                       hipStream_t s) {
+    if (a.num_agents <= 0) return hipSuccess;
+    // variant 0: 16 lanes x 4 slots; 1: 64 lanes x 1 slot; 2: 64 lanes x 4 slots (wide)
+    if (op.nz == 6) {
+        if (variant == 0 && op.m < 64) return launch_impc_t<6, 16, 4>(op, buf, a, s);
+        if (variant == 1 && op.m < 64) return launch_impc_t<6, 64, 1>(op, buf, a, s);
+        if (op.m < 256) return launch_impc_t<6, 64, 4>(op, buf, a, s);
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace mpccbf

@@ -1,0 +1,12 @@
+"""Python host binding of libmpccbf.so (include/mpccbf.h) — the MI355X batched MPC-CBF solver.
+
+The product is the C ABI + HIP kernels; this module only marshals torch device tensors (device
+memory, streams) into it. There is no CPU fallback: without the built library, or without a
+GPU, every solve raises.
+"""
+from ._lib import (  # noqa: F401
+    LIB_PATH, MpccbfError, Params, Options, Context, status_name, build_library, load,
+    dense_qp_solve, STATUS_NAMES, OPTIMAL, FEASIBLE, UNBOUNDED, INFEASIBLE, ERROR, UNKNOWN,
+    INFEASIBLEORUNBOUNDED,
+)
+from . import swarm  # noqa: F401

@@ -1,0 +1,258 @@
+"""ctypes marshalling for libmpccbf.so. Mirrors include/mpccbf.h one to one."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # mpc-cbf_amd/
+LIB_PATH = os.path.join(PKG_DIR, "build", "libmpccbf.so")
+
+OPTIMAL, FEASIBLE, UNBOUNDED, INFEASIBLE, ERROR, UNKNOWN, INFEASIBLEORUNBOUNDED = range(7)
+STATUS_NAMES = ["OPTIMAL", "FEASIBLE", "UNBOUNDED", "INFEASIBLE", "ERROR", "UNKNOWN",
+                "INFEASIBLEORUNBOUNDED"]
+
+# every symbol include/mpccbf.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED = [
+    "mpccbf_create", "mpccbf_destroy", "mpccbf_num_vars", "mpccbf_reduced_dim",
+    "mpccbf_num_shared_rows", "mpccbf_impc_solve", "mpccbf_set_variant", "mpccbf_build_neighbors",
+    "mpccbf_qp_solve_dense", "mpccbf_qp_solve_dense_batch", "mpccbf_last_error",
+    "mpccbf_status_string", "mpccbf_abi_version",
+]
+
+
+class MpccbfError(RuntimeError):
+    pass
+
+
+def status_name(s: int) -> str:
+    return STATUS_NAMES[s] if 0 <= s < len(STATUS_NAMES) else str(s)
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("h", C.c_double), ("Ts", C.c_double), ("k_hor", C.c_int32),
+        ("w_pos_err", C.c_double), ("w_u_eff", C.c_double), ("spd_f", C.c_int32),
+        ("v_min", C.c_double * 3), ("v_max", C.c_double * 3),
+        ("a_min", C.c_double * 3), ("a_max", C.c_double * 3),
+        ("d_min", C.c_double),
+        ("cbf_horizon", C.c_int32), ("impc_iter", C.c_int32), ("slack_mode", C.c_int32),
+        ("slack_cost", C.c_double), ("slack_decay_rate", C.c_double),
+        ("num_pieces", C.c_int32), ("num_control_points", C.c_int32),
+        ("piece_max_parameter", C.c_double), ("continuity_upto_degree", C.c_int32),
+    ]
+
+    @classmethod
+    def from_dict(cls, cfg: dict) -> "Params":
+        p = cls()
+        for k, v in cfg.items():
+            if isinstance(v, (list, tuple)):
+                arr = getattr(p, k)
+                for i, x in enumerate(v):
+                    arr[i] = x
+            else:
+                setattr(p, k, v)
+        return p
+
+
+class Options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("keep_redundant", C.c_int32),
+                ("no_cbf_filter", C.c_int32), ("max_pdip_iters", C.c_int32),
+                ("tolerance", C.c_double)]
+
+
+class Batch(C.Structure):
+    _fields_ = [
+        ("num_states", C.c_int32), ("states", C.c_void_p), ("agent_first", C.c_int32),
+        ("num_agents", C.c_int32), ("targets", C.c_void_p), ("refs", C.c_void_p),
+        ("nb_row_ptr", C.c_void_p), ("nb_col", C.c_void_p), ("x", C.c_void_p),
+        ("status", C.c_void_p), ("obj", C.c_void_p), ("iters", C.c_void_p),
+        ("next_states", C.c_void_p),
+    ]
+
+
+class DenseQP(C.Structure):
+    _fields_ = [("n", C.c_int32), ("m", C.c_int32), ("H", C.c_void_p), ("c", C.c_void_p),
+                ("c0", C.c_double), ("A", C.c_void_p), ("lo", C.c_void_p), ("hi", C.c_void_p),
+                ("vlo", C.c_void_p), ("vhi", C.c_void_p)]
+
+
+def build_library(quiet: bool = True) -> str:
+    """Compile libmpccbf.so for gfx950 with hipcc (works without a GPU)."""
+    out = subprocess.run(["make", "-C", PKG_DIR, "-j8"], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise MpccbfError("libmpccbf build failed:\n" + out.stdout[-4000:] + out.stderr[-4000:])
+    return LIB_PATH
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpccbfError(f"{LIB_PATH} not built: run `make -C mpc-cbf_amd` (no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    vp = C.c_void_p
+    L.mpccbf_create.argtypes = [C.POINTER(Params), C.POINTER(Options), C.POINTER(vp)]
+    L.mpccbf_destroy.argtypes = [vp]
+    L.mpccbf_destroy.restype = None
+    for f in ("mpccbf_num_vars", "mpccbf_reduced_dim", "mpccbf_num_shared_rows"):
+        getattr(L, f).argtypes = [vp]
+    L.mpccbf_impc_solve.argtypes = [vp, C.POINTER(Batch), vp]
+    L.mpccbf_set_variant.argtypes = [vp, C.c_int]
+    L.mpccbf_build_neighbors.argtypes = [vp, vp, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                         C.c_double, vp, vp, vp]
+    L.mpccbf_qp_solve_dense.argtypes = [C.POINTER(DenseQP), vp, vp, vp]
+    L.mpccbf_qp_solve_dense_batch.argtypes = [C.c_int32, C.POINTER(DenseQP), vp, vp, vp]
+    L.mpccbf_last_error.restype = C.c_char_p
+    L.mpccbf_status_string.restype = C.c_char_p
+    L.mpccbf_status_string.argtypes = [C.c_int32]
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load().mpccbf_last_error().decode()
+        raise MpccbfError(f"mpccbf error {rc}: {msg}")
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    import torch  # noqa: F401  (device tensors only)
+    if not t.is_cuda:
+        raise MpccbfError("libmpccbf batch entry points take device tensors")
+    if not t.is_contiguous():
+        raise MpccbfError("tensor must be contiguous")
+    return t.data_ptr()
+
+
+def _stream(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+class Context:
+    """One controller configuration on one device (mpccbf_create / mpccbf_destroy)."""
+
+    def __init__(self, cfg: dict, device: int = 0, keep_redundant: bool = False,
+                 no_cbf_filter: bool = False, max_iters: int = 0, tol: float = 0.0):
+        L = load()
+        self.cfg = dict(cfg)
+        self.params = Params.from_dict(cfg)
+        o = Options(device=device, keep_redundant=int(keep_redundant),
+                    no_cbf_filter=int(no_cbf_filter), max_pdip_iters=max_iters, tolerance=tol)
+        h = C.c_void_p()
+        _check(L.mpccbf_create(C.byref(self.params), C.byref(o), C.byref(h)))
+        self._h = h
+        self.n = L.mpccbf_num_vars(h)
+        self.nz = L.mpccbf_reduced_dim(h)
+        self.shared_rows = L.mpccbf_num_shared_rows(h)
+        self.impc_iter = int(cfg["impc_iter"])
+        self.k_hor = int(cfg["k_hor"])
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().mpccbf_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_variant(self, v: int):
+        _check(load().mpccbf_set_variant(self._h, v))
+
+    def build_neighbors(self, states, first, count, k, radius, row_ptr, col, stream=None):
+        _check(load().mpccbf_build_neighbors(self._h, _ptr(states), states.shape[0], first, count,
+                                             k, float(radius), _ptr(row_ptr), _ptr(col),
+                                             _stream(stream)))
+
+    def impc_solve(self, states, nb_row_ptr, nb_col, targets=None, refs=None, agent_first=0,
+                   num_agents=None, x=None, status=None, obj=None, iters=None, next_states=None,
+                   stream=None):
+        if num_agents is None:
+            num_agents = states.shape[0] - agent_first
+        b = Batch(num_states=states.shape[0], states=_ptr(states), agent_first=agent_first,
+                  num_agents=num_agents, targets=_ptr(targets), refs=_ptr(refs),
+                  nb_row_ptr=_ptr(nb_row_ptr), nb_col=_ptr(nb_col), x=_ptr(x),
+                  status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters),
+                  next_states=_ptr(next_states))
+        _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
+
+    def alloc_outputs(self, num_agents: int, device=None):
+        import torch
+        dev = device or torch.device("cuda", self.device)
+        return dict(
+            x=torch.empty((num_agents, self.n), dtype=torch.float64, device=dev),
+            status=torch.empty((num_agents, self.impc_iter), dtype=torch.int32, device=dev),
+            obj=torch.empty((num_agents, self.impc_iter), dtype=torch.float64, device=dev),
+            iters=torch.empty((num_agents, self.impc_iter), dtype=torch.int32, device=dev),
+            next_states=torch.empty((num_agents, 6), dtype=torch.float64, device=dev),
+        )
+
+
+class HostOps(C.Structure):
+    _fields_ = [("n", C.c_int32), ("nz", C.c_int32), ("m", C.c_int32), ("mc", C.c_int32),
+                ("rows_total", C.c_int32), ("rows_removed", C.c_int32),
+                ("capacity_ok", C.c_int32)] + [
+        (f, C.c_void_p) for f in ("H", "Z", "Xs", "Pr", "Qs", "Qt", "Ks", "Kt", "G", "Gs", "lo",
+                                  "hi", "Cs", "clo", "chi", "UZ0", "US0")]
+
+
+def host_operators(cfg: dict, keep_redundant: bool = False) -> dict:
+    """Host-only condensed operators (mpccbf_host_operators); no GPU needed."""
+    L = load()
+    L.mpccbf_host_operators.argtypes = [C.POINTER(Params), C.c_int32, C.POINTER(HostOps)]
+    L.mpccbf_host_last_error.restype = C.c_char_p
+    p = Params.from_dict(cfg)
+    o = HostOps(capacity_ok=0)
+    rc = L.mpccbf_host_operators(C.byref(p), int(keep_redundant), C.byref(o))
+    if rc != 0:
+        raise MpccbfError(L.mpccbf_host_last_error().decode())
+    n, nz, m, mc = o.n, o.nz, o.m, o.mc
+    shapes = dict(H=(n, n), Z=(n, nz), Xs=(n, 6), Pr=(nz, nz), Qs=(nz, 6), Qt=(nz, 3),
+                  Ks=(6, 6), Kt=(3, 6), G=(m, nz), Gs=(m, 6), lo=(m,), hi=(m,), Cs=(mc, 6),
+                  clo=(mc,), chi=(mc,), UZ0=(3, nz), US0=(3, 6))
+    arrs = {k: np.zeros(s) for k, s in shapes.items()}
+    o.capacity_ok = 1
+    for k, a in arrs.items():
+        setattr(o, k, a.ctypes.data if a.size else None)
+    rc = L.mpccbf_host_operators(C.byref(p), int(keep_redundant), C.byref(o))
+    if rc != 0:
+        raise MpccbfError(L.mpccbf_host_last_error().decode())
+    arrs.update(n=n, nz=nz, m=m, mc=mc, rows_total=o.rows_total, rows_removed=o.rows_removed)
+    return arrs
+
+
+def dense_qp_solve(H, c, A, lo, hi, vlo=None, vhi=None, c0=0.0):
+    """Generic dense QP (mpccbf_qp_solve_dense); host numpy arrays. Returns (status, x, obj)."""
+    L = load()
+    H = np.ascontiguousarray(H, dtype=np.float64)
+    c = np.ascontiguousarray(c, dtype=np.float64)
+    n = c.shape[0]
+    A = np.ascontiguousarray(A, dtype=np.float64).reshape(-1, n)
+    lo = np.ascontiguousarray(lo, dtype=np.float64)
+    hi = np.ascontiguousarray(hi, dtype=np.float64)
+    vlo_a = None if vlo is None else np.ascontiguousarray(vlo, dtype=np.float64)
+    vhi_a = None if vhi is None else np.ascontiguousarray(vhi, dtype=np.float64)
+    qp = DenseQP(n=n, m=A.shape[0], H=H.ctypes.data, c=c.ctypes.data, c0=c0, A=A.ctypes.data,
+                 lo=lo.ctypes.data, hi=hi.ctypes.data,
+                 vlo=None if vlo_a is None else vlo_a.ctypes.data,
+                 vhi=None if vhi_a is None else vhi_a.ctypes.data)
+    x = np.zeros(n)
+    obj = np.zeros(1)
+    st = np.zeros(1, dtype=np.int32)
+    _check(L.mpccbf_qp_solve_dense(C.byref(qp), x.ctypes.data, obj.ctypes.data, st.ctypes.data))
+    return int(st[0]), x, float(obj[0])

@@ -1,0 +1,117 @@
+/*
+ * oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference (ywang760/mpc-cbf @ 2025-08-29) hot path:
+ * assembly of the per-agent MPC-CBF QP (workspace/lib/{model,splines,mpc,cbf,mpc_cbf})
+ * and an independent full-space dense QP solver standing in for CPLEXSolver::solve
+ * (workspace/lib/qpcpp/src/solvers/CPLEX.cpp:35-177), which cannot run here (CPLEX 22.1.1 is
+ * proprietary and absent, as are Eigen3 and GiNaC; see DESIGN.md "Oracle").
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this library,
+ * and only as the checker / the CPU baseline. The product (mpc-cbf_amd/) never links it.
+ *
+ * Pinning: the restatement is checked against every known-answer test the reference holds for
+ * this path (tests/golden/reference_kats.json: TestInitSafetyCBF.cpp:50-143, CPLEXTest.cpp:28-56,
+ * DoubleIntegratorXYYawTest.cpp:19-47, CombinatoricsTest.cpp) and, for whole QPs (which no
+ * reference test pins), by KKT certificates plus an independent numpy restatement
+ * (tests/golden/make_golden.py).
+ */
+#ifndef MPCCBF_ORACLE_H
+#define MPCCBF_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Parameters: same meaning as experiments/config/base_config.json parsed by
+ * common/include/common/parsing.hpp:20-135. DIM is fixed to 3 (x, y, yaw) as in
+ * mpc_cbf (only <double, 3U> is instantiated, MPCCBFQPOperationsBase.cpp:35). */
+typedef struct orc_params {
+    double h, Ts;
+    int32_t k_hor;
+    double w_pos_err, w_u_eff;
+    int32_t spd_f;
+    double v_min[3], v_max[3], a_min[3], a_max[3];
+    double d_min;
+    int32_t cbf_horizon, impc_iter, slack_mode;
+    double slack_cost, slack_decay_rate;
+    int32_t num_pieces, num_control_points;
+    double piece_max_parameter;
+    int32_t continuity_upto_degree;
+} orc_params;
+
+/* Status codes: index of qpcpp::SolveStatus (qpcpp/include/qpcpp/solvers/Solver.h:13-21). */
+enum { ORC_OPTIMAL = 0, ORC_FEASIBLE = 1, ORC_UNBOUNDED = 2, ORC_INFEASIBLE = 3, ORC_ERROR = 4,
+       ORC_UNKNOWN = 5, ORC_INFEASIBLEORUNBOUNDED = 6 };
+
+/* --- known-answer surface (for pinning against the reference's own tests) --- */
+uint64_t orc_fac(uint64_t n);
+uint64_t orc_comb(uint64_t n, uint64_t k);
+uint64_t orc_perm(uint64_t n, uint64_t k);
+/* bernsteinBasis (splines/src/detail/BezierOperations.cpp:11-50); returns 0 ok, -1 out of range */
+int orc_bernstein_basis(uint64_t degree, double max_parameter, double parameter, uint64_t deriv,
+                        double* out /* degree+1 */);
+int orc_bernstein_coefficient_matrix(uint64_t degree, double max_parameter, uint64_t deriv,
+                                     double* out /* (degree+1)^2 row-major */);
+/* ConnectivityCBF safety row, closed form of ConnectivityCBF.cpp:152-198 (gamma 5, cubic alpha) */
+void orc_safety_cbf(const double* state6, const double* neighbor6, double d_min, double* a3,
+                    double* b);
+/* DoubleIntegratorXYYaw(ts).applyInput (model/src/DoubleIntegrator.cpp:54-63) */
+void orc_apply_input(double ts, const double* state6, const double* u3, double* out6);
+/* get_A0(K).pos_ (3K x 6) and get_lambda(K).pos_ (3K x 3K) (DoubleIntegrator.cpp:9-51) */
+void orc_prediction_matrices(double ts, int32_t K, double* A0pos, double* Lpos);
+
+/* --- QP sizes for a parameter set --- */
+int orc_num_vars(const orc_params* p, int32_t num_neighbors); /* curve vars (+ slack vars) */
+
+/* --- assembly of one QP (one IMPC iteration) into the dense "flattened CPLEX" form ---
+ * objective  x^T H x + c^T x + c0  (CPLEX.cpp:122-147: sum_{i<=j} q_ij x_i x_j, H symmetric)
+ * rows       lo_r <= A_r x <= hi_r  (+-1e308 mean +-inf: numeric_limits lowest()/max())
+ * var bounds vlo_i <= x_i <= vhi_i
+ * iter == 0: CBF rows at the current ego state; iter > 0: CBF rows at pred_states (cbf_horizon x 6)
+ * Returns number of rows, or -1 if capacity (max_rows) is too small. */
+int orc_assemble_qp(const orc_params* p, const double* state6, const double* ref /* 3K */,
+                    int32_t num_neighbors, const double* neighbors /* nb x 6 */,
+                    const double* slack_weights /* nb, or NULL */, int32_t iter,
+                    const double* pred_states /* cbf_horizon x 6 */, int32_t max_rows,
+                    double* H /* n x n */, double* c /* n */, double* c0, double* A /* rows x n */,
+                    double* lo, double* hi, double* vlo, double* vhi);
+
+/* --- dense QP solve (stands in for CPLEXSolver<double>::solve) ---
+ * kkt_out[0..3] = stationarity, primal infeasibility, dual infeasibility, complementarity
+ * (all inf-norms; dual infeasibility = max(-z)). Returns status. */
+int orc_solve_dense_qp(int32_t n, const double* H, const double* c, double c0, int32_t m,
+                       const double* A, const double* lo, const double* hi, const double* vlo,
+                       const double* vhi, double* x_out, double* obj_out, int32_t* iters_out,
+                       double* kkt_out);
+
+/* --- one agent's ConnectivityIMPCCBF::optimize (mpc_cbf/src/controller/ConnectivityIMPCCBF.cpp:47-215)
+ * states: all agents (N x 6); neighbors of self are given explicitly (indices into states)
+ * (the reference passes all N-1 others; pass them all for reference semantics).
+ * ref: 3K reference positions of this agent.
+ * Outputs per IMPC iteration it (< impc_iter): status[it], obj[it], x[it*n ..] (n = orc_num_vars).
+ * Returns number of iterations attempted; success = (status[last attempted] == OPTIMAL). */
+int orc_impc_optimize(const orc_params* p, int32_t num_agents, const double* states,
+                      int32_t self_idx, int32_t num_neighbors, const int32_t* neighbor_idx,
+                      const double* ref, int32_t* status, double* obj, double* x,
+                      int32_t* qp_iters);
+
+/* Batched CPU baseline: agents [first, first+count) with neighbor CSR (row_ptr, col).
+ * nthreads worker threads, one agent per task (CPLEX Threads=1 per solve, CPLEX.cpp:158).
+ * x_last: n per agent (solution of the last OPTIMAL iteration). Returns total QPs solved. */
+int64_t orc_impc_batch(const orc_params* p, int32_t num_agents, const double* states,
+                       const double* refs /* N x 3K */, const int32_t* nb_row_ptr,
+                       const int32_t* nb_col, int32_t first, int32_t count, int32_t nthreads,
+                       int32_t* status /* count x impc_iter */, double* obj /* count x impc_iter */,
+                       double* x_last /* count x n_curve */);
+
+/* Curve evaluation of a solution vector (SingleParameterPiecewiseCurve::eval,
+ * splines/src/curves/SingleParameterPiecewiseCurve.cpp:94-127): out3 = d-th derivative at t. */
+int orc_eval_curve(const orc_params* p, const double* x, double t, int32_t deriv, double* out3);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

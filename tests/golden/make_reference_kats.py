@@ -1,0 +1,71 @@
+"""Writes reference_kats.json: the known-answer vectors the reference's own tests hold for the
+hot path, transcribed as data (inputs + expected outputs, with the tolerance each test uses).
+
+Sources (paths under workspace/lib of ywang760/mpc-cbf @ 2025-08-29):
+  cbf/tests/TestInitSafetyCBF.cpp:50-143   collision (safety) CBF Ac/Bc, d_min 0.8, gamma 5
+  qpcpp/tests/CPLEXTest.cpp:28-56          min x^2 + y^2 s.t. x + y >= 1 -> x = y = 0.5
+  model/tests/DoubleIntegratorXYYawTest.cpp:19-47  applyInput with ts = 0.1
+  math/tests/CombinatoricsTest.cpp:17-63   fac / comb / perm
+Run:  python tests/golden/make_reference_kats.py
+"""
+import json
+import os
+
+KATS = {
+    "safety_cbf": {
+        "source": "cbf/tests/TestInitSafetyCBF.cpp:50-143",
+        "d_min": 0.8,
+        "tolerance_Bc": 1e-6,
+        "cases": [
+            {"name": "TwoRobotInSafeRegion", "state": [0, 0, 0, 0, 0, 0],
+             "neighbor": [1, 0, 0, 0, 0, 0], "Ac": [-2.0, 0.0, 0.0],
+             "Bc": 0.06347497291775989, "sign": ">0"},
+            {"name": "TwoRobotInSafeRegionWithHugeVelocity", "state": [0, 0, 0, 100, 100, 0],
+             "neighbor": [1, 0, 0, 0, 0, 0], "Ac": [-2.0, 0.0, 0.0],
+             "Bc": -39820583.995200224, "sign": "<0"},
+            {"name": "TwoRobotOnSafetyBound", "state": [0, 0, 0, 0, 0, 0],
+             "neighbor": [0.8, 0, 0, 0, 0, 0], "Ac": [-1.6, 0.0, 0.0], "Bc": 0.0, "sign": "==0"},
+            {"name": "TwoRobotInUnsafeRegion", "state": [0, 0, 0, 0, 0, 0],
+             "neighbor": [0.5, 0, 0, 0, 0, 0], "Ac": [-1.0, 0.0, 0.0],
+             "Bc": -0.13045522572422458, "sign": "<0"},
+        ],
+    },
+    "cplex_toy_qp": {
+        "source": "qpcpp/tests/CPLEXTest.cpp:28-56",
+        "objective": "x^2 + y^2 (addQuadraticTerm(x,x,1), (y,y,1))",
+        "H": [[1.0, 0.0], [0.0, 1.0]], "c": [0.0, 0.0],
+        "A": [[1.0, 1.0]], "lo": [1.0], "hi": ["inf"],
+        "status": "OPTIMAL", "x": [0.5, 0.5], "tolerance": 1e-6,
+    },
+    "xyyaw_apply_input": {
+        "source": "model/tests/DoubleIntegratorXYYawTest.cpp:19-47",
+        "ts": 0.1, "state": [1.0, 2.0, 0.5, 0.1, 0.2, 0.3], "u": [0.5, 0.6, 0.1],
+        "expected": [1.0 + 0.1 * 0.1 + 0.5 * 0.5 * 0.01, 2.0 + 0.2 * 0.1 + 0.5 * 0.6 * 0.01,
+                     0.5 + 0.3 * 0.1 + 0.5 * 0.1 * 0.01, 0.1 + 0.5 * 0.1, 0.2 + 0.6 * 0.1,
+                     0.3 + 0.1 * 0.1],
+        "tolerance": 1e-10,
+        "prediction_shapes": {"horizon": 10, "A0_pos": [30, 6], "Lambda_pos": [30, 30]},
+    },
+}
+
+
+def combinatorics_cases():
+    """CombinatoricsTest.cpp:17-63, transcribed (fac(21) must throw; k > n gives 0)."""
+    return {
+        "source": "math/tests/CombinatoricsTest.cpp:17-63",
+        "fac": [[0, 1], [1, 1], [2, 2], [3, 6], [4, 24], [5, 120], [10, 3628800],
+                [20, 2432902008176640000]],
+        "fac_throws": [21],
+        "comb": [[5, 0, 1], [5, 1, 5], [5, 2, 10], [5, 3, 10], [5, 4, 5], [5, 5, 1], [0, 0, 1],
+                 [10, 0, 1], [10, 10, 1], [5, 6, 0], [20, 10, 184756]],
+        "perm": [[5, 0, 1], [5, 1, 5], [5, 2, 20], [5, 3, 60], [5, 4, 120], [5, 5, 120],
+                 [0, 0, 1], [10, 0, 1], [5, 6, 0], [10, 3, 720]],
+    }
+
+
+if __name__ == "__main__":
+    KATS["combinatorics"] = combinatorics_cases()
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_kats.json")
+    with open(out, "w") as f:
+        json.dump(KATS, f, indent=1)
+    print("wrote", out)

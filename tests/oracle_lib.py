@@ -1,0 +1,224 @@
+"""ctypes binding of oracle/build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The oracle is the CPU restatement of the reference hot path (see oracle/oracle.h). Only tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+OPTIMAL, FEASIBLE, UNBOUNDED, INFEASIBLE, ERROR, UNKNOWN, INFEASIBLEORUNBOUNDED = range(7)
+STATUS_NAMES = ["OPTIMAL", "FEASIBLE", "UNBOUNDED", "INFEASIBLE", "ERROR", "UNKNOWN",
+                "INFEASIBLEORUNBOUNDED"]
+
+
+class OrcParams(C.Structure):
+    _fields_ = [
+        ("h", C.c_double), ("Ts", C.c_double), ("k_hor", C.c_int32),
+        ("w_pos_err", C.c_double), ("w_u_eff", C.c_double), ("spd_f", C.c_int32),
+        ("v_min", C.c_double * 3), ("v_max", C.c_double * 3),
+        ("a_min", C.c_double * 3), ("a_max", C.c_double * 3),
+        ("d_min", C.c_double),
+        ("cbf_horizon", C.c_int32), ("impc_iter", C.c_int32), ("slack_mode", C.c_int32),
+        ("slack_cost", C.c_double), ("slack_decay_rate", C.c_double),
+        ("num_pieces", C.c_int32), ("num_control_points", C.c_int32),
+        ("piece_max_parameter", C.c_double), ("continuity_upto_degree", C.c_int32),
+    ]
+
+
+def make_params(cfg: dict) -> OrcParams:
+    p = OrcParams()
+    for k, v in cfg.items():
+        if isinstance(v, (list, tuple)):
+            arr = getattr(p, k)
+            for i, x in enumerate(v):
+                arr[i] = x
+        else:
+            setattr(p, k, v)
+    return p
+
+
+def build(quiet: bool = True) -> str:
+    """Compile the oracle (plain g++)."""
+    out = subprocess.run(["make", "-C", ORACLE_DIR], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+    return ORACLE_SO
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            build()
+        L = C.CDLL(ORACLE_SO)
+        dp = C.POINTER(C.c_double)
+        ip = C.POINTER(C.c_int32)
+        L.orc_fac.restype = C.c_uint64
+        L.orc_fac.argtypes = [C.c_uint64]
+        L.orc_comb.restype = C.c_uint64
+        L.orc_comb.argtypes = [C.c_uint64, C.c_uint64]
+        L.orc_perm.restype = C.c_uint64
+        L.orc_perm.argtypes = [C.c_uint64, C.c_uint64]
+        L.orc_bernstein_basis.argtypes = [C.c_uint64, C.c_double, C.c_double, C.c_uint64, dp]
+        L.orc_bernstein_coefficient_matrix.argtypes = [C.c_uint64, C.c_double, C.c_uint64, dp]
+        L.orc_safety_cbf.argtypes = [dp, dp, C.c_double, dp, dp]
+        L.orc_apply_input.argtypes = [C.c_double, dp, dp, dp]
+        L.orc_prediction_matrices.argtypes = [C.c_double, C.c_int32, dp, dp]
+        L.orc_num_vars.argtypes = [C.POINTER(OrcParams), C.c_int32]
+        L.orc_assemble_qp.argtypes = [C.POINTER(OrcParams), dp, dp, C.c_int32, dp, dp, C.c_int32,
+                                      dp, C.c_int32, dp, dp, dp, dp, dp, dp, dp, dp]
+        L.orc_solve_dense_qp.argtypes = [C.c_int32, dp, dp, C.c_double, C.c_int32, dp, dp, dp, dp,
+                                         dp, dp, dp, ip, dp]
+        L.orc_impc_optimize.argtypes = [C.POINTER(OrcParams), C.c_int32, dp, C.c_int32, C.c_int32,
+                                        ip, dp, ip, dp, dp, ip]
+        L.orc_impc_batch.restype = C.c_int64
+        L.orc_impc_batch.argtypes = [C.POINTER(OrcParams), C.c_int32, dp, dp, ip, ip, C.c_int32,
+                                     C.c_int32, C.c_int32, ip, dp, dp]
+        L.orc_eval_curve.argtypes = [C.POINTER(OrcParams), dp, C.c_double, C.c_int32, dp]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return np.ascontiguousarray(a, dtype=np.float64).ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _i(a):
+    return np.ascontiguousarray(a, dtype=np.int32).ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def bernstein_basis(deg, T, t, d):
+    out = np.zeros(deg + 1)
+    rc = lib().orc_bernstein_basis(deg, T, t, d, _d(out))
+    if rc != 0:
+        raise ValueError("parameter out of range")
+    return out
+
+
+def safety_cbf(state, nb, d_min):
+    a = np.zeros(3)
+    b = np.zeros(1)
+    st = np.ascontiguousarray(state, dtype=np.float64)
+    nbv = np.ascontiguousarray(nb, dtype=np.float64)
+    lib().orc_safety_cbf(_d(st), _d(nbv), d_min, _d(a), _d(b))
+    return a, float(b[0])
+
+
+def apply_input(ts, state, u):
+    out = np.zeros(6)
+    st = np.ascontiguousarray(state, dtype=np.float64)
+    uu = np.ascontiguousarray(u, dtype=np.float64)
+    lib().orc_apply_input(ts, _d(st), _d(uu), _d(out))
+    return out
+
+
+def prediction_matrices(ts, K):
+    A0 = np.zeros((3 * K, 6))
+    Lm = np.zeros((3 * K, 3 * K))
+    lib().orc_prediction_matrices(ts, K, _d(A0), _d(Lm))
+    return A0, Lm
+
+
+def assemble_qp(p: OrcParams, state, ref, neighbors, it=0, pred=None, slack_w=None,
+                max_rows=4096):
+    nb = 0 if neighbors is None else len(neighbors)
+    n = lib().orc_num_vars(C.byref(p), nb)
+    H = np.zeros((n, n))
+    c = np.zeros(n)
+    c0 = np.zeros(1)
+    A = np.zeros((max_rows, n))
+    lo = np.zeros(max_rows)
+    hi = np.zeros(max_rows)
+    vlo = np.zeros(n)
+    vhi = np.zeros(n)
+    nbs = np.ascontiguousarray(neighbors if nb else np.zeros((1, 6)), dtype=np.float64)
+    pr = np.ascontiguousarray(pred if pred is not None else np.zeros((max(1, p.cbf_horizon), 6)),
+                              dtype=np.float64)
+    st = np.ascontiguousarray(state, dtype=np.float64)
+    rf = np.ascontiguousarray(ref, dtype=np.float64)
+    sw = None if slack_w is None else np.ascontiguousarray(slack_w, dtype=np.float64)
+    m = lib().orc_assemble_qp(C.byref(p), _d(st), _d(rf), nb, _d(nbs),
+                              None if sw is None else _d(sw), it, _d(pr), max_rows, _d(H), _d(c),
+                              _d(c0), _d(A), _d(lo), _d(hi), _d(vlo), _d(vhi))
+    if m < 0:
+        raise RuntimeError(f"assemble failed: {m}")
+    return dict(n=n, H=H, c=c, c0=float(c0[0]), A=A[:m].copy(), lo=lo[:m].copy(),
+                hi=hi[:m].copy(), vlo=vlo, vhi=vhi)
+
+
+def solve_dense_qp(qp):
+    n = qp["n"]
+    m = len(qp["lo"])
+    x = np.zeros(n)
+    obj = np.zeros(1)
+    iters = np.zeros(1, dtype=np.int32)
+    kkt = np.zeros(4)
+    H = np.ascontiguousarray(qp["H"], dtype=np.float64)
+    c = np.ascontiguousarray(qp["c"], dtype=np.float64)
+    A = np.ascontiguousarray(qp["A"], dtype=np.float64).reshape(m, n) if m else np.zeros((1, n))
+    lo = np.ascontiguousarray(qp["lo"] if m else np.zeros(1), dtype=np.float64)
+    hi = np.ascontiguousarray(qp["hi"] if m else np.zeros(1), dtype=np.float64)
+    vlo = np.ascontiguousarray(qp["vlo"], dtype=np.float64)
+    vhi = np.ascontiguousarray(qp["vhi"], dtype=np.float64)
+    st = lib().orc_solve_dense_qp(n, _d(H), _d(c), qp.get("c0", 0.0), m, _d(A), _d(lo), _d(hi),
+                                  _d(vlo), _d(vhi), _d(x), _d(obj),
+                                  iters.ctypes.data_as(C.POINTER(C.c_int32)), _d(kkt))
+    return dict(status=st, x=x, obj=float(obj[0]), iters=int(iters[0]), kkt=kkt)
+
+
+def impc_optimize(p: OrcParams, states, self_idx, neighbor_idx, ref):
+    states = np.ascontiguousarray(states, dtype=np.float64)
+    nbi = np.ascontiguousarray(neighbor_idx, dtype=np.int32)
+    nb = len(nbi)
+    n = lib().orc_num_vars(C.byref(p), nb)
+    it_n = p.impc_iter
+    status = np.full(it_n, UNKNOWN, dtype=np.int32)
+    obj = np.full(it_n, np.nan)
+    x = np.zeros((it_n, n))
+    qi = np.zeros(it_n, dtype=np.int32)
+    rf = np.ascontiguousarray(ref, dtype=np.float64)
+    att = lib().orc_impc_optimize(C.byref(p), len(states), _d(states), self_idx, nb,
+                                  nbi.ctypes.data_as(C.POINTER(C.c_int32)) if nb else None,
+                                  _d(rf), status.ctypes.data_as(C.POINTER(C.c_int32)), _d(obj),
+                                  _d(x), qi.ctypes.data_as(C.POINTER(C.c_int32)))
+    if att < 0:
+        raise RuntimeError("orc_impc_optimize failed")
+    return dict(attempted=att, status=status, obj=obj, x=x, qp_iters=qi)
+
+
+def impc_batch(p: OrcParams, states, refs, row_ptr, col, first, count, nthreads=1):
+    states = np.ascontiguousarray(states, dtype=np.float64)
+    refs = np.ascontiguousarray(refs, dtype=np.float64)
+    rp = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    cl = np.ascontiguousarray(col if len(col) else np.zeros(1), dtype=np.int32)
+    it_n = p.impc_iter
+    status = np.full((count, it_n), UNKNOWN, dtype=np.int32)
+    obj = np.full((count, it_n), np.nan)
+    nc = p.num_pieces * 3 * p.num_control_points
+    xl = np.zeros((count, nc))
+    solved = lib().orc_impc_batch(C.byref(p), len(states), _d(states), _d(refs),
+                                  rp.ctypes.data_as(C.POINTER(C.c_int32)),
+                                  cl.ctypes.data_as(C.POINTER(C.c_int32)), first, count, nthreads,
+                                  status.ctypes.data_as(C.POINTER(C.c_int32)), _d(obj), _d(xl))
+    return dict(solved=int(solved), status=status, obj=obj, x_last=xl)
+
+
+def eval_curve(p: OrcParams, x, t, d):
+    out = np.zeros(3)
+    xx = np.ascontiguousarray(x, dtype=np.float64)
+    rc = lib().orc_eval_curve(C.byref(p), _d(xx), t, d, _d(out))
+    if rc != 0:
+        raise ValueError("eval out of range")
+    return out

@@ -1,0 +1,153 @@
+"""GPU parity: libmpccbf (HIP, gfx950) against the CPU oracle on identical seeded inputs.
+
+Parity rule: status must match; for OPTIMAL QPs
+|obj_gpu - obj_ref| <= 1e-4 * max(1, |obj_ref|) (north-star tolerance), and we additionally
+hold the control points to 1e-5 (inf-norm) to catch a wrong-but-close optimum.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from mpccbf import swarm
+
+pytestmark = pytest.mark.gpu
+
+OBJ_TOL = 1e-4
+X_TOL = 1e-5
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a visible MI355X")
+    return torch
+
+
+def run_gpu(ctx, states, targets, row_ptr, col, torch):
+    dev = torch.device("cuda", 0)
+    st = torch.tensor(states, dtype=torch.float64, device=dev)
+    tg = torch.tensor(targets, dtype=torch.float64, device=dev)
+    rp = torch.tensor(row_ptr, dtype=torch.int32, device=dev)
+    cl = torch.tensor(col if len(col) else np.zeros(1, np.int32), dtype=torch.int32, device=dev)
+    out = ctx.alloc_outputs(len(states))
+    ctx.impc_solve(st, rp, cl, targets=tg, **out)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+def run_oracle(cfg, states, targets, row_ptr, col, agents):
+    p = O.make_params(cfg)
+    refs = swarm.refs_from_targets(targets, cfg["k_hor"])
+    res = []
+    for a in agents:
+        res.append(O.impc_optimize(p, states, a, col[row_ptr[a]:row_ptr[a + 1]], refs[a]))
+    return res
+
+
+def compare(cfg, g, ref, agents):
+    n = g["x"].shape[1]
+    worst = 0.0
+    for i, a in enumerate(agents):
+        r = ref[i]
+        assert list(g["status"][a]) == list(r["status"]), (a, g["status"][a], r["status"])
+        for it in range(cfg["impc_iter"]):
+            if r["status"][it] == O.OPTIMAL:
+                ro = r["obj"][it]
+                err = abs(g["obj"][a, it] - ro) / max(1.0, abs(ro))
+                worst = max(worst, err)
+                assert err <= OBJ_TOL, (a, it, g["obj"][a, it], ro)
+        last = [it for it in range(cfg["impc_iter"]) if r["status"][it] == O.OPTIMAL]
+        if last:
+            xr = r["x"][last[-1]][:n]
+            assert np.max(np.abs(g["x"][a] - xr)) <= X_TOL, (a, np.max(np.abs(g["x"][a] - xr)))
+    return worst
+
+
+@pytest.mark.parametrize("k_hor,n_agents", [(10, 256), (15, 64)])
+def test_impc_knn_matches_oracle(mpclib, k_hor, n_agents):
+    torch = _torch()
+    cfg = swarm.config(k_hor)
+    states, targets = swarm.lattice_swarm(n_agents)
+    rp, col = swarm.knn_csr(states, 8, 3 * cfg["d_min"])
+    ctx = mpclib.Context(cfg)
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    agents = list(range(n_agents))
+    ref = run_oracle(cfg, states, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
+
+
+def test_impc_all_neighbours_reference_semantics(mpclib):
+    """Every other robot as a neighbour (ConnectivityIMPCCBF.cpp:59-67), closer spacing so some
+    CBF rows are active."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(36, seed=7)
+    states[:, :2] *= 0.5  # 2.5 m lattice: neighbours at ~d_min
+    rp, col = swarm.all_csr(len(states))
+    ctx = mpclib.Context(cfg)
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    agents = list(range(len(states)))
+    ref = run_oracle(cfg, states, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
+
+
+def test_config1_single_agent_static_obstacle(mpclib):
+    """BASELINE config 1: 1 agent, K=10, one static obstacle 3 m ahead."""
+    torch = _torch()
+    cfg = swarm.config(10)
+    states = np.array([[0.0, 0.0, 0.0, 0.8, 0.0, 0.0], [3.0, 0.0, 0.0, 0.0, 0.0, 0.0]])
+    targets = np.array([[6.0, 0.0, 0.0], [3.0, 0.0, 0.0]])
+    rp = np.array([0, 1, 2], np.int32)
+    col = np.array([1, 0], np.int32)
+    ctx = mpclib.Context(cfg)
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    ref = run_oracle(cfg, states, targets, rp, col, [0])
+    compare(cfg, g, ref, [0])
+
+
+def test_infeasible_initial_velocity(mpclib):
+    """v0 outside the velocity box: the k=0 velocity row equals the initial-velocity equality,
+    so the QP is infeasible and the IMPC loop stops after iteration 0 (:208-211)."""
+    torch = _torch()
+    cfg = swarm.config(10)
+    states = np.array([[0.0, 0.0, 0.0, 2.5, 0.0, 0.0]])
+    targets = np.array([[5.0, 0.0, 0.0]])
+    rp = np.array([0, 0], np.int32)
+    col = np.zeros(0, np.int32)
+    ctx = mpclib.Context(cfg)
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    ref = run_oracle(cfg, states, targets, rp, col, [0])
+    assert ref[0]["status"][0] == O.INFEASIBLE
+    compare(cfg, g, ref, [0])
+    assert np.all(np.isnan(g["x"][0]))
+
+
+def test_next_state_is_curve_at_h(mpclib):
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(16)
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    ctx = mpclib.Context(cfg)
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    p = O.make_params(cfg)
+    for a in range(16):
+        pos = O.eval_curve(p, g["x"][a], cfg["h"], 0)
+        vel = O.eval_curve(p, g["x"][a], cfg["h"], 1)
+        np.testing.assert_allclose(g["next_states"][a], np.concatenate([pos, vel]), atol=1e-9)
+
+
+def test_device_knn_matches_cpu(mpclib):
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, _ = swarm.lattice_swarm(1000)
+    rp_ref, col_ref = swarm.knn_csr(states, 8, 6.0)
+    ctx = mpclib.Context(cfg)
+    dev = torch.device("cuda", 0)
+    st = torch.tensor(states, dtype=torch.float64, device=dev)
+    rp = torch.empty(len(states) + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(len(states) * 8, dtype=torch.int32, device=dev)
+    ctx.build_neighbors(st, 0, len(states), 8, 6.0, rp, col)
+    torch.cuda.synchronize()
+    rp_h = rp.cpu().numpy()
+    np.testing.assert_array_equal(rp_h, rp_ref)
+    np.testing.assert_array_equal(col.cpu().numpy()[: rp_h[-1]], col_ref)
