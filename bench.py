@@ -1,0 +1,259 @@
+"""Benchmark: batched MPC-CBF QP solves on MI355X (BASELINE.json metric).
+
+A step = one IMPC control step of ConnectivityIMPCCBF::optimize for every agent
+(mpc_cbf/src/controller/ConnectivityIMPCCBF.cpp:47-215): state exchange (RCCL all-gather over
+xGMI when --gpus > 1), neighbour lists, two dependent QP solves per agent (fused HIP kernel), and
+the closed-loop state update. value = QPs solved by all ranks / wall time.
+
+Default workload (N=1): BASELINE config 3 — 4096 agents, horizon 15, pairwise collision CBF,
+8 nearest neighbours within 3 d_min, base_config.json parameters. Multi-GPU: weak scaling,
+4096 agents per GPU (config 4's 8192 agents at --gpus 2; --agents-total 8192 pins config 4).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mpc-cbf_amd"))
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= matrix) peak, vendor spec
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--agents-per-gpu", type=int, default=4096)
+    ap.add_argument("--agents-total", type=int, default=0, help="strong scaling: fixed total")
+    ap.add_argument("--k-hor", type=int, default=15)
+    ap.add_argument("--knn", type=int, default=8)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--cpu-baseline-agents", type=int, default=-1,
+                    help="agents in the CPU-oracle sample (default: sized for ~10 s)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--neighbours", choices=["grid", "csr"], default="grid",
+                    help="grid: fused in-kernel spatial-hash query; csr: separate KNN kernels")
+    return ap.parse_args()
+
+
+def flops_per_qp(iters: np.ndarray, rows: np.ndarray, nz: int) -> float:
+    """Algorithmic FP64 flops of the condensed Mehrotra PDIP actually executed (one QP):
+    per iteration and row: residual 2nz, normal matrix nz(nz+1), rhs 2nz, two step directions
+    2*2nz, step/update ~20; per iteration: Cholesky nz^3/3, four triangular solves 4nz^2,
+    P y 2nz^2. (roofline uses min(canonical, executed); executed is smaller.)"""
+    per_row = 2 * nz + nz * (nz + 1) + 2 * nz + 4 * nz + 20
+    per_it = nz ** 3 / 3 + 6 * nz * nz
+    return float(np.sum(iters * (rows * per_row + per_it)))
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from mpccbf import swarm, Context
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if rank == 0:
+            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
+                  file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    total = args.agents_total if args.agents_total > 0 else args.agents_per_gpu * world
+    per = total // world
+    assert per * world == total, "agents must divide evenly over ranks"
+    first = rank * per
+    cfg = swarm.config(args.k_hor)
+    radius = 3.0 * cfg["d_min"]
+    states_h, targets_h = swarm.lattice_swarm(total)
+    ctx = Context(cfg, device=local)
+    ctx.set_variant(args.variant)
+
+    states = torch.tensor(states_h, dtype=torch.float64, device=dev)
+    targets = torch.tensor(targets_h[first:first + per], dtype=torch.float64, device=dev)
+    local_states = states[first:first + per].clone()
+    nb_rp = torch.empty(per + 1, dtype=torch.int32, device=dev)
+    nb_col = torch.empty(per * max(args.knn, 1), dtype=torch.int32, device=dev)
+    out = ctx.alloc_outputs(per, device=dev)
+    next_states = out.pop("next_states")
+    nsteps = args.steps
+    status_log = torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev)
+    iters_log = torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def neighbours():
+        if args.neighbours == "csr":
+            ctx.build_neighbors(states, first, per, args.knn, radius, nb_rp, nb_col)
+            return dict(nb_row_ptr=nb_rp, nb_col=nb_col)
+        return dict(knn_k=args.knn, knn_radius=radius)  # fused device grid query
+
+    def step(slot: int | None):
+        if world > 1:
+            dist.all_gather_into_tensor(states, local_states)
+        else:
+            states.copy_(local_states)
+        nb = neighbours()
+        st = status_log[slot] if slot is not None else out["status"]
+        it = iters_log[slot] if slot is not None else out["iters"]
+        ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
+                       x=out["x"], status=st, obj=out["obj"], iters=it, next_states=next_states,
+                       **nb)
+        local_states.copy_(next_states)
+
+    for _ in range(args.warmup):
+        step(None)
+    torch.cuda.synchronize()
+
+    # per-step events (step latency) and per-launch events around the dominant kernel
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(nsteps + 1)]
+    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(nsteps)]
+
+    def step_timed(i):
+        if world > 1:
+            dist.all_gather_into_tensor(states, local_states)
+        else:
+            states.copy_(local_states)
+        nb = neighbours()
+        kev[i][0].record(stream)
+        ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
+                       x=out["x"], status=status_log[i], obj=out["obj"], iters=iters_log[i],
+                       next_states=next_states, **nb)
+        kev[i][1].record(stream)
+        local_states.copy_(next_states)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record(stream)
+    for i in range(nsteps):
+        step_timed(i)
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(nsteps)])
+    kern_ms = np.array([a.elapsed_time(b) for a, b in kev])
+
+    status = status_log.cpu().numpy()
+    iters = iters_log.cpu().numpy()
+    attempted = int(np.sum(~((status == 5) & (iters == 0))))
+    optimal = int(np.sum(status == 0))
+    rows = ctx.shared_rows  # CBF rows are few (filtered); counted as shared rows only
+    flops = flops_per_qp(iters.reshape(-1), np.full(iters.size, rows), ctx.nz)
+
+    t = torch.tensor([elapsed, float(attempted), float(optimal), flops, float(np.mean(kern_ms)),
+                      float(np.percentile(step_ms, 99))], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, kern_avg, p99 = float(mx[0]), float(mx[4]), float(mx[5])
+        attempted, optimal, flops = float(sm[1]), float(sm[2]), float(sm[3])
+        flops_rank0 = float(t[3])
+    else:
+        elapsed, attempted, optimal, flops, kern_avg, p99 = [float(v) for v in t.tolist()]
+        flops_rank0 = flops
+
+    if rank == 0:
+        qps = attempted / elapsed
+        # roofline of the dominant kernel on rank 0: executed algorithmic flops per launch /
+        # average launch time (FP64-compute bound; bytes per launch are tiny)
+        flops_per_launch = flops_rank0 / nsteps
+        achieved_tf = flops_per_launch / (kern_avg * 1e-3) / 1e12
+        res = {
+            "metric": "QP solves/sec (whole node) + p99 step latency, N-agent horizon-15 MPC-CBF",
+            "value": qps,
+            "unit": "QP/s",
+            "n_gpus": world,
+            "steps": nsteps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / nsteps * 1e3,
+            "p99_step_ms": p99,
+            "higher_is_better": True,
+            "scaling": "weak" if args.agents_total <= 0 else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (jittered-lattice swarm, seed 20251015)",
+            "config": {
+                "workload": (f"config3: {total} agents, horizon {cfg['k_hor']}, pairwise collision "
+                             f"CBF, knn{args.knn} r={radius:g}m ({args.neighbours}), base_config.json; 2 IMPC QPs/agent/step"
+                             if world == 1 else
+                             f"{total} agents ({per}/GPU), horizon {cfg['k_hor']}, RCCL all-gather of states"),
+                "agents_total": total,
+                "agents_per_gpu": per,
+                "k_hor": cfg["k_hor"],
+                "qp": {"n": ctx.n, "nz": ctx.nz, "shared_rows": ctx.shared_rows},
+                "parallelism": f"dp{world}",
+            },
+            "qps_attempted": attempted,
+            "qps_optimal_frac": optimal / max(attempted, 1),
+            "roofline": {
+                "bound": "mfma",
+                "achieved": achieved_tf,
+                "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved_tf / FP64_PEAK_TFLOPS,
+                "traffic": None,
+                "kernel": "impc_kernel<6,16,4>",
+                "kernel_avg_us": kern_avg * 1e3,
+                "flops_per_launch": flops_per_launch,
+            },
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(cfg, states_h, targets_h, args):
+    """The oracle (CPU restatement of the reference assembly + dense QP solve, standing in for
+    CPLEX which cannot run here) on a bounded sample of the same workload, 1 thread (CPLEX
+    Threads=1, CPLEX.cpp:158)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+    from mpccbf import swarm
+    p = O.make_params(cfg)
+    refs = swarm.refs_from_targets(targets_h, cfg["k_hor"])
+    rp, col = swarm.knn_csr(states_h, args.knn, 3.0 * cfg["d_min"])
+    n = len(states_h)
+    count = args.cpu_baseline_agents if args.cpu_baseline_agents > 0 else None
+    if count is None:
+        # calibrate on 32 agents, then size the sample for ~10 s
+        t = time.perf_counter()
+        r = O.impc_batch(p, states_h, refs, rp, col, 0, 32, 1)
+        dt = (time.perf_counter() - t) / 32
+        count = int(min(n, max(64, 10.0 / max(dt, 1e-6))))
+    t = time.perf_counter()
+    r = O.impc_batch(p, states_h, refs, rp, col, 0, count, 1)
+    dt = time.perf_counter() - t
+    return {"value": r["solved"] / dt, "unit": "QP/s", "cores": 1, "kind": "port",
+            "sample": f"first {count} agents of the same swarm/step, {r['solved']} QPs, "
+                      f"{dt:.1f} s single-threaded (oracle/ CPU restatement; CPLEX unavailable)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 1
+#define MPCCBF_ABI_VERSION 2
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -111,6 +111,10 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *   refs        num_agents x 3*k_hor full reference trajectory (ref_positions); or NULL
  *   nb_row_ptr  num_agents + 1 CSR offsets (nb_row_ptr[0] may be nonzero)
  *   nb_col      neighbour indices into `states` (the reference uses all N-1 others, :59-67)
+ *   knn_k, knn_radius   used when nb_row_ptr is NULL: the neighbours of each agent are its
+ *               knn_k nearest others (planar) within knn_radius, found on the device in the same
+ *               launch sequence (spatial hash of `states` + in-kernel 3x3-cell query);
+ *               requires num_states <= 32768 and at most 64 agents within the radius
  * Outputs (device, any may be NULL):
  *   x           num_agents x n: control points of the last OPTIMAL iteration (the curve the
  *               driver keeps, example :160-164); NaN if no iteration was OPTIMAL
@@ -134,6 +138,8 @@ typedef struct mpccbf_batch {
     double* obj;
     int32_t* iters;
     double* next_states;
+    int32_t knn_k;
+    double knn_radius;
 } mpccbf_batch;
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);

@@ -21,6 +21,9 @@ int launch_neighbors(const double* states, int num_states, int first, int num_ag
                      double radius, int32_t* row_ptr, int32_t* col, void* scratch,
                      size_t scratch_bytes, hipStream_t s);
 size_t neighbors_scratch_bytes(int num_states, int num_agents, int k);
+size_t grid_scratch_bytes(int num_states);
+uint32_t launch_grid_build(const double* states, int n, double radius, void* scratch,
+                           uint32_t** start, uint32_t** sorted, hipStream_t s);
 
 static thread_local std::string g_err;
 
@@ -47,6 +50,8 @@ struct mpccbf_ctx {
     size_t dbuf_elems = 0;
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
+    void* grid_scratch = nullptr;
+    size_t grid_bytes = 0;
     int variant = 0;
 };
 
@@ -166,6 +171,7 @@ void mpccbf_destroy(mpccbf_ctx* c) {
     if (!c) return;
     if (c->dbuf) (void)hipFree(c->dbuf);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->grid_scratch) (void)hipFree(c->grid_scratch);
     delete c;
 }
 
@@ -178,10 +184,35 @@ int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
     if (b->num_agents < 0 || b->agent_first < 0 || b->agent_first + b->num_agents > b->num_states)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
     if (b->num_agents == 0) return MPCCBF_OK;
-    if (!b->states || !b->nb_row_ptr || (!b->nb_col && b->num_states > 1))
+    const bool grid = b->nb_row_ptr == nullptr;
+    if (!b->states || (!grid && !b->nb_col && b->num_states > 1))
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "states / neighbour CSR missing");
+    if (grid && (b->knn_k < 1 || !(b->knn_radius > 0)))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
     if (!b->targets && !b->refs) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "targets or refs required");
     ImpcArgs a;
+    std::memset(&a, 0, sizeof(a));
+    HIP_TRY(hipSetDevice(c->device));
+    if (grid) {
+        const size_t need = grid_scratch_bytes(b->num_states);
+        if (need > c->grid_bytes) {
+            if (c->grid_scratch) (void)hipFree(c->grid_scratch);
+            c->grid_scratch = nullptr;
+            c->grid_bytes = 0;
+            HIP_TRY(hipMalloc(&c->grid_scratch, need));
+            c->grid_bytes = need;
+        }
+        uint32_t *start = nullptr, *sorted = nullptr;
+        const uint32_t T = launch_grid_build(b->states, b->num_states, b->knn_radius, c->grid_scratch,
+                                             &start, &sorted, (hipStream_t)stream);
+        if (T == 0) return fail(MPCCBF_ERR_CAPACITY, "grid neighbours: num_states > 32768 or launch failure");
+        a.grid.start = start;
+        a.grid.sorted = sorted;
+        a.grid.mask = T - 1;
+        a.grid.inv_cell = 1.0 / b->knn_radius;
+        a.grid.radius = b->knn_radius;
+        a.grid.k = b->knn_k;
+    }
     a.num_states = b->num_states;
     a.states = b->states;
     a.agent_first = b->agent_first;
@@ -195,7 +226,6 @@ int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
     a.obj = b->obj;
     a.iters = b->iters;
     a.next_states = b->next_states;
-    HIP_TRY(hipSetDevice(c->device));
     hipError_t e = launch_impc(c->dev, c->dbuf, a, c->variant, (hipStream_t)stream);
     if (e == hipErrorInvalidValue)
         return fail(MPCCBF_ERR_CAPACITY, "no kernel instantiation for this reduced dimension / row count");

@@ -2,7 +2,14 @@
 //
 // One QP is owned by a group of G lanes (G in {16, 32, 64}; G divides the 64-lane wavefront,
 // so a group never straddles waves). Rows of the QP are spread over the group's lanes; the
-// reductions below combine per-lane partials across the group with butterfly exchanges.
+// reductions below combine per-lane partials across the group.
+//
+// Within a 16-lane DPP row the butterfly uses DPP lane moves (no LDS traffic):
+//   quad_perm [1,0,3,2]  (xor 1)      quad_perm [2,3,0,1]  (xor 2)
+//   row_half_mirror      (i <-> 7-i)  row_mirror           (i <-> 15-i)
+// after the two quad stages every lane of a quad holds the quad total, so the mirrors pair each
+// lane with a lane of the other quad / other half-row, which is all an all-reduce needs.
+// Stages across 16-lane rows (G = 32, 64) use ds_swizzle/bpermute via __shfl_xor.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -10,35 +17,63 @@
 namespace mpccbf {
 namespace dev {
 
-template <int G>
-__device__ __forceinline__ double grp_sum(double v) {
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, G);
+constexpr int DPP_XOR1 = 0xB1;         // quad_perm(1,0,3,2)
+constexpr int DPP_XOR2 = 0x4E;         // quad_perm(2,3,0,1)
+constexpr int DPP_HALF_MIRROR = 0x141; // row_half_mirror
+constexpr int DPP_MIRROR = 0x140;      // row_mirror
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+enum class Op { Sum, Max, Min };
+
+template <Op OP>
+__device__ __forceinline__ double combine(double a, double b) {
+    if constexpr (OP == Op::Sum) return a + b;
+    else if constexpr (OP == Op::Max) return fmax(a, b);
+    else return fmin(a, b);
+}
+
+template <int G, Op OP>
+__device__ __forceinline__ double grp_reduce(double v) {
+    static_assert(G == 16 || G == 32 || G == 64, "group size");
+    v = combine<OP>(v, dpp_mov<DPP_XOR1>(v));
+    v = combine<OP>(v, dpp_mov<DPP_XOR2>(v));
+    v = combine<OP>(v, dpp_mov<DPP_HALF_MIRROR>(v));
+    v = combine<OP>(v, dpp_mov<DPP_MIRROR>(v));
+    if constexpr (G >= 32) v = combine<OP>(v, __shfl_xor(v, 16, G));
+    if constexpr (G >= 64) v = combine<OP>(v, __shfl_xor(v, 32, G));
     return v;
 }
 
-template <int G>
-__device__ __forceinline__ double grp_max(double v) {
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, G));
-    return v;
-}
-
-template <int G>
-__device__ __forceinline__ double grp_min(double v) {
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, G));
-    return v;
-}
+template <int G> __device__ __forceinline__ double grp_sum(double v) { return grp_reduce<G, Op::Sum>(v); }
+template <int G> __device__ __forceinline__ double grp_max(double v) { return grp_reduce<G, Op::Max>(v); }
+template <int G> __device__ __forceinline__ double grp_min(double v) { return grp_reduce<G, Op::Min>(v); }
 
 // In-place all-reduce (sum) of N values: every lane of the group ends with the totals.
-// Independent exchanges are issued back to back so their latencies overlap.
+// Stage-major so the N independent exchanges of a stage overlap.
 template <int G, int N>
 __device__ __forceinline__ void grp_sum_vec(double (&v)[N]) {
 #pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
+    for (int i = 0; i < N; i++) v[i] += dpp_mov<DPP_XOR1>(v[i]);
 #pragma unroll
-        for (int i = 0; i < N; i++) v[i] += __shfl_xor(v[i], o, G);
+    for (int i = 0; i < N; i++) v[i] += dpp_mov<DPP_XOR2>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += dpp_mov<DPP_HALF_MIRROR>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += dpp_mov<DPP_MIRROR>(v[i]);
+    if constexpr (G >= 32) {
+#pragma unroll
+        for (int i = 0; i < N; i++) v[i] += __shfl_xor(v[i], 16, G);
+    }
+    if constexpr (G >= 64) {
+#pragma unroll
+        for (int i = 0; i < N; i++) v[i] += __shfl_xor(v[i], 32, G);
     }
 }
 
@@ -53,9 +88,13 @@ __device__ __forceinline__ unsigned long long grp_ballot(bool pred) {
         return (all >> base) & ((1ull << G) - 1ull);
 }
 
-template <int G>
-__device__ __forceinline__ int grp_lane() {
-    return threadIdx.x & (G - 1);
+// Fast FP64 reciprocal: v_rcp_f64 refined by two Newton steps (full precision for the normal
+// range; the PDIP never divides by zero: slacks are clamped >= 1e-300).
+__device__ __forceinline__ double rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return r;
 }
 
 // Make this wave's LDS writes visible to its other lanes before they read them.

@@ -21,6 +21,32 @@ struct DevOps {
     double feas_tol;  // absolute row-violation tolerance for constant rows / single-row checks
 };
 
+// Spatial hash of agent positions (uniform cells of edge `radius`), built by grid_build_kernel:
+// bucket h holds sorted[start[h] .. start[h+1]).
+struct GridArgs {
+    const uint32_t* start;
+    const uint32_t* sorted;
+    uint32_t mask;
+    double inv_cell;
+    double radius;
+    int32_t k;  // keep the k nearest within radius
+};
+
+constexpr int NB_CAP = 64;  // grid-mode candidate capacity per agent (LDS)
+
+// bucket of uniform cell (cx, cy) in a power-of-two hash table (mask = size - 1)
+__host__ __device__ inline uint32_t cell_hash(long long cx, long long cy, uint32_t mask) {
+    const uint64_t h = (uint64_t)(cx * 73856093LL) ^ (uint64_t)(cy * 19349663LL);
+    return (uint32_t)(h ^ (h >> 29)) & mask;
+}
+
+// hash table size for n agents: power of two >= n (>= 1024)
+inline uint32_t grid_table_size(int n) {
+    uint32_t T = 1024;
+    while (T < (uint32_t)n) T <<= 1;
+    return T;
+}
+
 struct ImpcArgs {
     int32_t num_states;
     const double* states;
@@ -28,8 +54,9 @@ struct ImpcArgs {
     int32_t num_agents;
     const double* targets;
     const double* refs;  // full 3K per agent (tail used)
-    const int32_t* nb_row_ptr;
+    const int32_t* nb_row_ptr;  // CSR mode (NULL: grid mode)
     const int32_t* nb_col;
+    GridArgs grid;
     double* x;
     int32_t* status;
     double* obj;

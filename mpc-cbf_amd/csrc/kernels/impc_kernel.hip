@@ -47,6 +47,92 @@ __device__ __forceinline__ void safety_cbf(const double e[6], double npx, double
     a[2] = 0.0;
 }
 
+// Per-group LDS scratch of the grid neighbour query.
+struct NbScratch {
+    int32_t idx[NB_CAP];   // candidate / final neighbour indices
+    int32_t tmp[NB_CAP];   // sorted output
+    double d2[NB_CAP];     // candidate squared distances
+    int32_t keep[NB_CAP];  // k-nearest flags
+};
+
+// k nearest other agents (planar distance, ties by index) within the radius, found through the
+// spatial hash; the result is left in sc.idx sorted by agent index. Returns the count, or -1 if
+// more than NB_CAP candidates lie within the radius. Distance-only test: agents of a colliding
+// cell that share a bucket are still filtered by distance, and a bucket reached from two of the
+// 9 cells is scanned once.
+template <int G>
+__device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double py, NbScratch& sc,
+                              int gl) {
+    const GridArgs& gr = args.grid;
+    const long long cx = (long long)floor(px * gr.inv_cell), cy = (long long)floor(py * gr.inv_cell);
+    const double r2 = gr.radius * gr.radius;
+    uint32_t hs[9], b0[9], b1[9];
+#pragma unroll
+    for (int c = 0; c < 9; c++) {
+        hs[c] = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
+        b0[c] = gr.start[hs[c]];
+        b1[c] = gr.start[hs[c] + 1];
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int c = 0; c < 9; c++) {
+        bool dup = false;
+#pragma unroll
+        for (int p = 0; p < c; p++) dup = dup || (hs[p] == hs[c]);
+        if (dup) continue;
+        for (uint32_t base = b0[c]; base < b1[c]; base += G) {
+            const uint32_t e = base + gl;
+            bool keep = false;
+            int j = -1;
+            double d2 = 0.0;
+            if (e < b1[c]) {
+                j = (int)gr.sorted[e];
+                const double ex = args.states[(size_t)j * 6] - px;
+                const double ey = args.states[(size_t)j * 6 + 1] - py;
+                d2 = ex * ex + ey * ey;
+                keep = (j != self) && (d2 <= r2);
+            }
+            const unsigned long long msk = grp_ballot<G>(keep);
+            const int slot = cnt + __popcll(msk & ((1ull << gl) - 1ull));
+            if (keep && slot < NB_CAP) {
+                sc.idx[slot] = j;
+                sc.d2[slot] = d2;
+            }
+            cnt += __popcll(msk);
+        }
+    }
+    if (cnt > NB_CAP) return -1;
+    wave_lds_sync();
+    // rank by (d2, index): keep the k nearest
+    const int k = gr.k;
+    int nk = 0;
+    for (int i = gl; i < cnt; i += G) {
+        const double di = sc.d2[i];
+        const int ji = sc.idx[i];
+        int rank = 0;
+        for (int m = 0; m < cnt; m++) {
+            const double dm = sc.d2[m];
+            rank += (dm < di || (dm == di && sc.idx[m] < ji)) ? 1 : 0;
+        }
+        sc.keep[i] = rank < k ? 1 : 0;
+    }
+    nk = cnt < k ? cnt : k;
+    wave_lds_sync();
+    // order the kept set by agent index
+    for (int i = gl; i < cnt; i += G) {
+        if (sc.keep[i]) {
+            const int ji = sc.idx[i];
+            int pos = 0;
+            for (int m = 0; m < cnt; m++) pos += (sc.keep[m] && sc.idx[m] < ji) ? 1 : 0;
+            sc.tmp[pos] = ji;
+        }
+    }
+    wave_lds_sync();
+    for (int i = gl; i < nk; i += G) sc.idx[i] = sc.tmp[i];
+    wave_lds_sync();
+    return nk;
+}
+
 template <int NZ, int G, int R>
 __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double* __restrict__ buf,
                                                     const ImpcArgs args) {
@@ -137,10 +223,11 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
 #pragma unroll
             for (int j = 0; j < NZ; j++) rw.g[r][j] = on ? Gm[si * NZ + j] : 0.0;
             const double l = lo[si], h = hi[si];
-            rw.hl[r] = on && l > -1e300;
-            rw.hu[r] = on && h < 1e300;
-            rw.lo[r] = rw.hl[r] ? l - sh : 0.0;
-            rw.hi[r] = rw.hu[r] ? h - sh : 0.0;
+            const bool hl = on && l > -1e300, hu = on && h < 1e300;
+            rw.ml[r] = hl ? 1.0 : 0.0;
+            rw.mu[r] = hu ? 1.0 : 0.0;
+            rw.lo[r] = hl ? l - sh : 0.0;
+            rw.hi[r] = hu ? h - sh : 0.0;
         }
     }
     // ---- constant rows: pure feasibility checks on s0
@@ -158,8 +245,20 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
         infeasible = grp_ballot<G>(infeasible) != 0ull;
     }
 
-    const int nb0 = args.nb_row_ptr[ai], nb1 = args.nb_row_ptr[ai + 1];
-    const int nnb = nb1 - nb0;
+    // ---- neighbours: CSR (caller-provided, e.g. all N-1 others as the reference does) or the
+    // k nearest within the radius from the spatial hash (3 x 3 cells around the agent)
+    const bool grid_mode = args.nb_row_ptr == nullptr;
+    int nb0 = 0, nnb = 0;
+    __shared__ NbScratch nb_scratch[GPB];
+    const int32_t* nbl = nb_scratch[gib].idx;
+    if (!grid_mode) {
+        nb0 = args.nb_row_ptr[ai];
+        nnb = args.nb_row_ptr[ai + 1] - nb0;
+    } else {
+        nnb = grid_neighbors<G>(args, self, s0[0], s0[1], nb_scratch[gib], gl);
+    }
+    const bool nb_overflow = nnb < 0;
+    if (nb_overflow) nnb = 0;
     const double* UZ = opp(buf, op.o_UZ);
     const double* US = opp(buf, op.o_US);
 
@@ -221,7 +320,7 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
                 bool keep = false;
                 double a[3] = {0.0, 0.0, 0.0}, b = 0.0;
                 if (j < nnb) {
-                    const int nbi = args.nb_col[nb0 + j];
+                    const int nbi = grid_mode ? nbl[j] : args.nb_col[nb0 + j];
                     const double* ns = args.states + (size_t)nbi * 6;
                     safety_cbf(e, ns[0], ns[1], ns[3], ns[4], op.d_min, a, b);
                     // max / min of -a^T u over the acceleration box at sample k (those box rows
@@ -263,15 +362,15 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
                 const double* src = stage + (size_t)(on ? ci : 0) * (NZ + 1);
 #pragma unroll
                 for (int jz = 0; jz < NZ; jz++) rw.g[r][jz] = on ? src[jz] : 0.0;
-                rw.hl[r] = false;
-                rw.hu[r] = on;
+                rw.ml[r] = 0.0;
+                rw.mu[r] = on ? 1.0 : 0.0;
                 rw.lo[r] = 0.0;
                 rw.hi[r] = on ? src[NZ] : 0.0;
             }
         }
         int st;
         int nit = 0;
-        if (count > cap) {
+        if (count > cap || nb_overflow) {
             st = ST_ERROR;  // capacity: caller re-runs with a wider instantiation
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;

@@ -8,15 +8,13 @@
 
 #include <cstdint>
 
+#include "impc.hpp"
+
 namespace mpccbf {
 namespace dev {
 
 constexpr int KNN_MAX = 16;
 
-__device__ __forceinline__ uint32_t cell_hash(long long cx, long long cy, uint32_t mask) {
-    const uint64_t h = (uint64_t)(cx * 73856093LL) ^ (uint64_t)(cy * 19349663LL);
-    return (uint32_t)(h ^ (h >> 29)) & mask;
-}
 
 __device__ __forceinline__ void cell_of(double px, double py, double inv, long long& cx, long long& cy) {
     cx = (long long)floor(px * inv);
@@ -238,6 +236,84 @@ int launch_neighbors(const double* states, int num_states, int first, int num_ag
     hipLaunchKernelGGL(dev::knn_compact_kernel, dim3(1), dim3(1024), 0, s, num_agents, k, row_ptr,
                        wide, col);
     return (int)hipGetLastError();
+}
+
+}  // namespace mpccbf
+
+namespace mpccbf {
+namespace dev {
+
+// Spatial hash of all agents in ONE workgroup (n <= 32768): LDS histogram -> block scan ->
+// scatter. One launch instead of count/scan/scatter; bucket order inside a cell follows LDS
+// atomic order (the consumer orders neighbours by index, so results do not depend on it).
+__global__ void __launch_bounds__(1024) grid_build_kernel(const double* __restrict__ st, int n,
+                                                          double inv, uint32_t T, uint32_t* start,
+                                                          uint32_t* sorted, uint32_t* slot_off) {
+    extern __shared__ uint32_t cnt[];  // T buckets
+    __shared__ uint32_t part[1024];
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < T; i += 1024) cnt[i] = 0u;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const long long cx = (long long)floor(st[(size_t)i * 6] * inv);
+        const long long cy = (long long)floor(st[(size_t)i * 6 + 1] * inv);
+        slot_off[i] = atomicAdd(&cnt[cell_hash(cx, cy, T - 1)], 1u);
+    }
+    __syncthreads();
+    const uint32_t per = T / 1024, b = tid * per;
+    uint32_t s = 0;
+    for (uint32_t i = 0; i < per; i++) s += cnt[b + i];
+    part[tid] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const uint32_t v = tid >= o ? part[tid - o] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    uint32_t run = tid > 0 ? part[tid - 1] : 0u;
+    for (uint32_t i = 0; i < per; i++) {
+        const uint32_t c = cnt[b + i];
+        cnt[b + i] = run;
+        start[b + i] = run;
+        run += c;
+    }
+    if (tid == 1023) start[T] = part[1023];
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const long long cx = (long long)floor(st[(size_t)i * 6] * inv);
+        const long long cy = (long long)floor(st[(size_t)i * 6 + 1] * inv);
+        sorted[cnt[cell_hash(cx, cy, T - 1)] + slot_off[i]] = (uint32_t)i;
+    }
+}
+
+}  // namespace dev
+
+size_t grid_scratch_bytes(int num_states) {
+    const uint32_t T = grid_table_size(num_states);
+    return ((size_t)(T + 1) * 4 + 255) / 256 * 256 + ((size_t)num_states * 8 + 255) / 256 * 256;
+}
+
+// start (T+1) | sorted (n) | slot_off (n) carved from scratch; returns T or 0 on error
+uint32_t launch_grid_build(const double* states, int n, double radius, void* scratch,
+                           uint32_t** start, uint32_t** sorted, hipStream_t s) {
+    const uint32_t T = grid_table_size(n);
+    if (T > 32768) return 0;  // single-workgroup LDS histogram limit
+    char* p = (char*)scratch;
+    *start = (uint32_t*)p;
+    p += ((size_t)(T + 1) * 4 + 255) / 256 * 256;
+    *sorted = (uint32_t*)p;
+    uint32_t* slot_off = *sorted + n;
+    static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an opt-in (gfx950: 160 KiB/CU)
+    if (!attr_set) {
+        if (hipFuncSetAttribute((const void*)dev::grid_build_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4) != hipSuccess)
+            return 0;
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(dev::grid_build_kernel, dim3(1), dim3(1024), (size_t)T * 4, s, states, n,
+                       1.0 / radius, T, *start, *sorted, slot_off);
+    return hipGetLastError() == hipSuccess ? T : 0;
 }
 
 }  // namespace mpccbf

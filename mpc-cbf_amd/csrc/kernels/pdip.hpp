@@ -4,12 +4,15 @@
 //
 // executed by a group of G lanes per QP. Row i lives in register slot r = i / G of lane
 // i % G (R slots per lane), together with its slacks and duals, so one Newton step is:
-//   per lane:  row residuals, the rank-1 terms D_i g_i g_i^T, right-hand sides
-//   group:     one all-reduce of the packed normal matrix + vectors
+//   per lane:  row residuals, rank-1 terms D_i g_i g_i^T and right-hand sides (branch-free:
+//              an absent side has mask 0, slack 1 and dual 0, so it contributes nothing)
+//   group:     one all-reduce of the packed normal matrix + vector (DPP butterfly)
 //   uniform:   Cholesky of the NZ x NZ normal matrix (every lane of the group, same values)
-// Mehrotra predictor-corrector (Nocedal & Wright, Alg. 16.4 adapted to two-sided rows).
-// This is the solver that stands in for CPLEXSolver::solve (qpcpp/src/solvers/CPLEX.cpp:35-177);
-// the QP it receives is the reference QP condensed onto the null space of its equalities.
+// Mehrotra predictor-corrector (Nocedal & Wright, Alg. 16.4) on two-sided rows; the dual
+// residual is tracked (an exact Newton step scales it by 1 - alpha) and recomputed when the
+// tracked value claims convergence. This is the solver that stands in for
+// CPLEXSolver::solve (qpcpp/src/solvers/CPLEX.cpp:35-177); the QP it receives is the reference
+// QP condensed onto the null space of its equality constraints.
 #pragma once
 
 #include "group.hpp"
@@ -22,13 +25,13 @@ constexpr int ST_OPTIMAL = 0, ST_INFEASIBLE = 3, ST_ERROR = 4, ST_UNKNOWN = 5;
 template <int NZ>
 struct Sym {
     static constexpr int P = NZ * (NZ + 1) / 2;
-    __device__ static constexpr int idx(int i, int j) {  // i <= j, packed upper triangle row-major
+    __host__ __device__ static constexpr int idx(int i, int j) {  // i <= j, packed upper, row-major
         return i * NZ - (i * (i - 1)) / 2 + (j - i);
     }
 };
 
-// In-place Cholesky of packed symmetric M (upper triangle holds L^T). Returns false if a pivot
-// is not positive (caller regularises).
+// In-place Cholesky of packed symmetric M (upper triangle becomes L^T, diagonal stores L_jj,
+// dinv the reciprocal diagonal). Returns false if a pivot is not positive.
 template <int NZ>
 __device__ __forceinline__ bool chol_packed(double (&M)[Sym<NZ>::P], double (&dinv)[NZ]) {
     bool ok = true;
@@ -36,25 +39,23 @@ __device__ __forceinline__ bool chol_packed(double (&M)[Sym<NZ>::P], double (&di
     for (int j = 0; j < NZ; j++) {
         double d = M[Sym<NZ>::idx(j, j)];
 #pragma unroll
-        for (int k = 0; k < j; k++) d -= M[Sym<NZ>::idx(k, j)] * M[Sym<NZ>::idx(k, j)];
+        for (int k = 0; k < j; k++) d = fma(-M[Sym<NZ>::idx(k, j)], M[Sym<NZ>::idx(k, j)], d);
         ok = ok && (d > 0.0);
         d = d > 0.0 ? d : 1e-300;
         const double r = rsqrt(d);
-        const double ljj = d * r;
         dinv[j] = r;
-        M[Sym<NZ>::idx(j, j)] = ljj;
+        M[Sym<NZ>::idx(j, j)] = d * r;
 #pragma unroll
         for (int i = j + 1; i < NZ; i++) {
             double v = M[Sym<NZ>::idx(j, i)];
 #pragma unroll
-            for (int k = 0; k < j; k++) v -= M[Sym<NZ>::idx(k, i)] * M[Sym<NZ>::idx(k, j)];
+            for (int k = 0; k < j; k++) v = fma(-M[Sym<NZ>::idx(k, i)], M[Sym<NZ>::idx(k, j)], v);
             M[Sym<NZ>::idx(j, i)] = v * r;
         }
     }
     return ok;
 }
 
-// Solve (L L^T) x = b with the factor from chol_packed.
 template <int NZ>
 __device__ __forceinline__ void chol_solve(const double (&M)[Sym<NZ>::P], const double (&dinv)[NZ],
                                            const double (&b)[NZ], double (&x)[NZ]) {
@@ -63,14 +64,14 @@ __device__ __forceinline__ void chol_solve(const double (&M)[Sym<NZ>::P], const 
     for (int i = 0; i < NZ; i++) {
         double v = b[i];
 #pragma unroll
-        for (int k = 0; k < i; k++) v -= M[Sym<NZ>::idx(k, i)] * w[k];
+        for (int k = 0; k < i; k++) v = fma(-M[Sym<NZ>::idx(k, i)], w[k], v);
         w[i] = v * dinv[i];
     }
 #pragma unroll
     for (int i = NZ - 1; i >= 0; i--) {
         double v = w[i];
 #pragma unroll
-        for (int k = i + 1; k < NZ; k++) v -= M[Sym<NZ>::idx(i, k)] * x[k];
+        for (int k = i + 1; k < NZ; k++) v = fma(-M[Sym<NZ>::idx(i, k)], x[k], v);
         x[i] = v * dinv[i];
     }
 }
@@ -83,12 +84,13 @@ __device__ __forceinline__ double dotz(const double (&a)[NZ], const double (&b)[
     return s;
 }
 
-// Row storage of one lane: R slots.
+// Row storage of one lane: R slots. ml/mu are 1.0 when the lower/upper side is finite, else 0;
+// lo/hi are 0 for absent sides.
 template <int NZ, int R>
 struct Rows {
     double g[R][NZ];
     double lo[R], hi[R];
-    bool hl[R], hu[R];  // finite lower / upper side present
+    double ml[R], mu[R];
 };
 
 struct PdipCfg {
@@ -101,8 +103,12 @@ struct PdipOut {
     int iters;
 };
 
-// P: NZ x NZ row-major (uniform, global), LP: its lower Cholesky factor (row-major) used for
-// the unconstrained start. q: uniform. y: result (uniform).
+// step-to-boundary of s + a ds >= 0 (or z): returns the limiting a, or `big` if ds >= 0
+__device__ __forceinline__ double step_bound(double s, double ds, double big) {
+    return ds < 0.0 ? -s * rcp(ds) : big;
+}
+
+// P: NZ x NZ row-major, LP: lower Cholesky factor of P (row-major); both uniform (global).
 template <int NZ, int G, int R>
 __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ P,
                               const double* __restrict__ LP, const double (&q)[NZ],
@@ -115,86 +121,119 @@ __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ 
         for (int i = 0; i < NZ; i++) {
             double v = -q[i];
 #pragma unroll
-            for (int k = 0; k < i; k++) v -= LP[i * NZ + k] * w[k];
-            w[i] = v / LP[i * NZ + i];
+            for (int k = 0; k < i; k++) v = fma(-LP[i * NZ + k], w[k], v);
+            w[i] = v * rcp(LP[i * NZ + i]);
         }
 #pragma unroll
         for (int i = NZ - 1; i >= 0; i--) {
             double v = w[i];
 #pragma unroll
-            for (int k = i + 1; k < NZ; k++) v -= LP[k * NZ + i] * y[k];
-            y[i] = v / LP[i * NZ + i];
+            for (int k = i + 1; k < NZ; k++) v = fma(-LP[k * NZ + i], y[k], v);
+            y[i] = v * rcp(LP[i * NZ + i]);
         }
     }
-    double sl[R], su[R], zl[R], zu[R];
+    double sl[R], su[R], zl[R], zu[R], pl[R], pu[R];
     double nsides = 0.0;
 #pragma unroll
     for (int r = 0; r < R; r++) {
         const double t = dotz<NZ>(rw.g[r], y);
-        sl[r] = rw.hl[r] ? fmax(t - rw.lo[r], 1.0) : 1.0;
-        su[r] = rw.hu[r] ? fmax(rw.hi[r] - t, 1.0) : 1.0;
-        zl[r] = rw.hl[r] ? 1.0 / sl[r] : 0.0;
-        zu[r] = rw.hu[r] ? 1.0 / su[r] : 0.0;
-        nsides += (rw.hl[r] ? 1.0 : 0.0) + (rw.hu[r] ? 1.0 : 0.0);
+        sl[r] = rw.ml[r] > 0.0 ? fmax(t - rw.lo[r], 1.0) : 1.0;
+        su[r] = rw.mu[r] > 0.0 ? fmax(rw.hi[r] - t, 1.0) : 1.0;
+        zl[r] = rw.ml[r] * rcp(sl[r]);
+        zu[r] = rw.mu[r] * rcp(su[r]);
+        pl[r] = rw.ml[r] * rcp(1.0 + fabs(rw.lo[r]));  // relative primal-residual scale
+        pu[r] = rw.mu[r] * rcp(1.0 + fabs(rw.hi[r]));
+        nsides += rw.ml[r] + rw.mu[r];
     }
     nsides = grp_sum<G>(nsides);
     double qn = 0.0;
 #pragma unroll
     for (int j = 0; j < NZ; j++) qn = fmax(qn, fabs(q[j]));
-    const double inv_ns = nsides > 0.0 ? 1.0 / nsides : 0.0;
+    const double inv_ns = nsides > 0.0 ? rcp(nsides) : 0.0;
+    const double inv_qn = rcp(1.0 + qn);
 
     PdipOut out{ST_UNKNOWN, 0};
     double mu0 = 1.0;
+    double rd_track = 1e300;  // tracked ||r_d||_inf / (1 + ||q||_inf)
+    bool rd_exact = true;     // recompute r_d exactly this iteration
     for (int it = 0;; it++) {
-        // ---- residuals and the normal matrix
-        constexpr int NV = S::P + 2 * NZ + 1;
-        double acc[NV];
+        // ---- residuals, normal matrix, rhs: acc = [M (packed) | G^T w | mu], accr = G^T (zu - zl)
+        constexpr int NM = S::P;
+        constexpr int NA = NM + NZ + 1;
+        double acc[NA], accr[NZ];
 #pragma unroll
-        for (int k = 0; k < NV; k++) acc[k] = 0.0;
+        for (int k = 0; k < NA; k++) acc[k] = 0.0;
+#pragma unroll
+        for (int k = 0; k < NZ; k++) accr[k] = 0.0;
         double rp = 0.0;
-        double rsl[R], rsu[R], Dl[R], Du[R];
+        double rsl[R], rsu[R], Dl[R], Du[R], isl[R], isu[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const double t = dotz<NZ>(rw.g[r], y);
-            rsl[r] = rw.hl[r] ? (t - rw.lo[r] - sl[r]) : 0.0;
-            rsu[r] = rw.hu[r] ? (rw.hi[r] - t - su[r]) : 0.0;
-            Dl[r] = zl[r] / sl[r];
-            Du[r] = zu[r] / su[r];
+            rsl[r] = rw.ml[r] * (t - rw.lo[r] - sl[r]);
+            rsu[r] = rw.mu[r] * (rw.hi[r] - t - su[r]);
+            isl[r] = rcp(sl[r]);
+            isu[r] = rcp(su[r]);
+            Dl[r] = zl[r] * isl[r];
+            Du[r] = zu[r] * isu[r];
             const double D = Dl[r] + Du[r];
             const double wv = Du[r] * rsu[r] - Dl[r] * rsl[r];
-            const double wd = zu[r] - zl[r];
 #pragma unroll
             for (int i = 0; i < NZ; i++) {
                 const double dg = D * rw.g[r][i];
 #pragma unroll
                 for (int j = i; j < NZ; j++) acc[S::idx(i, j)] = fma(dg, rw.g[r][j], acc[S::idx(i, j)]);
-                acc[S::P + i] = fma(rw.g[r][i], wd, acc[S::P + i]);
-                acc[S::P + NZ + i] = fma(rw.g[r][i], wv, acc[S::P + NZ + i]);
+                acc[NM + i] = fma(rw.g[r][i], wv, acc[NM + i]);
             }
-            acc[NV - 1] += sl[r] * zl[r] + su[r] * zu[r];
-            if (rw.hl[r]) rp = fmax(rp, fabs(rsl[r]) / (1.0 + fabs(rw.lo[r])));
-            if (rw.hu[r]) rp = fmax(rp, fabs(rsu[r]) / (1.0 + fabs(rw.hi[r])));
+            acc[NM + NZ] = fma(sl[r], zl[r], fma(su[r], zu[r], acc[NM + NZ]));
+            if (rd_exact) {
+#pragma unroll
+                for (int i = 0; i < NZ; i++) accr[i] = fma(rw.g[r][i], zu[r] - zl[r], accr[i]);
+            }
+            rp = fmax(rp, fmax(fabs(rsl[r]) * pl[r], fabs(rsu[r]) * pu[r]));
         }
-        grp_sum_vec<G, NV>(acc);
+        grp_sum_vec<G, NA>(acc);
+        if (rd_exact) grp_sum_vec<G, NZ>(accr);
         rp = grp_max<G>(rp);
-        const double mu = acc[NV - 1] * inv_ns;
+        const double mu = acc[NM + NZ] * inv_ns;
         double py[NZ];
-        double rdn = 0.0;
 #pragma unroll
         for (int i = 0; i < NZ; i++) {
             double v = q[i];
 #pragma unroll
             for (int j = 0; j < NZ; j++) v = fma(P[i * NZ + j], y[j], v);
             py[i] = v;  // P y + q
-            rdn = fmax(rdn, fabs(v + acc[S::P + i]));
         }
-        rdn /= (1.0 + qn);
+        if (rd_exact) {
+            double rdn = 0.0;
+#pragma unroll
+            for (int i = 0; i < NZ; i++) rdn = fmax(rdn, fabs(py[i] + accr[i]));
+            rd_track = rdn * inv_qn;
+            rd_exact = false;
+        }
         out.iters = it;
         // NaN-safe: fmax drops NaN operands, so test finiteness of every reduced quantity
-        const bool finite = isfinite(rp) && isfinite(rdn) && isfinite(mu) && isfinite(acc[0]);
-        if (finite && rp <= cfg.tol && rdn <= cfg.tol && mu <= cfg.tol * 0.1) {
-            out.status = ST_OPTIMAL;
-            break;
+        const bool finite = isfinite(rp) && isfinite(rd_track) && isfinite(mu) && isfinite(acc[0]);
+        if (finite && rp <= cfg.tol && mu <= cfg.tol * 0.1) {
+            if (rd_track <= cfg.tol) {
+                // confirm with the exact dual residual before accepting
+                double chk[NZ];
+#pragma unroll
+                for (int i = 0; i < NZ; i++) chk[i] = 0.0;
+#pragma unroll
+                for (int r = 0; r < R; r++)
+#pragma unroll
+                    for (int i = 0; i < NZ; i++) chk[i] = fma(rw.g[r][i], zu[r] - zl[r], chk[i]);
+                grp_sum_vec<G, NZ>(chk);
+                double rdn = 0.0;
+#pragma unroll
+                for (int i = 0; i < NZ; i++) rdn = fmax(rdn, fabs(py[i] + chk[i]));
+                rd_track = rdn * inv_qn;
+                if (rd_track <= cfg.tol) {
+                    out.status = ST_OPTIMAL;
+                    break;
+                }
+            }
         }
         if (it == 0) mu0 = mu;
         // divergence (no feasible point): complementarity grows instead of shrinking
@@ -203,54 +242,54 @@ __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ 
             break;
         }
         // ---- factor M = P + G^T D G
-        double M[S::P], dinv[NZ];
+        double M[NM], dinv[NZ];
 #pragma unroll
         for (int i = 0; i < NZ; i++)
 #pragma unroll
             for (int j = i; j < NZ; j++) M[S::idx(i, j)] = acc[S::idx(i, j)] + P[i * NZ + j];
         if (!chol_packed<NZ>(M, dinv)) {
-            out.status = ST_UNKNOWN;  // numerically singular: let phase 1 decide feasibility
+            out.status = ST_UNKNOWN;  // numerically singular: phase 1 decides feasibility
             break;
         }
         // ---- predictor (affine) direction
         double rhs[NZ], dya[NZ];
 #pragma unroll
-        for (int i = 0; i < NZ; i++) rhs[i] = -py[i] + acc[S::P + NZ + i];
+        for (int i = 0; i < NZ; i++) rhs[i] = acc[NM + i] - py[i];
         chol_solve<NZ>(M, dinv, rhs, dya);
         double dsla[R], dzla[R], dsua[R], dzua[R];
         double ap = 1.0, ad = 1.0;
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const double td = dotz<NZ>(rw.g[r], dya);
-            dsla[r] = rw.hl[r] ? td + rsl[r] : 0.0;
-            dsua[r] = rw.hu[r] ? -td + rsu[r] : 0.0;
-            dzla[r] = rw.hl[r] ? -zl[r] - Dl[r] * dsla[r] : 0.0;
-            dzua[r] = rw.hu[r] ? -zu[r] - Du[r] * dsua[r] : 0.0;
-            if (dsla[r] < 0.0) ap = fmin(ap, -sl[r] / dsla[r]);
-            if (dsua[r] < 0.0) ap = fmin(ap, -su[r] / dsua[r]);
-            if (dzla[r] < 0.0) ad = fmin(ad, -zl[r] / dzla[r]);
-            if (dzua[r] < 0.0) ad = fmin(ad, -zu[r] / dzua[r]);
+            dsla[r] = rw.ml[r] * (td + rsl[r]);
+            dsua[r] = rw.mu[r] * (rsu[r] - td);
+            dzla[r] = -zl[r] - Dl[r] * dsla[r];
+            dzua[r] = -zu[r] - Du[r] * dsua[r];
+            ap = fmin(ap, fmin(step_bound(sl[r], dsla[r], 1.0), step_bound(su[r], dsua[r], 1.0)));
+            ad = fmin(ad, fmin(step_bound(zl[r], dzla[r], 1.0), step_bound(zu[r], dzua[r], 1.0)));
         }
         ap = grp_min<G>(ap);
         ad = grp_min<G>(ad);
         double mua = 0.0;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            if (rw.hl[r]) mua += (sl[r] + ap * dsla[r]) * (zl[r] + ad * dzla[r]);
-            if (rw.hu[r]) mua += (su[r] + ap * dsua[r]) * (zu[r] + ad * dzua[r]);
+            mua = fma(sl[r] + ap * dsla[r], zl[r] + ad * dzla[r], mua);
+            mua = fma(su[r] + ap * dsua[r], zu[r] + ad * dzua[r], mua);
         }
         mua = grp_sum<G>(mua) * inv_ns;
-        double sig = mu > 0.0 ? mua / mu : 0.0;
+        double sig = mu > 0.0 ? mua * rcp(mu) : 0.0;
         sig = fmin(sig * sig * sig, 1.0);
         const double smu = sig * mu;
         // ---- corrector: extra right-hand side from sigma*mu and the second-order term
         double vc[NZ];
 #pragma unroll
         for (int i = 0; i < NZ; i++) vc[i] = 0.0;
+        double cl[R], cu[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const double w = (rw.hl[r] ? (smu - dsla[r] * dzla[r]) / sl[r] : 0.0) -
-                             (rw.hu[r] ? (smu - dsua[r] * dzua[r]) / su[r] : 0.0);
+            cl[r] = rw.ml[r] * (smu - dsla[r] * dzla[r]);
+            cu[r] = rw.mu[r] * (smu - dsua[r] * dzua[r]);
+            const double w = cl[r] * isl[r] - cu[r] * isu[r];
 #pragma unroll
             for (int i = 0; i < NZ; i++) vc[i] = fma(rw.g[r][i], w, vc[i]);
         }
@@ -264,14 +303,14 @@ __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ 
 #pragma unroll
         for (int r = 0; r < R; r++) {
             const double td = dotz<NZ>(rw.g[r], dy);
-            dsl[r] = rw.hl[r] ? td + rsl[r] : 0.0;
-            dsu[r] = rw.hu[r] ? -td + rsu[r] : 0.0;
-            dzl[r] = rw.hl[r] ? (smu - sl[r] * zl[r] - dsla[r] * dzla[r] - zl[r] * dsl[r]) / sl[r] : 0.0;
-            dzu[r] = rw.hu[r] ? (smu - su[r] * zu[r] - dsua[r] * dzua[r] - zu[r] * dsu[r]) / su[r] : 0.0;
-            if (dsl[r] < 0.0) amax = fmin(amax, -sl[r] / dsl[r]);
-            if (dsu[r] < 0.0) amax = fmin(amax, -su[r] / dsu[r]);
-            if (dzl[r] < 0.0) amax = fmin(amax, -zl[r] / dzl[r]);
-            if (dzu[r] < 0.0) amax = fmin(amax, -zu[r] / dzu[r]);
+            dsl[r] = rw.ml[r] * (td + rsl[r]);
+            dsu[r] = rw.mu[r] * (rsu[r] - td);
+            // dz = (sigma mu - s z - ds_a dz_a - z ds) / s   (absent side: cl = 0, z = 0 -> 0)
+            dzl[r] = (cl[r] - sl[r] * zl[r] - zl[r] * dsl[r]) * isl[r];
+            dzu[r] = (cu[r] - su[r] * zu[r] - zu[r] * dsu[r]) * isu[r];
+            amax = fmin(amax, fmin(step_bound(sl[r], dsl[r], 1e300), step_bound(su[r], dsu[r], 1e300)));
+            amax = fmin(amax, fmin(step_bound(zl[r], rw.ml[r] * dzl[r], 1e300),
+                                   step_bound(zu[r], rw.mu[r] * dzu[r], 1e300)));
         }
         amax = grp_min<G>(amax);
         const double alpha = fmin(1.0, 0.99 * amax);
@@ -279,23 +318,20 @@ __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ 
         for (int i = 0; i < NZ; i++) y[i] = fma(alpha, dy[i], y[i]);
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            if (rw.hl[r]) {
-                sl[r] = fmax(fma(alpha, dsl[r], sl[r]), 1e-300);
-                zl[r] = fmax(fma(alpha, dzl[r], zl[r]), 1e-300);
-            }
-            if (rw.hu[r]) {
-                su[r] = fmax(fma(alpha, dsu[r], su[r]), 1e-300);
-                zu[r] = fmax(fma(alpha, dzu[r], zu[r]), 1e-300);
-            }
+            sl[r] = fmax(fma(alpha, dsl[r], sl[r]), 1e-300);
+            su[r] = fmax(fma(alpha, dsu[r], su[r]), 1e-300);
+            zl[r] = rw.ml[r] * fmax(fma(alpha, dzl[r], zl[r]), 1e-300);
+            zu[r] = rw.mu[r] * fmax(fma(alpha, dzu[r], zu[r]), 1e-300);
         }
+        rd_track *= (1.0 - alpha);
+        if (it % 8 == 7) rd_exact = true;  // refresh against rounding drift
     }
     return out;
 }
 
-
 // Phase 1 (feasibility): minimal uniform violation
 //     t* = min_{y, t >= 0} t   s.t.  lo_i - t <= g_i^T y <= hi_i + t
-// solved by the same Mehrotra scheme in the (y, t) space (tiny ridge eps/2 |y|^2 keeps the
+// solved by the same Mehrotra scheme in the (y, t) space (a tiny ridge eps/2 |y|^2 keeps the
 // Newton matrix definite). The QP is INFEASIBLE iff t* exceeds the feasibility tolerance --
 // the decision a 1e-6 row-violation tolerance (CPLEX's default) makes, and the rule the oracle
 // applies (oracle/oracle.cpp phase1). Only run for QPs whose main solve did not converge.
@@ -304,49 +340,45 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
     constexpr int NV = NZ + 1;
     using S = Sym<NV>;
     constexpr double eps = 1e-10;
-    double v[NV];
+    double y[NZ], t;
 #pragma unroll
-    for (int i = 0; i < NV; i++) v[i] = 0.0;
-    // t0 = max violation at y = 0, plus one
+    for (int i = 0; i < NZ; i++) y[i] = 0.0;
     double viol = 0.0;
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-        if (rw.hl[r]) viol = fmax(viol, rw.lo[r]);
-        if (rw.hu[r]) viol = fmax(viol, -rw.hi[r]);
-    }
-    v[NZ] = grp_max<G>(viol) + 1.0;
+    for (int r = 0; r < R; r++) viol = fmax(viol, fmax(rw.ml[r] * rw.lo[r], -rw.mu[r] * rw.hi[r]));
+    t = grp_max<G>(viol) + 1.0;
+    // sides: lower a_l = (g, 1), s_l = g y + t - lo ; upper a_u = (-g, 1), s_u = hi - g y + t ;
+    // plus t >= 0 (uniform, s_t = t exactly)
     double sl[R], su[R], zl[R], zu[R];
-    double nsides = 1.0;  // the t >= 0 side (uniform, tracked by every lane)
-    double st_ = v[NZ], zt = 1.0 / st_;
     double nloc = 0.0;
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        sl[r] = rw.hl[r] ? v[NZ] - rw.lo[r] : 1.0;
-        su[r] = rw.hu[r] ? rw.hi[r] + v[NZ] : 1.0;
-        zl[r] = rw.hl[r] ? 1.0 / sl[r] : 0.0;
-        zu[r] = rw.hu[r] ? 1.0 / su[r] : 0.0;
-        nloc += (rw.hl[r] ? 1.0 : 0.0) + (rw.hu[r] ? 1.0 : 0.0);
+        sl[r] = rw.ml[r] > 0.0 ? t - rw.lo[r] : 1.0;
+        su[r] = rw.mu[r] > 0.0 ? rw.hi[r] + t : 1.0;
+        zl[r] = rw.ml[r] * rcp(sl[r]);
+        zu[r] = rw.mu[r] * rcp(su[r]);
+        nloc += rw.ml[r] + rw.mu[r];
     }
-    nsides += grp_sum<G>(nloc);
-    const double inv_ns = 1.0 / nsides;
+    double zt = rcp(t);
+    const double inv_ns = rcp(grp_sum<G>(nloc) + 1.0);
     for (int it = 0; it < 2 * cfg.maxit; it++) {
         constexpr int NA = S::P + NV + 1;
         double acc[NA];
 #pragma unroll
         for (int k = 0; k < NA; k++) acc[k] = 0.0;
-        double rsl[R], rsu[R], Dl[R], Du[R];
+        double rsl[R], rsu[R], Dl[R], Du[R], isl[R], isu[R];
         double rp = 0.0;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const double t = dotz<NZ>(rw.g[r], *reinterpret_cast<const double(*)[NZ]>(v));
-            rsl[r] = rw.hl[r] ? (t + v[NZ] - rw.lo[r] - sl[r]) : 0.0;
-            rsu[r] = rw.hu[r] ? (rw.hi[r] - t + v[NZ] - su[r]) : 0.0;
-            Dl[r] = zl[r] / sl[r];
-            Du[r] = zu[r] / su[r];
-            // side vectors a_l = (g, 1), a_u = (-g, 1); affine rhs term a (z + (rc - z rs)/s)
-            // = -a D rs with rc = -s z (the +a z part cancels the -r_d dual term)
-            const double wl = rw.hl[r] ? -Dl[r] * rsl[r] : 0.0;
-            const double wu = rw.hu[r] ? -Du[r] * rsu[r] : 0.0;
+            const double gy = dotz<NZ>(rw.g[r], y);
+            rsl[r] = rw.ml[r] * (gy + t - rw.lo[r] - sl[r]);
+            rsu[r] = rw.mu[r] * (rw.hi[r] - gy + t - su[r]);
+            isl[r] = rcp(sl[r]);
+            isu[r] = rcp(su[r]);
+            Dl[r] = zl[r] * isl[r];
+            Du[r] = zu[r] * isu[r];
+            // affine rhs term: -a D rs (the dual +a z part cancels the -r_d term)
+            const double wl = -Dl[r] * rsl[r], wu = -Du[r] * rsu[r];
             const double Ds = Dl[r] + Du[r], Dd = Dl[r] - Du[r];
 #pragma unroll
             for (int i = 0; i < NZ; i++) {
@@ -358,18 +390,17 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
             }
             acc[S::idx(NZ, NZ)] += Ds;
             acc[S::P + NZ] += wl + wu;
-            acc[NA - 1] += sl[r] * zl[r] + su[r] * zu[r];
-            if (rw.hl[r]) rp = fmax(rp, fabs(rsl[r]) / (1.0 + fabs(rw.lo[r])));
-            if (rw.hu[r]) rp = fmax(rp, fabs(rsu[r]) / (1.0 + fabs(rw.hi[r])));
+            acc[NA - 1] = fma(sl[r], zl[r], fma(su[r], zu[r], acc[NA - 1]));
+            rp = fmax(rp, fmax(fabs(rsl[r]) * rw.ml[r] * rcp(1.0 + fabs(rw.lo[r])),
+                               fabs(rsu[r]) * rw.mu[r] * rcp(1.0 + fabs(rw.hi[r]))));
         }
         grp_sum_vec<G, NA>(acc);
         rp = grp_max<G>(rp);
-        // affine rhs = -(eps y, 1) - sum_j a_j D_j rs_j  (rs of the t >= 0 side is exactly 0)
-        const double mu = (acc[NA - 1] + st_ * zt) * inv_ns;
+        const double mu = (acc[NA - 1] + t * zt) * inv_ns;
         if (!isfinite(mu) || !isfinite(rp)) return 1e300;
         if (rp <= cfg.tol && mu <= cfg.tol * 0.1) break;
         double M[S::P], dinv[NV], rhs[NV], dv[NV];
-        const double Dt = zt / st_;
+        const double Dt = zt * rcp(t);
 #pragma unroll
         for (int k = 0; k < S::P; k++) M[k] = acc[k];
 #pragma unroll
@@ -377,51 +408,53 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
         M[S::idx(NZ, NZ)] += Dt;
         if (!chol_packed<NV>(M, dinv)) return 1e300;
 #pragma unroll
-        for (int i = 0; i < NZ; i++) rhs[i] = -eps * v[i] + acc[S::P + i];
+        for (int i = 0; i < NZ; i++) rhs[i] = -eps * y[i] + acc[S::P + i];
         rhs[NZ] = -1.0 + acc[S::P + NZ];
-        // predictor
         chol_solve<NV>(M, dinv, rhs, dv);
         double ap = 1.0, ad = 1.0, dsla[R], dzla[R], dsua[R], dzua[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const double td = dotz<NZ>(rw.g[r], *reinterpret_cast<const double(*)[NZ]>(dv));
-            dsla[r] = rw.hl[r] ? td + dv[NZ] + rsl[r] : 0.0;
-            dsua[r] = rw.hu[r] ? -td + dv[NZ] + rsu[r] : 0.0;
-            dzla[r] = rw.hl[r] ? -zl[r] - Dl[r] * dsla[r] : 0.0;
-            dzua[r] = rw.hu[r] ? -zu[r] - Du[r] * dsua[r] : 0.0;
-            if (dsla[r] < 0.0) ap = fmin(ap, -sl[r] / dsla[r]);
-            if (dsua[r] < 0.0) ap = fmin(ap, -su[r] / dsua[r]);
-            if (dzla[r] < 0.0) ad = fmin(ad, -zl[r] / dzla[r]);
-            if (dzua[r] < 0.0) ad = fmin(ad, -zu[r] / dzua[r]);
+            double dgy = 0.0;
+#pragma unroll
+            for (int i = 0; i < NZ; i++) dgy = fma(rw.g[r][i], dv[i], dgy);
+            dsla[r] = rw.ml[r] * (dgy + dv[NZ] + rsl[r]);
+            dsua[r] = rw.mu[r] * (-dgy + dv[NZ] + rsu[r]);
+            dzla[r] = -zl[r] - Dl[r] * dsla[r];
+            dzua[r] = -zu[r] - Du[r] * dsua[r];
+            ap = fmin(ap, fmin(step_bound(sl[r], dsla[r], 1.0), step_bound(su[r], dsua[r], 1.0)));
+            ad = fmin(ad, fmin(step_bound(zl[r], dzla[r], 1.0), step_bound(zu[r], dzua[r], 1.0)));
         }
         const double dsta = dv[NZ], dzta = -zt - Dt * dsta;
-        if (dsta < 0.0) ap = fmin(ap, -st_ / dsta);
-        if (dzta < 0.0) ad = fmin(ad, -zt / dzta);
+        ap = fmin(ap, step_bound(t, dsta, 1.0));
+        ad = fmin(ad, step_bound(zt, dzta, 1.0));
         ap = grp_min<G>(ap);
         ad = grp_min<G>(ad);
         double mua = 0.0;
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            if (rw.hl[r]) mua += (sl[r] + ap * dsla[r]) * (zl[r] + ad * dzla[r]);
-            if (rw.hu[r]) mua += (su[r] + ap * dsua[r]) * (zu[r] + ad * dzua[r]);
+            mua = fma(sl[r] + ap * dsla[r], zl[r] + ad * dzla[r], mua);
+            mua = fma(su[r] + ap * dsua[r], zu[r] + ad * dzua[r], mua);
         }
-        mua = (grp_sum<G>(mua) + (st_ + ap * dsta) * (zt + ad * dzta)) * inv_ns;
-        double sig = mu > 0.0 ? mua / mu : 0.0;
+        mua = (grp_sum<G>(mua) + (t + ap * dsta) * (zt + ad * dzta)) * inv_ns;
+        double sig = mu > 0.0 ? mua * rcp(mu) : 0.0;
         sig = fmin(sig * sig * sig, 1.0);
         const double smu = sig * mu;
         double vc[NV];
 #pragma unroll
         for (int i = 0; i < NV; i++) vc[i] = 0.0;
+        double cl[R], cu[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const double cl = rw.hl[r] ? (smu - dsla[r] * dzla[r]) / sl[r] : 0.0;
-            const double cu = rw.hu[r] ? (smu - dsua[r] * dzua[r]) / su[r] : 0.0;
+            cl[r] = rw.ml[r] * (smu - dsla[r] * dzla[r]);
+            cu[r] = rw.mu[r] * (smu - dsua[r] * dzua[r]);
+            const double a = cl[r] * isl[r], b = cu[r] * isu[r];
 #pragma unroll
-            for (int i = 0; i < NZ; i++) vc[i] = fma(rw.g[r][i], cl - cu, vc[i]);
-            vc[NZ] += cl + cu;
+            for (int i = 0; i < NZ; i++) vc[i] = fma(rw.g[r][i], a - b, vc[i]);
+            vc[NZ] += a + b;
         }
         grp_sum_vec<G, NV>(vc);
-        vc[NZ] += (smu - dsta * dzta) / st_;
+        const double ct = smu - dsta * dzta;
+        vc[NZ] += ct * rcp(t);
         double dvc[NV];
         chol_solve<NV>(M, dinv, vc, dvc);
 #pragma unroll
@@ -429,45 +462,40 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
         double amax = 1e300, dsl[R], dzl[R], dsu[R], dzu[R];
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            const double td = dotz<NZ>(rw.g[r], *reinterpret_cast<const double(*)[NZ]>(dv));
-            dsl[r] = rw.hl[r] ? td + dv[NZ] + rsl[r] : 0.0;
-            dsu[r] = rw.hu[r] ? -td + dv[NZ] + rsu[r] : 0.0;
-            dzl[r] = rw.hl[r] ? (smu - sl[r] * zl[r] - dsla[r] * dzla[r] - zl[r] * dsl[r]) / sl[r] : 0.0;
-            dzu[r] = rw.hu[r] ? (smu - su[r] * zu[r] - dsua[r] * dzua[r] - zu[r] * dsu[r]) / su[r] : 0.0;
-            if (dsl[r] < 0.0) amax = fmin(amax, -sl[r] / dsl[r]);
-            if (dsu[r] < 0.0) amax = fmin(amax, -su[r] / dsu[r]);
-            if (dzl[r] < 0.0) amax = fmin(amax, -zl[r] / dzl[r]);
-            if (dzu[r] < 0.0) amax = fmin(amax, -zu[r] / dzu[r]);
+            double dgy = 0.0;
+#pragma unroll
+            for (int i = 0; i < NZ; i++) dgy = fma(rw.g[r][i], dv[i], dgy);
+            dsl[r] = rw.ml[r] * (dgy + dv[NZ] + rsl[r]);
+            dsu[r] = rw.mu[r] * (-dgy + dv[NZ] + rsu[r]);
+            dzl[r] = (cl[r] - sl[r] * zl[r] - zl[r] * dsl[r]) * isl[r];
+            dzu[r] = (cu[r] - su[r] * zu[r] - zu[r] * dsu[r]) * isu[r];
+            amax = fmin(amax, fmin(step_bound(sl[r], dsl[r], 1e300), step_bound(su[r], dsu[r], 1e300)));
+            amax = fmin(amax, fmin(step_bound(zl[r], rw.ml[r] * dzl[r], 1e300),
+                                   step_bound(zu[r], rw.mu[r] * dzu[r], 1e300)));
         }
         const double dst = dv[NZ];
-        const double dzt = (smu - st_ * zt - dsta * dzta - zt * dst) / st_;
-        if (dst < 0.0) amax = fmin(amax, -st_ / dst);
-        if (dzt < 0.0) amax = fmin(amax, -zt / dzt);
+        const double dzt = (ct - t * zt - zt * dst) * rcp(t);
+        amax = fmin(amax, fmin(step_bound(t, dst, 1e300), step_bound(zt, dzt, 1e300)));
         amax = grp_min<G>(amax);
         const double alpha = fmin(1.0, 0.99 * amax);
 #pragma unroll
-        for (int i = 0; i < NV; i++) v[i] = fma(alpha, dv[i], v[i]);
+        for (int i = 0; i < NZ; i++) y[i] = fma(alpha, dv[i], y[i]);
+        t = fmax(fma(alpha, dst, t), 1e-300);
+        zt = fmax(fma(alpha, dzt, zt), 1e-300);
 #pragma unroll
         for (int r = 0; r < R; r++) {
-            if (rw.hl[r]) {
-                sl[r] = fmax(fma(alpha, dsl[r], sl[r]), 1e-300);
-                zl[r] = fmax(fma(alpha, dzl[r], zl[r]), 1e-300);
-            }
-            if (rw.hu[r]) {
-                su[r] = fmax(fma(alpha, dsu[r], su[r]), 1e-300);
-                zu[r] = fmax(fma(alpha, dzu[r], zu[r]), 1e-300);
-            }
+            sl[r] = fmax(fma(alpha, dsl[r], sl[r]), 1e-300);
+            su[r] = fmax(fma(alpha, dsu[r], su[r]), 1e-300);
+            zl[r] = rw.ml[r] * fmax(fma(alpha, dzl[r], zl[r]), 1e-300);
+            zu[r] = rw.mu[r] * fmax(fma(alpha, dzu[r], zu[r]), 1e-300);
         }
-        st_ = fmax(fma(alpha, dst, st_), 1e-300);
-        zt = fmax(fma(alpha, dzt, zt), 1e-300);
     }
     // t* from the iterate: the largest actual row violation at y (>= 0)
     double worst = 0.0;
 #pragma unroll
     for (int r = 0; r < R; r++) {
-        const double t = dotz<NZ>(rw.g[r], *reinterpret_cast<const double(*)[NZ]>(v));
-        if (rw.hl[r]) worst = fmax(worst, rw.lo[r] - t);
-        if (rw.hu[r]) worst = fmax(worst, t - rw.hi[r]);
+        const double gy = dotz<NZ>(rw.g[r], y);
+        worst = fmax(worst, fmax(rw.ml[r] * (rw.lo[r] - gy), rw.mu[r] * (gy - rw.hi[r])));
     }
     return grp_max<G>(worst);
 }

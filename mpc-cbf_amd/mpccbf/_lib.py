@@ -69,7 +69,7 @@ class Batch(C.Structure):
         ("num_agents", C.c_int32), ("targets", C.c_void_p), ("refs", C.c_void_p),
         ("nb_row_ptr", C.c_void_p), ("nb_col", C.c_void_p), ("x", C.c_void_p),
         ("status", C.c_void_p), ("obj", C.c_void_p), ("iters", C.c_void_p),
-        ("next_states", C.c_void_p),
+        ("next_states", C.c_void_p), ("knn_k", C.c_int32), ("knn_radius", C.c_double),
     ]
 
 
@@ -179,16 +179,18 @@ class Context:
                                              k, float(radius), _ptr(row_ptr), _ptr(col),
                                              _stream(stream)))
 
-    def impc_solve(self, states, nb_row_ptr, nb_col, targets=None, refs=None, agent_first=0,
-                   num_agents=None, x=None, status=None, obj=None, iters=None, next_states=None,
-                   stream=None):
+    def impc_solve(self, states, nb_row_ptr=None, nb_col=None, targets=None, refs=None,
+                   agent_first=0, num_agents=None, x=None, status=None, obj=None, iters=None,
+                   next_states=None, knn_k=0, knn_radius=0.0, stream=None):
+        """CSR neighbours (nb_row_ptr/nb_col) or, with both None, the knn_k nearest within
+        knn_radius found on the device in the same launch sequence."""
         if num_agents is None:
             num_agents = states.shape[0] - agent_first
         b = Batch(num_states=states.shape[0], states=_ptr(states), agent_first=agent_first,
                   num_agents=num_agents, targets=_ptr(targets), refs=_ptr(refs),
                   nb_row_ptr=_ptr(nb_row_ptr), nb_col=_ptr(nb_col), x=_ptr(x),
                   status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters),
-                  next_states=_ptr(next_states))
+                  next_states=_ptr(next_states), knn_k=int(knn_k), knn_radius=float(knn_radius))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
 
     def alloc_outputs(self, num_agents: int, device=None):

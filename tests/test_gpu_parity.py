@@ -151,3 +151,28 @@ def test_device_knn_matches_cpu(mpclib):
     rp_h = rp.cpu().numpy()
     np.testing.assert_array_equal(rp_h, rp_ref)
     np.testing.assert_array_equal(col.cpu().numpy()[: rp_h[-1]], col_ref)
+
+
+def test_grid_neighbours_match_csr(mpclib):
+    """Fused device neighbour query (spatial hash + in-kernel 3x3 cells) == CSR path with the CPU
+    k-nearest lists, on a swarm where several CBF rows are active."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(400, seed=11)
+    states[:, :2] *= 0.55  # 2.75 m spacing: close neighbours, non-redundant CBF rows
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    ctx = mpclib.Context(cfg)
+    g_csr = run_gpu(ctx, states, targets, rp, col, torch)
+    dev = torch.device("cuda", 0)
+    out = ctx.alloc_outputs(len(states))
+    ctx.impc_solve(torch.tensor(states, device=dev), targets=torch.tensor(targets, device=dev),
+                   knn_k=8, knn_radius=6.0, **out)
+    torch.cuda.synchronize()
+    g = {k: v.cpu().numpy() for k, v in out.items()}
+    np.testing.assert_array_equal(g["status"], g_csr["status"])
+    ok = g["status"] == 0
+    np.testing.assert_allclose(g["obj"][ok], g_csr["obj"][ok], rtol=1e-10, atol=1e-9)
+    # and against the oracle on a sample of agents
+    agents = list(range(0, 400, 13))
+    ref = run_oracle(cfg, states, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
