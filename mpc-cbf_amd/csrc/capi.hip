@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../include/mpccbf.h"
+#include "host/errors.hpp"
 #include "host/operators.hpp"
 #include "kernels/impc.hpp"
 
@@ -27,10 +28,12 @@ uint32_t launch_grid_build(const double* states, int n, double radius, void* scr
 
 static thread_local std::string g_err;
 
-static int fail(int code, const std::string& msg) {
+int set_error(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+
+static int fail(int code, const std::string& msg) { return set_error(code, msg); }
 
 #define HIP_TRY(expr)                                                                       \
     do {                                                                                    \
@@ -264,12 +267,3 @@ int mpccbf_build_neighbors(mpccbf_ctx* c, const double* states, int32_t num_stat
 
 }  // extern "C"
 
-extern "C" {
-// Implemented in dense_qp.hip (generic flattened-CPLEX QP path); placeholders until then.
-int mpccbf_qp_solve_dense(const mpccbf_dense_qp*, double*, double*, int32_t*) {
-    return fail(MPCCBF_ERR_INTERNAL, "dense path not built");
-}
-int mpccbf_qp_solve_dense_batch(int32_t, const mpccbf_dense_qp*, double* const*, double*, int32_t*) {
-    return fail(MPCCBF_ERR_INTERNAL, "dense path not built");
-}
-}

@@ -96,6 +96,7 @@ struct Rows {
 struct PdipCfg {
     int maxit;
     double tol;
+    double reg = 0.0;  // added to the Newton matrix diagonal (direction only; residuals exact)
 };
 
 struct PdipOut {
@@ -108,14 +109,18 @@ __device__ __forceinline__ double step_bound(double s, double ds, double big) {
     return ds < 0.0 ? -s * rcp(ds) : big;
 }
 
-// P: NZ x NZ row-major, LP: lower Cholesky factor of P (row-major); both uniform (global).
+// P: NZ x NZ row-major, LP: lower Cholesky factor of P (row-major) or nullptr when P is only
+// positive semidefinite (generic dense path); uniform per group (global).
 template <int NZ, int G, int R>
 __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ P,
                               const double* __restrict__ LP, const double (&q)[NZ],
                               double (&y)[NZ], const PdipCfg cfg) {
     using S = Sym<NZ>;
-    // ---- start: y0 = argmin of the unconstrained objective (P is SPD on the reduced space)
-    {
+    // ---- start: y0 = argmin of the unconstrained objective when P is SPD (LP given), else 0
+    if (LP == nullptr) {
+#pragma unroll
+        for (int i = 0; i < NZ; i++) y[i] = 0.0;
+    } else {
         double w[NZ];
 #pragma unroll
         for (int i = 0; i < NZ; i++) {
@@ -247,6 +252,8 @@ __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ 
         for (int i = 0; i < NZ; i++)
 #pragma unroll
             for (int j = i; j < NZ; j++) M[S::idx(i, j)] = acc[S::idx(i, j)] + P[i * NZ + j];
+#pragma unroll
+        for (int i = 0; i < NZ; i++) M[S::idx(i, i)] += cfg.reg;
         if (!chol_packed<NZ>(M, dinv)) {
             out.status = ST_UNKNOWN;  // numerically singular: phase 1 decides feasibility
             break;

@@ -96,6 +96,14 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MpccbfError(f"{LIB_PATH} not built: run `make -C mpc-cbf_amd` (no CPU fallback)")
+    # torch ships its own libamdhip64 (soname libamdhip64.so.7, the one libmpccbf needs). Load
+    # torch first so the dynamic loader binds libmpccbf to that same HIP runtime: one runtime per
+    # process, so torch's device pointers, streams and events are valid handles for the library.
+    # (Loading libmpccbf first would pull /opt/rocm's copy and leave torch with a second one.)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp = C.c_void_p
     L.mpccbf_create.argtypes = [C.POINTER(Params), C.POINTER(Options), C.POINTER(vp)]
@@ -258,3 +266,38 @@ def dense_qp_solve(H, c, A, lo, hi, vlo=None, vhi=None, c0=0.0):
     st = np.zeros(1, dtype=np.int32)
     _check(L.mpccbf_qp_solve_dense(C.byref(qp), x.ctypes.data, obj.ctypes.data, st.ctypes.data))
     return int(st[0]), x, float(obj[0])
+
+
+def dense_qp_solve_batch(qps):
+    """Batched generic dense QPs (mpccbf_qp_solve_dense_batch): one launch for all of them.
+    qps: list of dicts with H, c, A, lo, hi and optional vlo, vhi, c0. Returns
+    (status[count], list of x (None unless OPTIMAL), obj[count])."""
+    L = load()
+    keep = []  # hold the arrays alive for the call
+    arr = (DenseQP * max(len(qps), 1))()
+    xs = []
+    for k, q in enumerate(qps):
+        c = np.ascontiguousarray(q["c"], dtype=np.float64)
+        n = c.shape[0]
+        H = np.ascontiguousarray(q["H"], dtype=np.float64).reshape(n, n)
+        A = np.ascontiguousarray(q.get("A", np.zeros((0, n))), dtype=np.float64).reshape(-1, n)
+        lo = np.ascontiguousarray(q.get("lo", np.zeros(0)), dtype=np.float64)
+        hi = np.ascontiguousarray(q.get("hi", np.zeros(0)), dtype=np.float64)
+        vlo = q.get("vlo")
+        vhi = q.get("vhi")
+        vlo = None if vlo is None else np.ascontiguousarray(vlo, dtype=np.float64)
+        vhi = None if vhi is None else np.ascontiguousarray(vhi, dtype=np.float64)
+        keep += [c, H, A, lo, hi, vlo, vhi]
+        arr[k] = DenseQP(n=n, m=A.shape[0], H=H.ctypes.data, c=c.ctypes.data, c0=q.get("c0", 0.0),
+                         A=A.ctypes.data if A.size else None, lo=lo.ctypes.data if lo.size else None,
+                         hi=hi.ctypes.data if hi.size else None,
+                         vlo=None if vlo is None else vlo.ctypes.data,
+                         vhi=None if vhi is None else vhi.ctypes.data)
+        xs.append(np.full(n, np.nan))
+    xptr = (C.c_void_p * max(len(qps), 1))(*[x.ctypes.data for x in xs])
+    obj = np.zeros(max(len(qps), 1))
+    st = np.zeros(max(len(qps), 1), dtype=np.int32)
+    _check(L.mpccbf_qp_solve_dense_batch(len(qps), arr, C.cast(xptr, C.c_void_p), obj.ctypes.data,
+                                         st.ctypes.data))
+    n = len(qps)
+    return st[:n], [xs[k] if st[k] == 0 else None for k in range(n)], obj[:n]

@@ -1,0 +1,104 @@
+"""Generic dense-QP boundary (mpccbf_qp_solve_dense*), the path a qpcpp::Solver<double> adapter
+uses in place of CPLEXSolver::solve (qpcpp/src/solvers/CPLEX.cpp:35-177).
+
+CPU tests: argument validation happens before any device work, and a valid QP without a GPU
+fails loudly (no CPU fallback). GPU tests: the CPLEXTest toy (qpcpp/tests/CPLEXTest.cpp:28-56),
+the 42 golden MPC-CBF QPs in their full (un-condensed) CPLEX form, and status cases.
+"""
+import os
+
+import numpy as np
+import pytest
+
+INF = np.finfo(np.float64).max  # numeric_limits<double>::max() as qpcpp::Problem uses it
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden_qps.npz")
+
+
+def toy():
+    # min x^2 + y^2  s.t.  x + y >= 1   (CPLEXTest.cpp:34-47)
+    return dict(H=np.eye(2), c=np.zeros(2), A=np.array([[1.0, 1.0]]), lo=np.array([1.0]),
+                hi=np.array([INF]))
+
+
+def test_dense_invalid_arguments_rejected_on_host(mpclib):
+    bad = dict(H=np.eye(2), c=np.array([0.0, np.nan]))
+    with pytest.raises(mpclib.MpccbfError, match="non-finite"):
+        mpclib.dense_qp_solve_batch([bad])
+    bad = dict(H=np.eye(2), c=np.zeros(2), A=np.array([[1.0, 1.0]]), lo=np.array([np.nan]),
+               hi=np.array([1.0]))
+    with pytest.raises(mpclib.MpccbfError, match="NaN"):
+        mpclib.dense_qp_solve_batch([bad])
+
+
+def test_dense_without_gpu_fails_loudly(mpclib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(mpclib.MpccbfError, match="no HIP device"):
+        mpclib.dense_qp_solve_batch([toy()])
+
+
+def test_dense_fully_determined_needs_no_solve(mpclib):
+    # equalities pin x completely: decided during elimination, no device launch
+    q = dict(H=np.eye(2), c=np.array([1.0, 0.0]), A=np.eye(2), lo=np.array([1.0, 2.0]),
+             hi=np.array([1.0, 2.0]))
+    st, xs, obj = mpclib.dense_qp_solve_batch([q])
+    assert st[0] == mpclib.OPTIMAL
+    np.testing.assert_allclose(xs[0], [1.0, 2.0])
+    assert abs(obj[0] - (1 + 4 + 1)) < 1e-12
+    q["lo"] = np.array([1.0, 2.0])
+    q["A"] = np.array([[1.0, 0.0], [1.0, 0.0]])  # x = 1 and x = 2: inconsistent
+    st, xs, _ = mpclib.dense_qp_solve_batch([q])
+    assert st[0] == mpclib.INFEASIBLE and xs[0] is None
+
+
+@pytest.mark.gpu
+def test_cplex_toy(mpclib):
+    st, x, obj = mpclib.dense_qp_solve(**toy())
+    assert st == mpclib.OPTIMAL
+    np.testing.assert_allclose(x, [0.5, 0.5], atol=1e-6)  # CPLEXTest.cpp:53-54 tolerance
+    assert abs(obj - 0.5) < 1e-8
+
+
+@pytest.mark.gpu
+def test_dense_status_cases(mpclib):
+    qps = [
+        toy(),
+        # infeasible: x >= 1 and x <= 0
+        dict(H=np.eye(1), c=np.zeros(1), A=np.array([[1.0], [1.0]]), lo=np.array([1.0, -INF]),
+             hi=np.array([INF, 0.0])),
+        # unbounded LP: min -x, x >= 0
+        dict(H=np.zeros((1, 1)), c=np.array([-1.0]), vlo=np.array([0.0]), vhi=np.array([INF])),
+        # equality only: min x^2 + y^2 s.t. x + y = 1
+        dict(H=np.eye(2), c=np.zeros(2), A=np.array([[1.0, 1.0]]), lo=np.array([1.0]),
+             hi=np.array([1.0])),
+        # LP with a bounded optimum (P = 0): min x + y, 0 <= x, y <= 3, x + y >= 2
+        dict(H=np.zeros((2, 2)), c=np.ones(2), A=np.array([[1.0, 1.0]]), lo=np.array([2.0]),
+             hi=np.array([INF]), vlo=np.zeros(2), vhi=np.full(2, 3.0)),
+        # variable bounds active: min (x - 5)^2 with x <= 2  -> x = 2, obj = x^2 - 10 x + 25 = 9
+        dict(H=np.eye(1), c=np.array([-10.0]), c0=25.0, vlo=np.array([-INF]), vhi=np.array([2.0])),
+    ]
+    st, xs, obj = mpclib.dense_qp_solve_batch(qps)
+    assert list(st) == [mpclib.OPTIMAL, mpclib.INFEASIBLE, mpclib.UNBOUNDED, mpclib.OPTIMAL,
+                        mpclib.OPTIMAL, mpclib.OPTIMAL]
+    np.testing.assert_allclose(xs[3], [0.5, 0.5], atol=1e-9)
+    assert abs(obj[4] - 2.0) < 1e-7 and abs(xs[4].sum() - 2.0) < 1e-7
+    np.testing.assert_allclose(xs[5], [2.0], atol=1e-8)
+    assert abs(obj[5] - 9.0) < 1e-7
+    assert xs[1] is None and xs[2] is None
+
+
+@pytest.mark.gpu
+def test_dense_golden_mpc_qps(mpclib):
+    """Every golden MPC-CBF QP in its full CPLEX form (36 variables, 30 equalities, box + CBF
+    rows) through the generic path: same optimum as the independent solver + KKT certificate."""
+    g = np.load(GOLDEN)
+    count = int(g["count"])
+    qps = [dict(H=g[f"c{i}_H"], c=g[f"c{i}_c"], A=g[f"c{i}_A"], lo=g[f"c{i}_lo"], hi=g[f"c{i}_hi"])
+           for i in range(count)]
+    st, xs, obj = mpclib.dense_qp_solve_batch(qps)
+    for i in range(count):
+        assert st[i] == mpclib.OPTIMAL, (i, st[i])
+        ref = float(g[f"c{i}_obj"])
+        assert abs(obj[i] - ref) <= 1e-4 * max(1.0, abs(ref)), (i, obj[i], ref)
+        assert np.max(np.abs(xs[i] - g[f"c{i}_x"])) <= 1e-5
