@@ -33,8 +33,8 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--agents-per-gpu", type=int, default=4096)
     ap.add_argument("--agents-total", type=int, default=0, help="strong scaling: fixed total")
     ap.add_argument("--k-hor", type=int, default=15)
@@ -63,6 +63,7 @@ def main():
     import torch
     import torch.distributed as dist
     from mpccbf import swarm, Context
+    from mpccbf.dist import SwarmShard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -86,9 +87,9 @@ def main():
     ctx = Context(cfg, device=local)
     ctx.set_variant(args.variant)
 
-    states = torch.tensor(states_h, dtype=torch.float64, device=dev)
+    shard = SwarmShard(torch.tensor(states_h, dtype=torch.float64, device=dev), world, rank)
+    states, local_states = shard.full, shard.local
     targets = torch.tensor(targets_h[first:first + per], dtype=torch.float64, device=dev)
-    local_states = states[first:first + per].clone()
     nb_rp = torch.empty(per + 1, dtype=torch.int32, device=dev)
     nb_col = torch.empty(per * max(args.knn, 1), dtype=torch.int32, device=dev)
     out = ctx.alloc_outputs(per, device=dev)
@@ -105,10 +106,7 @@ def main():
         return dict(knn_k=args.knn, knn_radius=radius)  # fused device grid query
 
     def step(slot: int | None):
-        if world > 1:
-            dist.all_gather_into_tensor(states, local_states)
-        else:
-            states.copy_(local_states)
+        shard.exchange()  # RCCL all-gather of agent states (copy at N=1)
         nb = neighbours()
         st = status_log[slot] if slot is not None else out["status"]
         it = iters_log[slot] if slot is not None else out["iters"]
@@ -127,10 +125,7 @@ def main():
            for _ in range(nsteps)]
 
     def step_timed(i):
-        if world > 1:
-            dist.all_gather_into_tensor(states, local_states)
-        else:
-            states.copy_(local_states)
+        shard.exchange()  # RCCL all-gather of agent states (copy at N=1)
         nb = neighbours()
         kev[i][0].record(stream)
         ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
