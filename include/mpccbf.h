@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 2
+#define MPCCBF_ABI_VERSION 3
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -123,7 +123,10 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *   iters       num_agents x impc_iter interior-point iterations
  *   next_states num_agents x 6: position/velocity of the kept curve at t = h (Jacobi update of
  *               the closed-loop driver, example :188-207, without noise); unchanged input if no
- *               curve was found. */
+ *               curve was found.
+ *   stamps      diagnostics, normally NULL: num_agents x 8 int64 shader-clock stamps (s_memtime)
+ *               at the kernel's phase boundaries (start, setup, neighbours, CBF rows 0, solve 0,
+ *               CBF rows 1, solve 1, end). */
 typedef struct mpccbf_batch {
     int32_t num_states;
     const double* states;
@@ -140,6 +143,7 @@ typedef struct mpccbf_batch {
     double* next_states;
     int32_t knn_k;
     double knn_radius;
+    int64_t* stamps;
 } mpccbf_batch;
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);

@@ -3,6 +3,7 @@
 // become MPCCBF_ERR_INVALID_ARGUMENT plus a thread-local message).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -146,6 +147,41 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     pack(v, d.o_PS, o.PS);
     pack(v, d.o_AZ, o.AZ);
     pack(v, d.o_AS, o.AS);
+    // separable layout: box rows regrouped by channel, 16 per channel (lanes of a group)
+    d.sep = 0;
+    d.o_Gsep = 0;
+    if (o.sep && o.nzd == SEP_NZD_HOST) {
+        int per[DIM] = {0, 0, 0};
+        bool ok = true;
+        for (int i = 0; i < o.G.r; i++) {
+            if (o.row_dim[i] < 0 || o.row_dim[i] >= DIM) ok = false;
+            else per[o.row_dim[i]]++;
+            if (!(o.lo[i] > -1e300 && o.hi[i] < 1e300)) ok = false;  // the layout is two-sided only
+        }
+        const int rpd = std::max(per[0], std::max(per[1], per[2]));
+        if (ok && rpd <= 16) {
+            std::vector<double> B((size_t)DIM * 16 * SEP_ROW, 0.0);
+            for (int dd = 0; dd < DIM; dd++)
+                for (int l = 0; l < 16; l++) {
+                    B[((size_t)dd * 16 + l) * SEP_ROW + 8] = -1.0;  // inert row: 0 in [-1, 1]
+                    B[((size_t)dd * 16 + l) * SEP_ROW + 9] = 1.0;
+                }
+            int fill[DIM] = {0, 0, 0};
+            for (int i = 0; i < o.G.r; i++) {
+                const int dd = o.row_dim[i], l = fill[dd]++;
+                double* r = &B[((size_t)dd * 16 + l) * SEP_ROW];
+                r[0] = o.G(i, dd * o.nzd);
+                r[1] = o.G(i, dd * o.nzd + 1);
+                for (int s = 0; s < SD; s++) r[2 + s] = o.Gs(i, s);
+                r[8] = o.lo[i];
+                r[9] = o.hi[i];
+            }
+            pack(v, d.o_Gsep, B);
+            d.sep = 1;
+            d.nzd = o.nzd;
+            d.sep_rows_per_dim = rpd;
+        }
+    }
     v.push_back(0.0);  // keep every offset addressable even for empty operators
     for (int i = 0; i < 3; i++) {
         d.a_lo[i] = o.a_lo[i];
@@ -229,6 +265,7 @@ int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
     a.obj = b->obj;
     a.iters = b->iters;
     a.next_states = b->next_states;
+    a.stamps = b->stamps;
     hipError_t e = launch_impc(c->dev, c->dbuf, a, c->variant, (hipStream_t)stream);
     if (e == hipErrorInvalidValue)
         return fail(MPCCBF_ERR_CAPACITY, "no kernel instantiation for this reduced dimension / row count");

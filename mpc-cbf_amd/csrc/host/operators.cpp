@@ -273,7 +273,50 @@ Operators build_operators(const mpccbf_params& p, bool keep_redundant) {
         for (int j = 0; j < n; j++) Ae(e, j) = eq[e][j];
     Mat Xp;
     int rank = 0;
-    null_space(Ae, 1e-12, op.Z, Xp, rank);
+    auto var_dim = [&](int j) { return (j % cv.n_piece) / cv.C; };  // layout [piece][dim][cp]
+    // separable? every equality row and every cost entry stays within one channel
+    bool sep = true;
+    std::vector<int> eq_dim(op.me, -1);
+    for (int e = 0; e < op.me && sep; e++)
+        for (int j = 0; j < n; j++) {
+            if (Ae(e, j) == 0.0) continue;
+            if (eq_dim[e] < 0) eq_dim[e] = var_dim(j);
+            else if (eq_dim[e] != var_dim(j)) sep = false;
+        }
+    for (int i = 0; i < n && sep; i++)
+        for (int j = 0; j < n; j++)
+            if (op.H(i, j) != 0.0 && var_dim(i) != var_dim(j)) sep = false;
+    if (sep) {
+        // per-channel null spaces, assembled block-diagonally (columns [x | y | yaw])
+        std::vector<Mat> Zd(DIM), Xpd(DIM);
+        std::vector<std::vector<int>> vars(DIM), rows_d(DIM);
+        for (int j = 0; j < n; j++) vars[var_dim(j)].push_back(j);
+        for (int e = 0; e < op.me; e++) rows_d[eq_dim[e] < 0 ? 0 : eq_dim[e]].push_back(e);
+        int nzd = -1;
+        for (int d = 0; d < DIM && sep; d++) {
+            Mat Ed((int)rows_d[d].size(), (int)vars[d].size());
+            for (int a = 0; a < Ed.r; a++)
+                for (int b = 0; b < Ed.c; b++) Ed(a, b) = Ae(rows_d[d][a], vars[d][b]);
+            int rk = 0;
+            null_space(Ed, 1e-12, Zd[d], Xpd[d], rk);
+            if (nzd < 0) nzd = Zd[d].c;
+            if (Zd[d].c != nzd) sep = false;  // channels must share one reduced size
+            rank += rk;
+        }
+        if (sep) {
+            op.Z = Mat(n, DIM * nzd);
+            Xp = Mat(n, op.me);
+            for (int d = 0; d < DIM; d++) {
+                for (size_t b = 0; b < vars[d].size(); b++) {
+                    for (int c = 0; c < nzd; c++) op.Z(vars[d][b], d * nzd + c) = Zd[d](b, c);
+                    for (size_t a = 0; a < rows_d[d].size(); a++) Xp(vars[d][b], rows_d[d][a]) = Xpd[d](b, a);
+                }
+            }
+            op.sep = true;
+            op.nzd = nzd;
+        }
+    }
+    if (!op.sep) null_space(Ae, 1e-12, op.Z, Xp, rank);
     // consistency: the initial-state rows must be independent of the rest (always true for
     // C >= 2); otherwise b_eq could be inconsistent for some s0.
     op.Xs = Mat(n, SD);
@@ -394,6 +437,7 @@ Operators build_operators(const mpccbf_params& p, bool keep_redundant) {
             op.lo.push_back(r.lo);
             op.hi.push_back(r.hi);
             op.row_kind.push_back(r.kind);
+            op.row_dim.push_back(r.dim);
             im++;
         }
     }

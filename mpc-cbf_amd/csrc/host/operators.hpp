@@ -32,6 +32,12 @@ struct Operators {
     Mat G, Gs;      // m x nz, m x 6 shared inequality rows (kept after exact reduction)
     std::vector<double> lo, hi;
     std::vector<int> row_kind;  // 0 accel, 1 vel (for diagnostics)
+    std::vector<int> row_dim;   // spatial dimension a kept shared row constrains (-1: several)
+    // Dimension-separable structure (base_config.json): equalities and cost never couple the
+    // x / y / yaw channels, so Z is block-diagonal with nzd columns per channel, ordered
+    // [x | y | yaw]; every shared row then touches one channel's nzd columns only.
+    bool sep = false;
+    int nzd = 0;
     Mat Cs;                     // mc x 6 constant rows
     std::vector<double> clo, chi;
     int rows_total = 0, rows_removed = 0;

@@ -22,12 +22,13 @@ constexpr int DPP_XOR2 = 0x4E;         // quad_perm(2,3,0,1)
 constexpr int DPP_HALF_MIRROR = 0x141; // row_half_mirror
 constexpr int DPP_MIRROR = 0x140;      // row_mirror
 
+// Every control used here reads a lane of the same 16-lane row that always exists, so the
+// "old" operand is never observed: mov_dpp (old = undef, bound_ctrl) lets the compiler skip
+// materialising a zero register per move.
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    return __longlong_as_double(__builtin_amdgcn_mov_dpp(b, CTRL, 0xF, 0xF, true));
 }
 
 enum class Op { Sum, Max, Min };
@@ -95,6 +96,24 @@ __device__ __forceinline__ double rcp(double x) {
     r = fma(fma(-x, r, 1.0), r, r);
     r = fma(fma(-x, r, 1.0), r, r);
     return r;
+}
+
+// Raw v_rcp_f64 (unrefined hardware estimate): only for step-length ratios, where the
+// fraction-to-boundary factor 0.99 absorbs its error.
+__device__ __forceinline__ double rcp_fast(double x) { return __builtin_amdgcn_rcp(x); }
+
+// Two independent group max-reductions, stage-interleaved.
+template <int G>
+__device__ __forceinline__ void grp_max2(double& a, double& b) {
+    static_assert(G == 16, "grp_max2: 16-lane groups");
+    a = fmax(a, dpp_mov<DPP_XOR1>(a));
+    b = fmax(b, dpp_mov<DPP_XOR1>(b));
+    a = fmax(a, dpp_mov<DPP_XOR2>(a));
+    b = fmax(b, dpp_mov<DPP_XOR2>(b));
+    a = fmax(a, dpp_mov<DPP_HALF_MIRROR>(a));
+    b = fmax(b, dpp_mov<DPP_HALF_MIRROR>(b));
+    a = fmax(a, dpp_mov<DPP_MIRROR>(a));
+    b = fmax(b, dpp_mov<DPP_MIRROR>(b));
 }
 
 // Make this wave's LDS writes visible to its other lanes before they read them.

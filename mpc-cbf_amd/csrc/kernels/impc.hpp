@@ -19,7 +19,14 @@ struct DevOps {
     int32_t maxit;
     double tol;
     double feas_tol;  // absolute row-violation tolerance for constant rows / single-row checks
+    // separable layout (impc_sep_kernel): per channel d and lane l, row l of channel d as
+    // [g0, g1, Gs(6), lo, hi] (SEP_ROW doubles), 16 rows per channel (unused: inert g = 0, [-1, 1])
+    int32_t sep, nzd, sep_rows_per_dim;
+    int32_t o_Gsep;
 };
+
+constexpr int SEP_ROW = 10;
+constexpr int SEP_NZD_HOST = 2;  // reduced variables per channel the separable kernel handles
 
 // Spatial hash of agent positions (uniform cells of edge `radius`), built by grid_build_kernel:
 // bucket h holds sorted[start[h] .. start[h+1]).
@@ -62,6 +69,9 @@ struct ImpcArgs {
     double* obj;
     int32_t* iters;
     double* next_states;
+    int64_t* stamps;  // diagnostics: num_agents x NSTAMP shader-clock stamps, or nullptr
 };
+
+constexpr int NSTAMP = 8;
 
 }  // namespace mpccbf

@@ -8,7 +8,7 @@ import subprocess
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # mpc-cbf_amd/
-LIB_PATH = os.path.join(PKG_DIR, "build", "libmpccbf.so")
+LIB_PATH = os.environ.get("MPCCBF_LIB") or os.path.join(PKG_DIR, "build", "libmpccbf.so")
 
 OPTIMAL, FEASIBLE, UNBOUNDED, INFEASIBLE, ERROR, UNKNOWN, INFEASIBLEORUNBOUNDED = range(7)
 STATUS_NAMES = ["OPTIMAL", "FEASIBLE", "UNBOUNDED", "INFEASIBLE", "ERROR", "UNKNOWN",
@@ -70,6 +70,7 @@ class Batch(C.Structure):
         ("nb_row_ptr", C.c_void_p), ("nb_col", C.c_void_p), ("x", C.c_void_p),
         ("status", C.c_void_p), ("obj", C.c_void_p), ("iters", C.c_void_p),
         ("next_states", C.c_void_p), ("knn_k", C.c_int32), ("knn_radius", C.c_double),
+        ("stamps", C.c_void_p),
     ]
 
 
@@ -189,7 +190,7 @@ class Context:
 
     def impc_solve(self, states, nb_row_ptr=None, nb_col=None, targets=None, refs=None,
                    agent_first=0, num_agents=None, x=None, status=None, obj=None, iters=None,
-                   next_states=None, knn_k=0, knn_radius=0.0, stream=None):
+                   next_states=None, knn_k=0, knn_radius=0.0, stream=None, stamps=None):
         """CSR neighbours (nb_row_ptr/nb_col) or, with both None, the knn_k nearest within
         knn_radius found on the device in the same launch sequence."""
         if num_agents is None:
@@ -198,7 +199,8 @@ class Context:
                   num_agents=num_agents, targets=_ptr(targets), refs=_ptr(refs),
                   nb_row_ptr=_ptr(nb_row_ptr), nb_col=_ptr(nb_col), x=_ptr(x),
                   status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters),
-                  next_states=_ptr(next_states), knn_k=int(knn_k), knn_radius=float(knn_radius))
+                  next_states=_ptr(next_states), knn_k=int(knn_k), knn_radius=float(knn_radius),
+                  stamps=_ptr(stamps))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
 
     def alloc_outputs(self, num_agents: int, device=None):

@@ -176,3 +176,24 @@ def test_grid_neighbours_match_csr(mpclib):
     agents = list(range(0, 400, 13))
     ref = run_oracle(cfg, states, targets, rp, col, agents)
     compare(cfg, g, ref, agents)
+
+
+def test_separable_and_dense_layouts_agree(mpclib):
+    """variant 0 (separable x/y/yaw layout, pdip_sep.hpp) and variant 3 (dense 6x6 layout,
+    pdip.hpp) solve the same QPs: same statuses, objectives within solver tolerance."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(1024, seed=3)
+    states[:, :2] *= 0.55
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    res = {}
+    for variant in (0, 3):
+        ctx = mpclib.Context(cfg)
+        ctx.set_variant(variant)
+        res[variant] = run_gpu(ctx, states, targets, rp, col, torch)
+    np.testing.assert_array_equal(res[0]["status"], res[3]["status"])
+    ok = res[0]["status"] == 0
+    assert ok.sum() > 1000
+    err = np.abs(res[0]["obj"][ok] - res[3]["obj"][ok]) / np.maximum(1.0, np.abs(res[3]["obj"][ok]))
+    assert err.max() <= 1e-8, err.max()
+    assert np.nanmax(np.abs(res[0]["x"] - res[3]["x"])) <= 1e-6

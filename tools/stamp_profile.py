@@ -1,0 +1,74 @@
+"""Per-phase timing of the fused IMPC kernel from its s_memrealtime stamps (100 MHz).
+
+Runs the bench workload closed-loop for a few steps, then one instrumented launch per variant,
+and prints, over agents: start skew, per-phase durations (setup, neighbours, CBF rows, solves,
+outputs) as mean / p50 / p99 / max in microseconds, and the critical (latest-ending) agent.
+
+    python tools/stamp_profile.py [N] [warm_steps] [variants...]
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "mpc-cbf_amd"))
+from mpccbf import Context, swarm  # noqa: E402
+
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+WARM = int(sys.argv[2]) if len(sys.argv) > 2 else 100
+VARIANTS = [int(v) for v in sys.argv[3:]] or [0, 3]
+PH = ["setup", "neighbours", "cbf_rows0", "solve0", "cbf_rows1", "solve1", "outputs"]
+cfg = swarm.config(15)
+states_h, targets_h = swarm.lattice_swarm(N)
+dev = torch.device("cuda", 0)
+st = torch.tensor(states_h, device=dev)
+tg = torch.tensor(targets_h, device=dev)
+radius = 3.0 * cfg["d_min"]
+ctx = Context(cfg)
+out = ctx.alloc_outputs(N)
+for _ in range(WARM):
+    ctx.impc_solve(st, targets=tg, knn_k=8, knn_radius=radius, **out)
+    st.copy_(out["next_states"])
+torch.cuda.synchronize()
+snap = st.clone()
+PDIP = os.environ.get("MPCCBF_LIB", "").find("prof") >= 0  # profiling build: in-loop stamps
+PPH = ["rows+acc", "reduce acc", "rp/py/conv", "cholesky", "pred solve", "pred steps+min",
+       "mua", "corr rows+vc", "corr solve", "corr steps+min", "update"]
+for v in VARIANTS:
+    ctx.set_variant(v)
+    stamps = torch.zeros(N * 8 + (N * 16 if PDIP else 0), dtype=torch.int64, device=dev)
+    for rep in range(3):  # last rep measured (warm caches)
+        ctx.impc_solve(snap, targets=tg, knn_k=8, knn_radius=radius, stamps=stamps, **out)
+    torch.cuda.synchronize()
+    allst = stamps.cpu().numpy()
+    s = allst[:N * 8].reshape(N, 8).astype(np.float64) * 0.01  # 10 ns ticks -> us
+    if PDIP and v == 0:
+        ps = allst[N * 8:].reshape(N, 16).astype(np.float64)  # shader cycles
+        okp = ps[:, 11] > 0
+        d = np.diff(ps[okp, :12], axis=1)
+        tot = ps[okp, 11] - ps[okp, 0]
+        print(f"variant {v}: Newton step 2 of solve 0, {okp.sum()} agents, cycles mean {tot.mean():.0f} "
+              f"p50 {np.median(tot):.0f}")
+        for k, name in enumerate(PPH):
+            print(f"   {name:15s} mean {d[:, k].mean():7.0f}  p50 {np.median(d[:, k]):7.0f} cycles")
+    status = out["status"].cpu().numpy()
+    t0 = s[:, 0].min()
+    start = s[:, 0] - t0
+    end = s[:, 7] - t0
+    print(f"variant {v}: span {end.max():.1f} us, start skew p50 {np.median(start):.1f} "
+          f"max {start.max():.1f} us, agent wall mean {np.mean(end - start):.1f} max {np.max(end - start):.1f}")
+    # phases; iteration-1 phases only for agents that attempted iteration 1
+    for k, name in enumerate(PH):
+        d = s[:, k + 1] - s[:, k]
+        if k >= 4:
+            d = d[status[:, 0] == 0]
+        if k == 4 or k == 5:
+            pass
+        print(f"   {name:11s} mean {d.mean():7.2f} p50 {np.median(d):7.2f} p99 {np.percentile(d, 99):7.2f} "
+              f"max {d.max():7.2f} us")
+    crit = int(np.argmax(end))
+    print(f"   critical agent {crit}: status {status[crit]}, start {start[crit]:.1f}, "
+          f"phases {np.round(np.diff(s[crit]), 2)}")
+    # how many agents end late
+    print(f"   agents ending after 0.8*span: {(end > 0.8 * end.max()).sum()}")
