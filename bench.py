@@ -43,13 +43,15 @@ def parse():
     ap.add_argument("--cpu-baseline-agents", type=int, default=-1,
                     help="agents in the CPU-oracle sample (default: sized for ~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loop", choices=["native", "python"], default="native",
+                    help="native: mpccbf_run_steps (C++ loop, RCCL); python: one call per step")
     ap.add_argument("--neighbours", choices=["grid", "csr"], default="grid",
                     help="grid: fused in-kernel spatial-hash query; csr: separate KNN kernels")
     return ap.parse_args()
 
 
 def flops_per_qp(iters: np.ndarray, rows: np.ndarray, nz: int) -> float:
-    """Algorithmic FP64 flops of the condensed Mehrotra PDIP actually executed (one QP):
+    """Algorithmic FP64 flops of the dense-layout condensed Mehrotra PDIP (impc_kernel), one QP:
     per iteration and row: residual 2nz, normal matrix nz(nz+1), rhs 2nz, two step directions
     2*2nz, step/update ~20; per iteration: Cholesky nz^3/3, four triangular solves 4nz^2,
     P y 2nz^2. (roofline uses min(canonical, executed); executed is smaller.)"""
@@ -58,11 +60,22 @@ def flops_per_qp(iters: np.ndarray, rows: np.ndarray, nz: int) -> float:
     return float(np.sum(iters * (rows * per_row + per_it)))
 
 
+def flops_per_qp_sep(iters: np.ndarray, rows: int) -> float:
+    """Algorithmic FP64 flops of the separable-layout PDIP (impc_sep_kernel), one QP: a box row
+    has 2 nonzeros; per Newton step and box row (both sides) ~60 flops — residuals and D (10),
+    its 3 normal-matrix entries and 2 right-hand-side terms (10), predictor direction, ratios and
+    complementarity (18), corrector right-hand side (7), combined direction and ratios (10),
+    update (8); per step 100 flops of 4x4 + 2x2 Cholesky and four triangular solves. CBF rows
+    (4 nonzeros, ~90 flops) are not counted: a lower bound."""
+    return float(np.sum(iters * (rows * 60 + 100)))
+
+
 def main():
     args = parse()
     import torch
     import torch.distributed as dist
-    from mpccbf import swarm, Context
+    from mpccbf import swarm, Context, Comm, comm_unique_id
+    from mpccbf._lib import COMM_ID_BYTES
     from mpccbf.dist import SwarmShard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,75 +100,102 @@ def main():
     ctx = Context(cfg, device=local)
     ctx.set_variant(args.variant)
 
-    shard = SwarmShard(torch.tensor(states_h, dtype=torch.float64, device=dev), world, rank)
-    states, local_states = shard.full, shard.local
     targets = torch.tensor(targets_h[first:first + per], dtype=torch.float64, device=dev)
-    nb_rp = torch.empty(per + 1, dtype=torch.int32, device=dev)
-    nb_col = torch.empty(per * max(args.knn, 1), dtype=torch.int32, device=dev)
     out = ctx.alloc_outputs(per, device=dev)
-    next_states = out.pop("next_states")
+    out.pop("next_states")  # written straight into the next state table
     nsteps = args.steps
     status_log = torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev)
     iters_log = torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream()
+    full0 = torch.tensor(states_h, dtype=torch.float64, device=dev)
 
-    def neighbours():
-        if args.neighbours == "csr":
-            ctx.build_neighbors(states, first, per, args.knn, radius, nb_rp, nb_col)
-            return dict(nb_row_ptr=nb_rp, nb_col=nb_col)
-        return dict(knn_k=args.knn, knn_radius=radius)  # fused device grid query
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
 
-    def step(slot: int | None):
-        shard.exchange()  # RCCL all-gather of agent states (copy at N=1)
-        nb = neighbours()
-        st = status_log[slot] if slot is not None else out["status"]
-        it = iters_log[slot] if slot is not None else out["iters"]
-        ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
-                       x=out["x"], status=st, obj=out["obj"], iters=it, next_states=next_states,
-                       **nb)
-        local_states.copy_(next_states)
+    if args.loop == "native" and args.neighbours == "grid":
+        # the whole closed loop in libmpccbf (mpccbf_run_steps): per step the grid build, the
+        # fused IMPC kernel and, across ranks, one in-place RCCL all-gather of agent states
+        comm = None
+        if world > 1:
+            uid = torch.zeros(COMM_ID_BYTES, dtype=torch.uint8, device=dev)
+            if rank == 0:
+                uid.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
+            dist.broadcast(uid, 0)
+            comm = Comm(bytes(uid.cpu().tolist()), world, rank, local)
+        tables = [full0, torch.empty_like(full0)]
+        common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn,
+                      knn_radius=radius, x=out["x"], obj=out["obj"], comm=comm)
+        r = ctx.run_steps(tables[0], tables[1], args.warmup, status=out["status"],
+                          iters=out["iters"], reserve_steps=nsteps, **common)
+        if r["final"] is not tables[0]:
+            tables.reverse()
+        barrier_sync()
+        t0 = time.perf_counter()
+        # one event per step (p99 step latency); the IMPC kernel is bracketed by its own events on
+        # every 16th step only (each event pair adds ~10 us of barrier packets to a step)
+        r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=status_log, iters_log=iters_log,
+                          timing=True, solve_stride=16, **common)
+        barrier_sync()
+        t1 = time.perf_counter()
+        step_ms, kern_ms = r["step_ms"].astype(np.float64), r["solve_ms"].astype(np.float64)
+        if comm is not None:
+            comm.close()
+    else:
+        # host-driven loop (one mpccbf_impc_solve per step; torch.distributed all-gather)
+        shard = SwarmShard(full0, world, rank)
+        nb_rp = torch.empty(per + 1, dtype=torch.int32, device=dev)
+        nb_col = torch.empty(per * max(args.knn, 1), dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream()
 
-    for _ in range(args.warmup):
-        step(None)
-    torch.cuda.synchronize()
+        def neighbours(states):
+            if args.neighbours == "csr":
+                ctx.build_neighbors(states, first, per, args.knn, radius, nb_rp, nb_col)
+                return dict(nb_row_ptr=nb_rp, nb_col=nb_col)
+            return dict(knn_k=args.knn, knn_radius=radius)
 
-    # per-step events (step latency) and per-launch events around the dominant kernel
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(nsteps + 1)]
-    kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(nsteps)]
+        def step(slot, kev_pair=None):
+            states = shard.full
+            nb = neighbours(states)
+            st = status_log[slot] if slot is not None else out["status"]
+            it = iters_log[slot] if slot is not None else out["iters"]
+            if kev_pair is not None:
+                kev_pair[0].record(stream)
+            ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
+                           x=out["x"], status=st, obj=out["obj"], iters=it,
+                           next_states=shard.next_out, **nb)
+            if kev_pair is not None:
+                kev_pair[1].record(stream)
+            shard.publish()
 
-    def step_timed(i):
-        shard.exchange()  # RCCL all-gather of agent states (copy at N=1)
-        nb = neighbours()
-        kev[i][0].record(stream)
-        ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
-                       x=out["x"], status=status_log[i], obj=out["obj"], iters=iters_log[i],
-                       next_states=next_states, **nb)
-        kev[i][1].record(stream)
-        local_states.copy_(next_states)
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev[0].record(stream)
-    for i in range(nsteps):
-        step_timed(i)
-        ev[i + 1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
+        for _ in range(args.warmup):
+            step(None)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(nsteps + 1)]
+        kev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(nsteps)]
+        barrier_sync()
+        t0 = time.perf_counter()
+        ev[0].record(stream)
+        for i in range(nsteps):
+            step(i, kev[i])
+            ev[i + 1].record(stream)
+        barrier_sync()
+        t1 = time.perf_counter()
+        step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(nsteps)])
+        kern_ms = np.array([a.elapsed_time(b) for a, b in kev])
     elapsed = t1 - t0
-    step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(nsteps)])
-    kern_ms = np.array([a.elapsed_time(b) for a, b in kev])
 
     status = status_log.cpu().numpy()
     iters = iters_log.cpu().numpy()
     attempted = int(np.sum(~((status == 5) & (iters == 0))))
     optimal = int(np.sum(status == 0))
     rows = ctx.shared_rows  # CBF rows are few (filtered); counted as shared rows only
-    flops = flops_per_qp(iters.reshape(-1), np.full(iters.size, rows), ctx.nz)
+    kname = ctx.kernel_name
+    if kname.startswith("impc_sep_kernel"):
+        flops = flops_per_qp_sep(iters.reshape(-1), rows)
+    else:
+        flops = flops_per_qp(iters.reshape(-1), np.full(iters.size, rows), ctx.nz)
 
     t = torch.tensor([elapsed, float(attempted), float(optimal), flops, float(np.mean(kern_ms)),
                       float(np.percentile(step_ms, 99))], dtype=torch.float64, device=dev)
@@ -211,7 +251,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / FP64_PEAK_TFLOPS,
                 "traffic": None,
-                "kernel": "impc_kernel<6,16,4>",
+                "kernel": kname,
                 "kernel_avg_us": kern_avg * 1e3,
                 "flops_per_launch": flops_per_launch,
             },

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 3
+#define MPCCBF_ABI_VERSION 4
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -148,9 +148,46 @@ typedef struct mpccbf_batch {
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);
 
+/* ---- Closed-loop stepping (the MPCCBFFormationControl_example.cpp:131-231 loop: every agent
+ * re-plans from the states the previous step produced, Jacobi update at t = h, no noise) ------
+ *
+ * mpccbf_run_steps enqueues num_steps control steps back to back on the stream. Step s reads
+ * table T_s (T_0 = batch->states, then alternating with run->states_alt; both num_states x 6,
+ * device) and writes the next states of agents [agent_first, agent_first + num_agents) into
+ * T_{s+1}. Rows of other agents are carried over (copy), or, with a communicator, filled by one
+ * in-place RCCL all-gather of every rank's block (ranks own equal contiguous blocks:
+ * agent_first = rank * num_agents, num_states = nranks * num_agents). batch->next_states is
+ * ignored; batch->status / iters receive the last step unless per-step logs are given.
+ * When step_ms or solve_ms is given the call waits for the GPU and fills them (host arrays,
+ * num_steps entries: device time of each step, and of its IMPC kernel alone). */
+typedef struct mpccbf_comm mpccbf_comm;
+#define MPCCBF_COMM_ID_BYTES 128
+int mpccbf_comm_unique_id(char id_out[MPCCBF_COMM_ID_BYTES]);  /* on one rank; share the bytes */
+int mpccbf_comm_create(const char id[MPCCBF_COMM_ID_BYTES], int32_t nranks, int32_t rank,
+                       int32_t device, mpccbf_comm** out);     /* collective over the nranks */
+void mpccbf_comm_destroy(mpccbf_comm* comm);
+
+typedef struct mpccbf_run {
+    int32_t num_steps;
+    double* states_alt;     /* second state table (device) */
+    int32_t* status_log;    /* num_steps x num_agents x impc_iter (device), or NULL */
+    int32_t* iters_log;     /* likewise, or NULL */
+    float* step_ms;         /* host, num_steps, or NULL */
+    float* solve_ms;        /* host, num_steps, or NULL */
+    mpccbf_comm* comm;      /* NULL: single process */
+    int32_t reserve_steps;  /* keep timing events for this many steps (avoids creating them later) */
+    int32_t solve_stride;   /* time the IMPC kernel on every solve_stride-th step only (<= 1: all);
+                               solve_ms of untimed steps is set to -1 */
+    int32_t final_table;    /* out: 0 = batch->states holds the final states, 1 = states_alt */
+} mpccbf_run;
+
+int mpccbf_run_steps(mpccbf_ctx* ctx, const mpccbf_batch* batch, mpccbf_run* run, void* hip_stream);
+
 /* Tuning knob: kernel geometry for mpccbf_impc_solve. 0 (default): 16 lanes per agent,
  * 4 row slots per lane; 1: 64 lanes per agent, 1 slot; 2: 64 lanes, 4 slots (wide rows). */
 int mpccbf_set_variant(mpccbf_ctx* ctx, int variant);
+/* Name of the IMPC kernel instantiation the current variant launches (diagnostics). */
+const char* mpccbf_kernel_name(const mpccbf_ctx* ctx);
 
 /* Neighbour lists on the device: for each agent of [agent_first, agent_first+num_agents) the
  * (at most) k nearest other agents of `states` (planar distance) within `radius`, sorted by

@@ -2,6 +2,7 @@
 // No exception crosses this boundary (the reference's std::invalid_argument / runtime_error
 // become MPCCBF_ERR_INVALID_ARGUMENT plus a thread-local message).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -19,6 +20,7 @@ namespace mpccbf {
 
 hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
                        hipStream_t s);
+const char* impc_kernel_name(const DevOps& op, int variant);
 int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
                      double radius, int32_t* row_ptr, int32_t* col, void* scratch,
                      size_t scratch_bytes, hipStream_t s);
@@ -45,6 +47,7 @@ static int fail(int code, const std::string& msg) { return set_error(code, msg);
 }  // namespace mpccbf
 
 struct mpccbf_ctx {
+    std::vector<hipEvent_t> events;  // timing events of mpccbf_run_steps (grown on demand)
     mpccbf_params p;
     mpccbf_options opt;
     mpccbf::Operators ops;
@@ -73,6 +76,66 @@ static void pack(std::vector<double>& v, int32_t& off, const std::vector<Mat>& m
     off = (int32_t)v.size();
     for (const Mat& m : ms) v.insert(v.end(), m.a.begin(), m.a.end());
 }
+
+// One IMPC step for a batch: grid build (grid mode) + the fused kernel, enqueued on `stream`;
+// ev0 / ev1 (optional) are recorded around the IMPC kernel alone.
+int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
+    if (!c || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    if (b->num_agents < 0 || b->agent_first < 0 || b->agent_first + b->num_agents > b->num_states)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
+    if (b->num_agents == 0) return MPCCBF_OK;
+    const bool grid = b->nb_row_ptr == nullptr;
+    if (!b->states || (!grid && !b->nb_col && b->num_states > 1))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "states / neighbour CSR missing");
+    if (grid && (b->knn_k < 1 || !(b->knn_radius > 0)))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
+    if (!b->targets && !b->refs) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "targets or refs required");
+    ImpcArgs a;
+    std::memset(&a, 0, sizeof(a));
+    HIP_TRY(hipSetDevice(c->device));
+    if (grid) {
+        const size_t need = grid_scratch_bytes(b->num_states);
+        if (need > c->grid_bytes) {
+            if (c->grid_scratch) (void)hipFree(c->grid_scratch);
+            c->grid_scratch = nullptr;
+            c->grid_bytes = 0;
+            HIP_TRY(hipMalloc(&c->grid_scratch, need));
+            c->grid_bytes = need;
+        }
+        uint32_t *start = nullptr, *sorted = nullptr;
+        const uint32_t T = launch_grid_build(b->states, b->num_states, b->knn_radius, c->grid_scratch,
+                                             &start, &sorted, stream);
+        if (T == 0) return fail(MPCCBF_ERR_CAPACITY, "grid neighbours: num_states > 32768 or launch failure");
+        a.grid.start = start;
+        a.grid.sorted = sorted;
+        a.grid.mask = T - 1;
+        a.grid.inv_cell = 1.0 / b->knn_radius;
+        a.grid.radius = b->knn_radius;
+        a.grid.k = b->knn_k;
+    }
+    a.num_states = b->num_states;
+    a.states = b->states;
+    a.agent_first = b->agent_first;
+    a.num_agents = b->num_agents;
+    a.targets = b->targets;
+    a.refs = b->targets ? nullptr : b->refs;
+    a.nb_row_ptr = b->nb_row_ptr;
+    a.nb_col = b->nb_col;
+    a.x = b->x;
+    a.status = b->status;
+    a.obj = b->obj;
+    a.iters = b->iters;
+    a.next_states = b->next_states;
+    a.stamps = b->stamps;
+    if (ev0) HIP_TRY(hipEventRecord(ev0, stream));
+    hipError_t e = launch_impc(c->dev, c->dbuf, a, c->variant, stream);
+    if (e == hipSuccess && ev1) e = hipEventRecord(ev1, stream);
+    if (e == hipErrorInvalidValue)
+        return fail(MPCCBF_ERR_CAPACITY, "no kernel instantiation for this reduced dimension / row count");
+    HIP_TRY(e);
+    return MPCCBF_OK;
+}
+
 
 extern "C" {
 
@@ -208,6 +271,7 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
 
 void mpccbf_destroy(mpccbf_ctx* c) {
     if (!c) return;
+    for (hipEvent_t e : c->events) (void)hipEventDestroy(e);
     if (c->dbuf) (void)hipFree(c->dbuf);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->grid_scratch) (void)hipFree(c->grid_scratch);
@@ -219,58 +283,13 @@ int mpccbf_reduced_dim(const mpccbf_ctx* c) { return c ? c->ops.nz : -1; }
 int mpccbf_num_shared_rows(const mpccbf_ctx* c) { return c ? c->ops.G.r : -1; }
 
 int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
-    if (!c || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
-    if (b->num_agents < 0 || b->agent_first < 0 || b->agent_first + b->num_agents > b->num_states)
-        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
-    if (b->num_agents == 0) return MPCCBF_OK;
-    const bool grid = b->nb_row_ptr == nullptr;
-    if (!b->states || (!grid && !b->nb_col && b->num_states > 1))
-        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "states / neighbour CSR missing");
-    if (grid && (b->knn_k < 1 || !(b->knn_radius > 0)))
-        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
-    if (!b->targets && !b->refs) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "targets or refs required");
-    ImpcArgs a;
-    std::memset(&a, 0, sizeof(a));
-    HIP_TRY(hipSetDevice(c->device));
-    if (grid) {
-        const size_t need = grid_scratch_bytes(b->num_states);
-        if (need > c->grid_bytes) {
-            if (c->grid_scratch) (void)hipFree(c->grid_scratch);
-            c->grid_scratch = nullptr;
-            c->grid_bytes = 0;
-            HIP_TRY(hipMalloc(&c->grid_scratch, need));
-            c->grid_bytes = need;
-        }
-        uint32_t *start = nullptr, *sorted = nullptr;
-        const uint32_t T = launch_grid_build(b->states, b->num_states, b->knn_radius, c->grid_scratch,
-                                             &start, &sorted, (hipStream_t)stream);
-        if (T == 0) return fail(MPCCBF_ERR_CAPACITY, "grid neighbours: num_states > 32768 or launch failure");
-        a.grid.start = start;
-        a.grid.sorted = sorted;
-        a.grid.mask = T - 1;
-        a.grid.inv_cell = 1.0 / b->knn_radius;
-        a.grid.radius = b->knn_radius;
-        a.grid.k = b->knn_k;
-    }
-    a.num_states = b->num_states;
-    a.states = b->states;
-    a.agent_first = b->agent_first;
-    a.num_agents = b->num_agents;
-    a.targets = b->targets;
-    a.refs = b->targets ? nullptr : b->refs;
-    a.nb_row_ptr = b->nb_row_ptr;
-    a.nb_col = b->nb_col;
-    a.x = b->x;
-    a.status = b->status;
-    a.obj = b->obj;
-    a.iters = b->iters;
-    a.next_states = b->next_states;
-    a.stamps = b->stamps;
-    hipError_t e = launch_impc(c->dev, c->dbuf, a, c->variant, (hipStream_t)stream);
-    if (e == hipErrorInvalidValue)
-        return fail(MPCCBF_ERR_CAPACITY, "no kernel instantiation for this reduced dimension / row count");
-    HIP_TRY(e);
-    return MPCCBF_OK;
+    return impc_enqueue(c, b, (hipStream_t)stream, nullptr, nullptr);
+}
+
+const char* mpccbf_kernel_name(const mpccbf_ctx* c) {
+    if (!c) return "";
+    const char* n = impc_kernel_name(c->dev, c->variant);
+    return n ? n : "";
 }
 
 int mpccbf_set_variant(mpccbf_ctx* c, int variant) {
@@ -304,3 +323,121 @@ int mpccbf_build_neighbors(mpccbf_ctx* c, const double* states, int32_t num_stat
 
 }  // extern "C"
 
+
+// ---------------------------------------------------------------------------------------------
+// Closed-loop stepping + RCCL exchange
+// ---------------------------------------------------------------------------------------------
+struct mpccbf_comm {
+    ncclComm_t nccl = nullptr;
+    int nranks = 1, rank = 0, device = 0;
+};
+
+extern "C" {
+
+int mpccbf_comm_unique_id(char id_out[MPCCBF_COMM_ID_BYTES]) {
+    if (!id_out) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    static_assert(sizeof(ncclUniqueId) == MPCCBF_COMM_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(MPCCBF_ERR_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(id_out, &id, sizeof(id));
+    return MPCCBF_OK;
+}
+
+int mpccbf_comm_create(const char id[MPCCBF_COMM_ID_BYTES], int32_t nranks, int32_t rank, int32_t device,
+                       mpccbf_comm** out) {
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "bad communicator arguments");
+    *out = nullptr;
+    HIP_TRY(hipSetDevice(device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    mpccbf_comm* cm = new mpccbf_comm();
+    cm->nranks = nranks;
+    cm->rank = rank;
+    cm->device = device;
+    const ncclResult_t r = ncclCommInitRank(&cm->nccl, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        delete cm;
+        return fail(MPCCBF_ERR_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    }
+    *out = cm;
+    return MPCCBF_OK;
+}
+
+void mpccbf_comm_destroy(mpccbf_comm* cm) {
+    if (!cm) return;
+    if (cm->nccl) (void)ncclCommDestroy(cm->nccl);
+    delete cm;
+}
+
+int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* stream_) {
+    if (!c || !b || !r) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    if (r->num_steps < 0 || !r->states_alt || !b->states)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "run: num_steps < 0 or missing state tables");
+    const int first = b->agent_first, count = b->num_agents, ns = b->num_states;
+    if (first < 0 || count < 0 || first + count > ns) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
+    if (r->comm && (ns != r->comm->nranks * count || first != r->comm->rank * count))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "run: ranks must own equal contiguous agent blocks");
+    hipStream_t stream = (hipStream_t)stream_;
+    HIP_TRY(hipSetDevice(c->device));
+    const bool timing = r->step_ms || r->solve_ms;
+    const int need = 3 * std::max(r->num_steps, r->reserve_steps) + 1;
+    while ((int)c->events.size() < need) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreate(&e));
+        c->events.push_back(e);
+    }
+    double* tables[2] = {const_cast<double*>(b->states), r->states_alt};
+    const size_t per_log = (size_t)count * c->p.impc_iter;
+    mpccbf_batch sb = *b;
+    hipEvent_t* ev = c->events.data();
+    if (timing) HIP_TRY(hipEventRecord(ev[0], stream));
+    for (int s = 0; s < r->num_steps; s++) {
+        double* cur = tables[s & 1];
+        double* nxt = tables[(s & 1) ^ 1];
+        sb.states = cur;
+        sb.next_states = nxt + (size_t)first * 6;
+        if (r->status_log) sb.status = r->status_log + (size_t)s * per_log;
+        if (r->iters_log) sb.iters = r->iters_log + (size_t)s * per_log;
+        if (!r->comm) {  // rows this batch does not solve (static agents) carry over
+            if (first > 0)
+                HIP_TRY(hipMemcpyAsync(nxt, cur, (size_t)first * 6 * sizeof(double), hipMemcpyDeviceToDevice, stream));
+            const int tail = ns - first - count;
+            if (tail > 0)
+                HIP_TRY(hipMemcpyAsync(nxt + (size_t)(first + count) * 6, cur + (size_t)(first + count) * 6,
+                                       (size_t)tail * 6 * sizeof(double), hipMemcpyDeviceToDevice, stream));
+        }
+        const bool tk = r->solve_ms && (r->solve_stride <= 1 || s % r->solve_stride == 0);
+        const int rc = impc_enqueue(c, &sb, stream, tk ? ev[3 * s + 1] : nullptr, tk ? ev[3 * s + 2] : nullptr);
+        if (rc != MPCCBF_OK) return rc;
+        if (r->comm && r->comm->nranks > 1) {
+            const ncclResult_t nr = ncclAllGather(nxt + (size_t)first * 6, nxt, (size_t)count * 6, ncclDouble,
+                                                  r->comm->nccl, stream);
+            if (nr != ncclSuccess) return fail(MPCCBF_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
+        }
+        if (r->step_ms || (timing && s == r->num_steps - 1)) HIP_TRY(hipEventRecord(ev[3 * s + 3], stream));
+    }
+    r->final_table = r->num_steps & 1;
+    if (timing && r->num_steps > 0) {
+        HIP_TRY(hipEventSynchronize(ev[3 * (r->num_steps - 1) + 3]));
+        for (int s = 0; s < r->num_steps; s++) {
+            float ms = 0.f;
+            if (r->step_ms) {
+                HIP_TRY(hipEventElapsedTime(&ms, ev[s == 0 ? 0 : 3 * (s - 1) + 3], ev[3 * s + 3]));
+                r->step_ms[s] = ms;
+            }
+            if (r->solve_ms) {
+                if (r->solve_stride <= 1 || s % r->solve_stride == 0) {
+                    HIP_TRY(hipEventElapsedTime(&ms, ev[3 * s + 1], ev[3 * s + 2]));
+                    r->solve_ms[s] = ms;
+                } else {
+                    r->solve_ms[s] = -1.f;
+                }
+            }
+        }
+    }
+    return MPCCBF_OK;
+}
+
+}  // extern "C"

@@ -658,6 +658,17 @@ static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const I
     return hipGetLastError();
 }
 
+// Instantiation launch_impc picks for (operators, variant); nullptr if none fits.
+const char* impc_kernel_name(const DevOps& op, int variant) {
+    if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1>";
+    if (op.nz == 6) {
+        if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
+        if (variant == 1 && op.m < 64) return "impc_kernel<6,64,1>";
+        if (op.m < 256) return "impc_kernel<6,64,4>";
+    }
+    return nullptr;
+}
+
 // Returns hipErrorInvalidValue if no instantiation fits (nz, m).
 //   variant 0: separable layout when the operators allow it (16 lanes, 16 box rows per channel,
 //              16 CBF rows), else 16 lanes x 4 dense slots

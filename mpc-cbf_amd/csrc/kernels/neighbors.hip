@@ -246,44 +246,67 @@ namespace dev {
 // Spatial hash of all agents in ONE workgroup (n <= 32768): LDS histogram -> block scan ->
 // scatter. One launch instead of count/scan/scatter; bucket order inside a cell follows LDS
 // atomic order (the consumer orders neighbours by index, so results do not depend on it).
-__global__ void __launch_bounds__(1024) grid_build_kernel(const double* __restrict__ st, int n,
-                                                          double inv, uint32_t T, uint32_t* start,
-                                                          uint32_t* sorted, uint32_t* slot_off) {
+// Each thread keeps the bucket and in-bucket offset of its (up to GB_PER) agents in registers
+// between the passes; the bucket scan is a per-thread serial sum, a wave-level DPP/shuffle scan
+// and one scan of the 16 wave totals (3 barriers instead of a 1024-wide Hillis-Steele).
+constexpr int GB_THREADS = 1024;
+constexpr int GB_PER = 32;  // agents per thread: n <= 32768
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(GB_THREADS) grid_build_kernel(const double* __restrict__ st, int n,
+                                                                double inv, uint32_t T, uint32_t* start,
+                                                                uint32_t* sorted) {
     extern __shared__ uint32_t cnt[];  // T buckets
-    __shared__ uint32_t part[1024];
-    const int tid = threadIdx.x;
-    for (uint32_t i = tid; i < T; i += 1024) cnt[i] = 0u;
+    __shared__ uint32_t wsum[GB_THREADS / 64];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (uint32_t i = tid; i < T; i += GB_THREADS) cnt[i] = 0u;
     __syncthreads();
-    for (int i = tid; i < n; i += 1024) {
-        const long long cx = (long long)floor(st[(size_t)i * 6] * inv);
-        const long long cy = (long long)floor(st[(size_t)i * 6 + 1] * inv);
-        slot_off[i] = atomicAdd(&cnt[cell_hash(cx, cy, T - 1)], 1u);
+    uint32_t h[GB_PER], off[GB_PER];
+#pragma unroll
+    for (int k = 0; k < GB_PER; k++) {
+        const int i = tid + k * GB_THREADS;
+        if (i < n) {
+            const long long cx = (long long)floor(st[(size_t)i * 6] * inv);
+            const long long cy = (long long)floor(st[(size_t)i * 6 + 1] * inv);
+            h[k] = cell_hash(cx, cy, T - 1);
+            off[k] = atomicAdd(&cnt[h[k]], 1u);
+        }
     }
     __syncthreads();
-    const uint32_t per = T / 1024, b = tid * per;
+    // exclusive scan of cnt: thread t owns buckets [t*per, (t+1)*per)
+    const uint32_t per = T / GB_THREADS, b = tid * per;
     uint32_t s = 0;
     for (uint32_t i = 0; i < per; i++) s += cnt[b + i];
-    part[tid] = s;
+    const uint32_t incl = wave_incl_scan(s, lane);
+    if (lane == 63) wsum[wid] = incl;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const uint32_t v = tid >= o ? part[tid - o] : 0u;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
+    if (wid == 0) {
+        const uint32_t w = lane < GB_THREADS / 64 ? wsum[lane] : 0u;
+        const uint32_t wi = wave_incl_scan(w, lane);
+        if (lane < GB_THREADS / 64) wsum[lane] = wi - w;  // exclusive wave offsets
+        if (lane == GB_THREADS / 64 - 1) start[T] = wi;
     }
-    uint32_t run = tid > 0 ? part[tid - 1] : 0u;
+    __syncthreads();
+    uint32_t run = wsum[wid] + incl - s;
     for (uint32_t i = 0; i < per; i++) {
         const uint32_t c = cnt[b + i];
         cnt[b + i] = run;
         start[b + i] = run;
         run += c;
     }
-    if (tid == 1023) start[T] = part[1023];
     __syncthreads();
-    for (int i = tid; i < n; i += 1024) {
-        const long long cx = (long long)floor(st[(size_t)i * 6] * inv);
-        const long long cy = (long long)floor(st[(size_t)i * 6 + 1] * inv);
-        sorted[cnt[cell_hash(cx, cy, T - 1)] + slot_off[i]] = (uint32_t)i;
+#pragma unroll
+    for (int k = 0; k < GB_PER; k++) {
+        const int i = tid + k * GB_THREADS;
+        if (i < n) sorted[cnt[h[k]] + off[k]] = (uint32_t)i;
     }
 }
 
@@ -298,12 +321,11 @@ size_t grid_scratch_bytes(int num_states) {
 uint32_t launch_grid_build(const double* states, int n, double radius, void* scratch,
                            uint32_t** start, uint32_t** sorted, hipStream_t s) {
     const uint32_t T = grid_table_size(n);
-    if (T > 32768) return 0;  // single-workgroup LDS histogram limit
+    if (T > 32768 || n > dev::GB_THREADS * dev::GB_PER) return 0;  // single-workgroup limits
     char* p = (char*)scratch;
     *start = (uint32_t*)p;
     p += ((size_t)(T + 1) * 4 + 255) / 256 * 256;
     *sorted = (uint32_t*)p;
-    uint32_t* slot_off = *sorted + n;
     static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an opt-in (gfx950: 160 KiB/CU)
     if (!attr_set) {
         if (hipFuncSetAttribute((const void*)dev::grid_build_kernel,
@@ -311,8 +333,8 @@ uint32_t launch_grid_build(const double* states, int n, double radius, void* scr
             return 0;
         attr_set = true;
     }
-    hipLaunchKernelGGL(dev::grid_build_kernel, dim3(1), dim3(1024), (size_t)T * 4, s, states, n,
-                       1.0 / radius, T, *start, *sorted, slot_off);
+    hipLaunchKernelGGL(dev::grid_build_kernel, dim3(1), dim3(dev::GB_THREADS), (size_t)T * 4, s, states,
+                       n, 1.0 / radius, T, *start, *sorted);
     return hipGetLastError() == hipSuccess ? T : 0;
 }
 

@@ -19,7 +19,8 @@ EXPORTED = [
     "mpccbf_create", "mpccbf_destroy", "mpccbf_num_vars", "mpccbf_reduced_dim",
     "mpccbf_num_shared_rows", "mpccbf_impc_solve", "mpccbf_set_variant", "mpccbf_build_neighbors",
     "mpccbf_qp_solve_dense", "mpccbf_qp_solve_dense_batch", "mpccbf_last_error",
-    "mpccbf_status_string", "mpccbf_abi_version",
+    "mpccbf_status_string", "mpccbf_abi_version", "mpccbf_run_steps", "mpccbf_comm_unique_id",
+    "mpccbf_comm_create", "mpccbf_comm_destroy", "mpccbf_kernel_name",
 ]
 
 
@@ -74,6 +75,13 @@ class Batch(C.Structure):
     ]
 
 
+class Run(C.Structure):
+    _fields_ = [("num_steps", C.c_int32), ("states_alt", C.c_void_p), ("status_log", C.c_void_p),
+                ("iters_log", C.c_void_p), ("step_ms", C.c_void_p), ("solve_ms", C.c_void_p),
+                ("comm", C.c_void_p), ("reserve_steps", C.c_int32), ("solve_stride", C.c_int32),
+                ("final_table", C.c_int32)]
+
+
 class DenseQP(C.Structure):
     _fields_ = [("n", C.c_int32), ("m", C.c_int32), ("H", C.c_void_p), ("c", C.c_void_p),
                 ("c0", C.c_double), ("A", C.c_void_p), ("lo", C.c_void_p), ("hi", C.c_void_p),
@@ -118,6 +126,13 @@ def load():
                                          C.c_double, vp, vp, vp]
     L.mpccbf_qp_solve_dense.argtypes = [C.POINTER(DenseQP), vp, vp, vp]
     L.mpccbf_qp_solve_dense_batch.argtypes = [C.c_int32, C.POINTER(DenseQP), vp, vp, vp]
+    L.mpccbf_run_steps.argtypes = [vp, C.POINTER(Batch), C.POINTER(Run), vp]
+    L.mpccbf_comm_unique_id.argtypes = [C.c_char_p]
+    L.mpccbf_comm_create.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(vp)]
+    L.mpccbf_comm_destroy.argtypes = [vp]
+    L.mpccbf_comm_destroy.restype = None
+    L.mpccbf_kernel_name.argtypes = [vp]
+    L.mpccbf_kernel_name.restype = C.c_char_p
     L.mpccbf_last_error.restype = C.c_char_p
     L.mpccbf_status_string.restype = C.c_char_p
     L.mpccbf_status_string.argtypes = [C.c_int32]
@@ -183,6 +198,10 @@ class Context:
     def set_variant(self, v: int):
         _check(load().mpccbf_set_variant(self._h, v))
 
+    @property
+    def kernel_name(self) -> str:
+        return load().mpccbf_kernel_name(self._h).decode()
+
     def build_neighbors(self, states, first, count, k, radius, row_ptr, col, stream=None):
         _check(load().mpccbf_build_neighbors(self._h, _ptr(states), states.shape[0], first, count,
                                              k, float(radius), _ptr(row_ptr), _ptr(col),
@@ -202,6 +221,37 @@ class Context:
                   next_states=_ptr(next_states), knn_k=int(knn_k), knn_radius=float(knn_radius),
                   stamps=_ptr(stamps))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
+
+    def run_steps(self, states, states_alt, num_steps, targets=None, refs=None, agent_first=0,
+                  num_agents=None, knn_k=0, knn_radius=0.0, nb_row_ptr=None, nb_col=None, x=None,
+                  status=None, obj=None, iters=None, status_log=None, iters_log=None,
+                  timing=False, comm=None, reserve_steps=0, solve_stride=1, step_timing=True,
+                  stream=None):
+        """Closed-loop control steps on the device (mpccbf_run_steps). Returns a dict with the
+        table holding the final states ('final', a tensor) and, with timing=True, per-step
+        device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms)."""
+        if num_agents is None:
+            num_agents = states.shape[0] - agent_first
+        b = Batch(num_states=states.shape[0], states=_ptr(states), agent_first=agent_first,
+                  num_agents=num_agents, targets=_ptr(targets), refs=_ptr(refs),
+                  nb_row_ptr=_ptr(nb_row_ptr), nb_col=_ptr(nb_col), x=_ptr(x),
+                  status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters), next_states=None,
+                  knn_k=int(knn_k), knn_radius=float(knn_radius), stamps=None)
+        step_ms = np.zeros(max(num_steps, 1), dtype=np.float32) if timing and step_timing else None
+        solve_ms = np.zeros(max(num_steps, 1), dtype=np.float32) if timing else None
+        r = Run(num_steps=num_steps, states_alt=_ptr(states_alt), status_log=_ptr(status_log),
+                iters_log=_ptr(iters_log),
+                step_ms=None if step_ms is None else step_ms.ctypes.data,
+                solve_ms=None if solve_ms is None else solve_ms.ctypes.data,
+                comm=None if comm is None else comm.handle, reserve_steps=reserve_steps,
+                solve_stride=solve_stride)
+        _check(load().mpccbf_run_steps(self._h, C.byref(b), C.byref(r), _stream(stream)))
+        out = {"final": states if r.final_table == 0 else states_alt}
+        if timing:
+            out["step_ms"] = None if step_ms is None else step_ms[:num_steps]
+            sm = solve_ms[:num_steps]
+            out["solve_ms"] = sm[sm >= 0]
+        return out
 
     def alloc_outputs(self, num_agents: int, device=None):
         import torch
@@ -303,3 +353,31 @@ def dense_qp_solve_batch(qps):
                                          st.ctypes.data))
     n = len(qps)
     return st[:n], [xs[k] if st[k] == 0 else None for k in range(n)], obj[:n]
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (mpccbf_comm_unique_id), created on one rank and shared with the others."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(load().mpccbf_comm_unique_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """RCCL communicator for the per-step all-gather of agent states (mpccbf_comm_create):
+    collective — every rank constructs it with the same id."""
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        h = C.c_void_p()
+        _check(load().mpccbf_comm_create(uid, nranks, rank, device, C.byref(h)))
+        self.handle = h
+        self.nranks, self.rank = nranks, rank
+
+    def close(self):
+        if getattr(self, "handle", None):
+            load().mpccbf_comm_destroy(self.handle)
+            self.handle = None

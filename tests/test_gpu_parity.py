@@ -197,3 +197,65 @@ def test_separable_and_dense_layouts_agree(mpclib):
     err = np.abs(res[0]["obj"][ok] - res[3]["obj"][ok]) / np.maximum(1.0, np.abs(res[3]["obj"][ok]))
     assert err.max() <= 1e-8, err.max()
     assert np.nanmax(np.abs(res[0]["x"] - res[3]["x"])) <= 1e-6
+
+
+def _manual_loop(ctx, st0, tg, steps, first, count, torch):
+    a = st0.clone()
+    b = st0.clone()
+    out = ctx.alloc_outputs(count)
+    for _ in range(steps):
+        b.copy_(a)  # rows outside the batch carry over
+        ctx.impc_solve(a, targets=tg, agent_first=first, num_agents=count, knn_k=8, knn_radius=6.0,
+                       x=out["x"], status=out["status"], obj=out["obj"], iters=out["iters"],
+                       next_states=b[first:first + count])
+        a, b = b, a
+    torch.cuda.synchronize()
+    return a.cpu().numpy(), out["status"].cpu().numpy()
+
+
+@pytest.mark.parametrize("first,count", [(0, 512), (0, 500), (12, 488)])
+def test_run_steps_matches_step_by_step(mpclib, first, count):
+    """mpccbf_run_steps (native closed loop, ping-pong tables) == the same steps issued one by
+    one through mpccbf_impc_solve; agents outside the batch stay where they are."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(512, seed=5)
+    states[:, :2] *= 0.6
+    dev = torch.device("cuda", 0)
+    st0 = torch.tensor(states, device=dev)
+    tg = torch.tensor(targets[first:first + count], device=dev)
+    ctx = mpclib.Context(cfg)
+    ref_states, ref_status = _manual_loop(ctx, st0, tg, 7, first, count, torch)
+    a, b = st0.clone(), torch.empty_like(st0)
+    out = ctx.alloc_outputs(count)
+    logs = torch.empty((7, count, 2), dtype=torch.int32, device=dev)
+    r = ctx.run_steps(a, b, 7, targets=tg, agent_first=first, num_agents=count, knn_k=8,
+                      knn_radius=6.0, x=out["x"], obj=out["obj"], status_log=logs, timing=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(r["final"].cpu().numpy(), ref_states)
+    np.testing.assert_array_equal(logs[-1].cpu().numpy(), ref_status)
+    assert np.all(r["step_ms"] > 0) and np.all(r["solve_ms"] > 0)
+    assert np.all(r["solve_ms"] <= r["step_ms"] + 1e-3)
+    if count < 512:
+        keep = np.ones(512, bool)
+        keep[first:first + count] = False
+        np.testing.assert_array_equal(ref_states[keep], states[keep])
+
+
+def test_run_steps_with_single_rank_communicator(mpclib):
+    """The RCCL exchange path (in-place all-gather after every step) with one rank equals the
+    single-process loop."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(256, seed=9)
+    dev = torch.device("cuda", 0)
+    st0 = torch.tensor(states, device=dev)
+    tg = torch.tensor(targets, device=dev)
+    ctx = mpclib.Context(cfg)
+    ref_states, _ = _manual_loop(ctx, st0, tg, 5, 0, 256, torch)
+    comm = mpclib.Comm(mpclib.comm_unique_id(), 1, 0, 0)
+    a, b = st0.clone(), torch.empty_like(st0)
+    r = ctx.run_steps(a, b, 5, targets=tg, knn_k=8, knn_radius=6.0, comm=comm)
+    torch.cuda.synchronize()
+    comm.close()
+    np.testing.assert_array_equal(r["final"].cpu().numpy(), ref_states)

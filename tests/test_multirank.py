@@ -48,7 +48,6 @@ def _run(world, rank):
     solve = _oracle_solver(cfg, targets)
     for _ in range(STEPS):
         sh.step(solve)
-    sh.exchange()
     return sh.full.numpy().copy()
 
 
