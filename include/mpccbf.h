@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 4
+#define MPCCBF_ABI_VERSION 5
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -76,6 +76,14 @@ typedef struct mpccbf_params {
     int32_t num_pieces, num_control_points;
     double piece_max_parameter;
     int32_t continuity_upto_degree;
+    /* controller family: 0 = ConnectivityIMPCCBF (collision CBF against neighbour states,
+     * continuity d <= degree), 1 = FovBezierIMPCCBF (FoV CBFs against neighbour positions +
+     * Voronoi rows on piece 0, continuity d < degree; FovBezierIMPCCBF.cpp:44-223) */
+    int32_t cbf_mode;
+    double fov_beta;  /* field of view (rad); FovCBF(fov, Ds, Rs, ...) (FovCBF.cpp:41-52) */
+    double fov_Ds;    /* safety distance (the FoV example passes aligned_box[0]) */
+    double fov_Rs;    /* sensing range (fov_cbf_params.Rs) */
+    double bbox[3];   /* robot aligned-box half extents (Voronoi shift, math/src/Helpers.cpp:20-36) */
 } mpccbf_params;
 
 typedef struct mpccbf_ctx mpccbf_ctx;

@@ -43,6 +43,8 @@ class Params(C.Structure):
         ("slack_cost", C.c_double), ("slack_decay_rate", C.c_double),
         ("num_pieces", C.c_int32), ("num_control_points", C.c_int32),
         ("piece_max_parameter", C.c_double), ("continuity_upto_degree", C.c_int32),
+        ("cbf_mode", C.c_int32), ("fov_beta", C.c_double), ("fov_Ds", C.c_double),
+        ("fov_Rs", C.c_double), ("bbox", C.c_double * 3),
     ]
 
     @classmethod

@@ -22,7 +22,15 @@ BASE_CONFIG = dict(
     d_min=2.0, cbf_horizon=2, impc_iter=2, slack_mode=0, slack_cost=50000.0,
     slack_decay_rate=0.1, num_pieces=3, num_control_points=4, piece_max_parameter=0.5,
     continuity_upto_degree=3,
+    # FoV controller (BASELINE config 5): FovBezierIMPCCBF with fov 120 deg, Ds = aligned_box[0],
+    # Rs = 3 d_min, robot box half extents (0.2, 0.2, 0)
+    cbf_mode=0, fov_beta=2.0 * math.pi / 3.0, fov_Ds=0.2, fov_Rs=6.0, bbox=[0.2, 0.2, 0.0],
 )
+
+
+def fov_config(k_hor: int = 20, **over) -> dict:
+    """BASELINE config 5: FoV controller, horizon 20 over 4 Bezier pieces (K h <= 4 x 0.5 s)."""
+    return config(k_hor, cbf_mode=1, num_pieces=4, **over)
 
 
 def config(k_hor: int, **over) -> dict:
@@ -105,6 +113,39 @@ def knn_csr(states: np.ndarray, k: int, radius: float):
     row_ptr[1:] = np.cumsum([len(r) for r in rows])
     col = np.concatenate(rows).astype(np.int32) if row_ptr[-1] else np.zeros(0, np.int32)
     return row_ptr, col
+
+
+def fov_csr(states: np.ndarray, k: int, radius: float, fov: float):
+    """Neighbour lists for the FoV controller: the k nearest agents (planar) within `radius` whose
+    bearing lies strictly inside the ego's field of view (|bearing - yaw| < fov / 2), i.e. the
+    robots it can observe. Ties by index; rows sorted by index. Returns (row_ptr, col)."""
+    p = states[:, :2]
+    n = len(p)
+    rows = []
+    for i in range(n):
+        d = p - p[i]
+        d2 = np.sum(d ** 2, axis=1)
+        d2[i] = np.inf
+        bearing = np.arctan2(d[:, 1], d[:, 0]) - states[i, 2]
+        off = np.abs(np.angle(np.exp(1j * bearing)))
+        cand = np.nonzero((d2 <= radius * radius) & (off < 0.5 * fov))[0]
+        order = np.lexsort((cand, d2[cand]))[:k]
+        rows.append(np.sort(cand[order]))
+    row_ptr = np.zeros(n + 1, dtype=np.int32)
+    row_ptr[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate(rows).astype(np.int32) if row_ptr[-1] else np.zeros(0, np.int32)
+    return row_ptr, col
+
+
+def heading_swarm(n_agents: int, d_min: float = 2.0, seed: int = SEED, v_range: float = 0.5,
+                  target_radius: float = 3.0):
+    """lattice_swarm with every agent's yaw drawn uniformly (the FoV controller observes the
+    neighbours inside its heading cone)."""
+    states, targets = lattice_swarm(n_agents, d_min, seed, v_range, target_radius)
+    rng = np.random.default_rng(seed + 1)
+    states[:, 2] = rng.uniform(-math.pi, math.pi, n_agents)
+    targets[:, 2] = states[:, 2]
+    return states, targets
 
 
 def all_csr(n: int):

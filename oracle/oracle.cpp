@@ -8,6 +8,7 @@
 #include "oracle.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -283,6 +284,106 @@ struct CostAccum {
     }
 };
 
+// ---------------------------------------------------------------- FoV CBF rows (closed form)
+// FovCBF::initSafetyCBF / initBorder1CBF / initBorder2CBF / initRangeCBF
+// (cbf/src/detail/FovCBF.cpp:152-535) evaluated symbolically by hand. With d = target - p,
+// rel = R(th) d = (c dx + s dy, -s dx + c dy), f = (vx, vy, w, 0, 0, 0), g = [0; I]:
+//   every barrier is b(px, py, th), Ac = LgLf b = (b_px, b_py, b_th), Lf b = Ac . v,
+//   Lf^2 b = v^T Hess(b) v, Bc = Lf^2 b + alpha'(b) Lf b + alpha(Lf b + alpha(b)),
+//   alpha(x) = gamma x^5 (fifthAlpha, :23-29), gamma = 0.1 (:58).
+// The border barriers are b = kap rel_x + sig rel_y with (kap, sig) per the fov branch of
+// :211-231 (fov < pi: (tan(fov/2), +1) left, (tan(fov/2), -1) right; fov == pi: (1, 0);
+// pi < fov < 2 pi: (tan((2 pi - fov)/2), -1) left, (.., +1) right — GiNaC's `py >= 0` on a symbol
+// is false; fov == 2 pi: vacuous row).
+struct FovRow {
+    double a[3], b;
+    bool present;
+};
+
+static void fov_rows(const double* st, const double* tg, double fov, double Ds, double Rs, FovRow out[4]) {
+    const double gamma = 0.1;
+    const double px = st[0], py = st[1], th = st[2], vx = st[3], vy = st[4], w = st[5];
+    const double dx = tg[0] - px, dy = tg[1] - py;
+    const double c = std::cos(th), s = std::sin(th);
+    const double rx = c * dx + s * dy, ry = -s * dx + c * dy;
+    auto finish = [&](FovRow& r, double bval, double lf2) {
+        const double lf = r.a[0] * vx + r.a[1] * vy + r.a[2] * w;
+        const double alpha_b = gamma * std::pow(bval, 5);
+        const double lf_alpha = 5.0 * gamma * std::pow(bval, 4) * lf;
+        r.b = lf2 + lf_alpha + gamma * std::pow(lf + alpha_b, 5);
+        r.present = true;
+    };
+    // safety: b = |rel|^2 - Ds^2 = dx^2 + dy^2 - Ds^2 (rotation invariant)
+    {
+        FovRow& r = out[0];
+        r.a[0] = -2 * dx;
+        r.a[1] = -2 * dy;
+        r.a[2] = 0.0;
+        finish(r, dx * dx + dy * dy - Ds * Ds, 2 * (vx * vx + vy * vy));
+    }
+    // borders
+    auto border = [&](FovRow& r, double kap, double sig) {
+        const double bval = kap * rx + sig * ry;
+        r.a[0] = -kap * c + sig * s;
+        r.a[1] = -kap * s - sig * c;
+        r.a[2] = kap * ry - sig * rx;
+        const double lf2 = 2 * w * ((kap * s + sig * c) * vx + (-kap * c + sig * s) * vy) - w * w * bval;
+        finish(r, bval, lf2);
+    };
+    const bool full = std::fabs(fov - 2 * M_PI) <= 1e-9 * std::max(1.0, 2 * M_PI);  // isApproximatelyEqual
+    if (fov < M_PI) {
+        border(out[1], std::tan(fov / 2), +1.0);
+        border(out[2], std::tan(fov / 2), -1.0);
+    } else if (fov == M_PI) {
+        border(out[1], 1.0, 0.0);
+        border(out[2], 1.0, 0.0);
+    } else if (full) {
+        for (int k : {1, 2}) {
+            out[k].a[0] = out[k].a[1] = out[k].a[2] = 0.0;
+            out[k].b = std::numeric_limits<double>::max();
+            out[k].present = false;
+        }
+    } else {
+        const double t2 = std::tan((2 * M_PI - fov) / 2);
+        border(out[1], t2, -1.0);
+        border(out[2], t2, +1.0);
+    }
+    // range: b = Rs^2 - |rel|^2
+    {
+        FovRow& r = out[3];
+        r.a[0] = 2 * dx;
+        r.a[1] = 2 * dy;
+        r.a[2] = 0.0;
+        finish(r, Rs * Rs - dx * dx - dy * dy, -2 * (vx * vx + vy * vy));
+    }
+}
+
+// separating_hyperplanes::voronoi (separating_hyperplanes/src/Voronoi.cpp:10-29) of the planar
+// positions (last dimension zeroed, FovBezierIMPCCBF.cpp:135-141), shifted by the robot box
+// (math::shiftHyperplane, math/src/Helpers.cpp:20-36): n . x + off <= 0 with off the max over
+// the box corners. Returns the 3-vector normal and the shifted offset.
+static void voronoi_shifted(const double* self_xy, const double* other_xy, const double* bbox,
+                            double n[3], double* off) {
+    double d0 = other_xy[0] - self_xy[0], d1 = other_xy[1] - self_xy[1];
+    const double nrm = std::sqrt(d0 * d0 + d1 * d1);
+    if (nrm > 0) {  // Eigen normalize(): no-op on a zero vector
+        d0 /= nrm;
+        d1 /= nrm;
+    }
+    n[0] = d0;
+    n[1] = d1;
+    n[2] = 0.0;
+    const double mid0 = 0.5 * (self_xy[0] + other_xy[0]), mid1 = 0.5 * (self_xy[1] + other_xy[1]);
+    const double offset = -(n[0] * mid0 + n[1] * mid1);
+    double best = std::numeric_limits<double>::lowest();
+    for (int corner = 0; corner < 8; corner++) {
+        double v = offset;
+        for (int d = 0; d < 3; d++) v += n[d] * ((corner & (1 << d)) ? -bbox[d] : bbox[d]);
+        best = std::max(best, v);
+    }
+    *off = best;
+}
+
 struct Assembler {
     const orc_params* p;
     Layout L;
@@ -422,9 +523,11 @@ struct Assembler {
                 addRow(qp, row, target, target);
             }
         }
-        // addContinuityConstraint(p, d) for d <= continuity (:126-131) -> Generator :182-226
+        // addContinuityConstraint(p, d): d <= continuity for ConnectivityIMPCCBF (:126-131),
+        // d < continuity for FovBezierIMPCCBF (FovBezierIMPCCBF.cpp:107-113) -> Generator :182-226
+        const int dmax = p->cbf_mode == 1 ? L.cont - 1 : L.cont;
         for (int pc = 0; pc + 1 < L.P; pc++)
-            for (int d = 0; d <= L.cont; d++) {
+            for (int d = 0; d <= dmax; d++) {
                 std::vector<double> b1 = bernsteinBasis(L.C - 1, L.T, L.T, d);
                 std::vector<double> b2 = bernsteinBasis(L.C - 1, L.T, 0.0, d);
                 for (int dim = 0; dim < DIM; dim++) {
@@ -452,7 +555,45 @@ struct Assembler {
             if (nslack > 0) row[nc + nbi] = -1.0;  // ConnectivityMPCCBFQPGenerator.cpp:33-40
             addRow(qp, row, LOWEST, b + 0.0);     // slack_value = 0 (:138, :172)
         };
-        if (iter == 0) {
+        if (p->cbf_mode == 1) {
+            if (nslack > 0) throw std::runtime_error("FoV slack mode not supported");
+            // Voronoi rows on every control point of piece 0 (FovBezierIMPCCBF.cpp:130-147 ->
+            // BezierQPOperations::hyperplaneConstraintAll :270-285, epsilon 1e-8)
+            for (int i = 0; i < nb; i++) {
+                double nrm[3], off;
+                voronoi_shifted(st, nbs + 6 * i, p->bbox, nrm, &off);
+                for (int cp = 0; cp < L.C; cp++) {
+                    zero_row();
+                    for (int d = 0; d < DIM; d++) row[0 * L.n_piece + d * L.C + cp] = nrm[d];
+                    addRow(qp, row, LOWEST, -off - 1e-8);
+                }
+            }
+            // FoV CBF rows: iter 0 at the current state (:150-171), later iterations at the
+            // predicted states, per neighbour all k of one kind, then the next kind (:172-210)
+            auto fov_row = [&](const FovRow& fr, int k) {
+                zero_row();
+                for (int j = 0; j < nc; j++) {
+                    double sum = 0;
+                    for (int d = 0; d < DIM; d++) sum += fr.a[d] * U[(k * DIM + d) * nc + j];
+                    row[j] = -1.0 * sum;
+                }
+                addRow(qp, row, LOWEST, fr.b + 0.0);
+            };
+            for (int i = 0; i < nb; i++) {
+                const double* tg = nbs + 6 * i;  // target = neighbour position (x, y)
+                if (iter == 0) {
+                    FovRow fr[4];
+                    fov_rows(st, tg, p->fov_beta, p->fov_Ds, p->fov_Rs, fr);
+                    for (int r = 0; r < 4; r++) fov_row(fr[r], 0);
+                } else {
+                    std::vector<std::array<FovRow, 4>> per_k(p->cbf_horizon);
+                    for (int k = 0; k < p->cbf_horizon; k++)
+                        fov_rows(pred + 6 * k, tg, p->fov_beta, p->fov_Ds, p->fov_Rs, per_k[k].data());
+                    for (int r = 0; r < 4; r++)
+                        for (int k = 0; k < p->cbf_horizon; k++) fov_row(per_k[k][r], k);
+                }
+            }
+        } else if (iter == 0) {
             for (int i = 0; i < nb; i++) cbf_row(st, nbs + 6 * i, 0, i);
         } else {
             for (int i = 0; i < nb; i++)
@@ -1110,6 +1251,17 @@ void orc_safety_cbf(const double* st, const double* nb, double d_min, double* a3
     a3[0] = 2 * dx;
     a3[1] = 2 * dy;
     a3[2] = 0.0;
+}
+
+void orc_fov_cbf(const double* st, const double* tg, double fov, double Ds, double Rs, double* a12,
+                 double* b4, int32_t* present4) {
+    orc::FovRow fr[4];
+    orc::fov_rows(st, tg, fov, Ds, Rs, fr);
+    for (int r = 0; r < 4; r++) {
+        for (int d = 0; d < 3; d++) a12[3 * r + d] = fr[r].a[d];
+        b4[r] = fr[r].b;
+        if (present4) present4[r] = fr[r].present ? 1 : 0;
+    }
 }
 
 void orc_apply_input(double ts, const double* st, const double* u, double* out) {

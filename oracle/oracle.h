@@ -40,6 +40,14 @@ typedef struct orc_params {
     int32_t num_pieces, num_control_points;
     double piece_max_parameter;
     int32_t continuity_upto_degree;
+    /* controller family: 0 = ConnectivityIMPCCBF (collision CBF vs neighbour states),
+     * 1 = FovBezierIMPCCBF (FoV CBFs vs neighbour positions + Voronoi rows on piece 0,
+     *     continuity d < degree; mpc_cbf/src/controller/FovBezierIMPCCBF.cpp:44-223) */
+    int32_t cbf_mode;
+    double fov_beta;   /* field of view (rad), FovCBF ctor fov (cbf/src/detail/FovCBF.cpp:41) */
+    double fov_Ds;     /* safety distance Ds (= aligned_box[0] in the FoV example) */
+    double fov_Rs;     /* sensing range Rs (fov_cbf_params.Rs) */
+    double bbox[3];    /* robot aligned-box half extents (collision_shape.aligned_box) */
 } orc_params;
 
 /* Status codes: index of qpcpp::SolveStatus (qpcpp/include/qpcpp/solvers/Solver.h:13-21). */
@@ -58,6 +66,12 @@ int orc_bernstein_coefficient_matrix(uint64_t degree, double max_parameter, uint
 /* ConnectivityCBF safety row, closed form of ConnectivityCBF.cpp:152-198 (gamma 5, cubic alpha) */
 void orc_safety_cbf(const double* state6, const double* neighbor6, double d_min, double* a3,
                     double* b);
+/* FovCBF rows (cbf/src/detail/FovCBF.cpp:152-535, gamma 0.1, alpha(x) = gamma x^5) at ego state
+ * state6 = (px, py, th, vx, vy, w) against a static target other2 = (x, y): rows 0..3 = safety,
+ * left border, right border, range; a12 = 4 x (Ac over (ux, uy, uw)), b4 = Bc; present4[r] = 0
+ * for a vacuous row (fov = 2 pi: Ac = 0, Bc = max). */
+void orc_fov_cbf(const double* state6, const double* other2, double fov, double Ds, double Rs,
+                 double* a12, double* b4, int32_t* present4);
 /* DoubleIntegratorXYYaw(ts).applyInput (model/src/DoubleIntegrator.cpp:54-63) */
 void orc_apply_input(double ts, const double* state6, const double* u3, double* out6);
 /* get_A0(K).pos_ (3K x 6) and get_lambda(K).pos_ (3K x 3K) (DoubleIntegrator.cpp:9-51) */

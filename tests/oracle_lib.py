@@ -31,6 +31,8 @@ class OrcParams(C.Structure):
         ("slack_cost", C.c_double), ("slack_decay_rate", C.c_double),
         ("num_pieces", C.c_int32), ("num_control_points", C.c_int32),
         ("piece_max_parameter", C.c_double), ("continuity_upto_degree", C.c_int32),
+        ("cbf_mode", C.c_int32), ("fov_beta", C.c_double), ("fov_Ds", C.c_double),
+        ("fov_Rs", C.c_double), ("bbox", C.c_double * 3),
     ]
 
 
@@ -75,6 +77,7 @@ def lib():
         L.orc_bernstein_coefficient_matrix.argtypes = [C.c_uint64, C.c_double, C.c_uint64, dp]
         L.orc_safety_cbf.argtypes = [dp, dp, C.c_double, dp, dp]
         L.orc_apply_input.argtypes = [C.c_double, dp, dp, dp]
+        L.orc_fov_cbf.argtypes = [dp, dp, C.c_double, C.c_double, C.c_double, dp, dp, ip]
         L.orc_prediction_matrices.argtypes = [C.c_double, C.c_int32, dp, dp]
         L.orc_num_vars.argtypes = [C.POINTER(OrcParams), C.c_int32]
         L.orc_assemble_qp.argtypes = [C.POINTER(OrcParams), dp, dp, C.c_int32, dp, dp, C.c_int32,
@@ -213,6 +216,17 @@ def impc_batch(p: OrcParams, states, refs, row_ptr, col, first, count, nthreads=
                                   cl.ctypes.data_as(C.POINTER(C.c_int32)), first, count, nthreads,
                                   status.ctypes.data_as(C.POINTER(C.c_int32)), _d(obj), _d(xl))
     return dict(solved=int(solved), status=status, obj=obj, x_last=xl)
+
+
+def fov_cbf(state, target, fov, Ds, Rs):
+    """FovCBF rows (safety, left border, right border, range): (a (4, 3), b (4,), present (4,))."""
+    st = np.ascontiguousarray(state, dtype=np.float64)
+    tg = np.ascontiguousarray(target, dtype=np.float64)
+    a = np.zeros(12)
+    b = np.zeros(4)
+    pr = np.zeros(4, dtype=np.int32)
+    lib().orc_fov_cbf(_d(st), _d(tg), fov, Ds, Rs, _d(a), _d(b), pr.ctypes.data_as(C.POINTER(C.c_int32)))
+    return a.reshape(4, 3), b, pr
 
 
 def eval_curve(p: OrcParams, x, t, d):
