@@ -21,6 +21,7 @@ namespace mpccbf {
 hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
                        hipStream_t s);
 const char* impc_kernel_name(const DevOps& op, int variant);
+hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
 int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
                      double radius, int32_t* row_ptr, int32_t* col, void* scratch,
                      size_t scratch_bytes, hipStream_t s);
@@ -112,6 +113,8 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
         a.grid.inv_cell = 1.0 / b->knn_radius;
         a.grid.radius = b->knn_radius;
         a.grid.k = b->knn_k;
+        // FoV controller: only agents inside the field of view are observed neighbours
+        a.grid.cone = (c->dev.cbf_mode == 1 && c->dev.fov_beta < 2.0 * M_PI - 1e-9) ? 0.5 * c->dev.fov_beta : 0.0;
     }
     a.num_states = b->num_states;
     a.states = b->states;
@@ -128,7 +131,8 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.next_states = b->next_states;
     a.stamps = b->stamps;
     if (ev0) HIP_TRY(hipEventRecord(ev0, stream));
-    hipError_t e = launch_impc(c->dev, c->dbuf, a, c->variant, stream);
+    hipError_t e = c->dev.cbf_mode == 1 ? launch_impc_fov(c->dev, c->dbuf, a, stream)
+                                        : launch_impc(c->dev, c->dbuf, a, c->variant, stream);
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, stream);
     if (e == hipErrorInvalidValue)
         return fail(MPCCBF_ERR_CAPACITY, "no kernel instantiation for this reduced dimension / row count");
@@ -245,6 +249,35 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
             d.sep_rows_per_dim = rpd;
         }
     }
+    // FoV controller: Voronoi operators, dense 16-wide box rows, P / LP padded to 16 x 16
+    d.cbf_mode = p->cbf_mode;
+    d.C = p->num_control_points;
+    d.fov_beta = p->fov_beta;
+    d.fov_Ds = p->fov_Ds;
+    d.fov_Rs = p->fov_Rs;
+    for (int k = 0; k < 3; k++) d.bbox[k] = p->bbox[k];
+    if (p->cbf_mode == 1 && o.nz <= 15) {
+        pack(v, d.o_VZ, o.VZ);
+        pack(v, d.o_VS, o.VS);
+        std::vector<double> W((size_t)o.G.r * WBOX_ROW, 0.0);
+        for (int i = 0; i < o.G.r; i++) {
+            double* r = &W[(size_t)i * WBOX_ROW];
+            for (int j = 0; j < o.nz; j++) r[j] = o.G(i, j);
+            for (int s2 = 0; s2 < SD; s2++) r[16 + s2] = o.Gs(i, s2);
+            r[22] = o.lo[i];
+            r[23] = o.hi[i];
+        }
+        pack(v, d.o_Wbox, W);
+        std::vector<double> P16(256, 0.0), L16(256, 0.0);
+        for (int a = 0; a < 16; a++)
+            for (int b = 0; b < 16; b++) {
+                const bool in = a < o.nz && b < o.nz;
+                P16[a * 16 + b] = in ? o.Pr(a, b) : (a == b ? 1.0 : 0.0);
+                L16[a * 16 + b] = in ? o.LPr(a, b) : (a == b ? 1.0 : 0.0);
+            }
+        pack(v, d.o_P16, P16);
+        pack(v, d.o_LP16, L16);
+    }
     v.push_back(0.0);  // keep every offset addressable even for empty operators
     for (int i = 0; i < 3; i++) {
         d.a_lo[i] = o.a_lo[i];
@@ -288,6 +321,7 @@ int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
 
 const char* mpccbf_kernel_name(const mpccbf_ctx* c) {
     if (!c) return "";
+    if (c->dev.cbf_mode == 1) return "impc_fov_kernel";
     const char* n = impc_kernel_name(c->dev, c->variant);
     return n ? n : "";
 }

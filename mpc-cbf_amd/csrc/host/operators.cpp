@@ -144,6 +144,12 @@ std::string validate_params(const mpccbf_params& p) {
     if (p.num_pieces < 1 || p.num_control_points < 1) return "num_pieces and num_control_points must be >= 1";
     if (p.continuity_upto_degree < 0) return "bezier_continuity_upto_degree must be >= 0";
     if (p.slack_mode) return "slack_mode is not supported by this build yet (SURVEY.md §8f rank 2)";
+    if (p.cbf_mode != 0 && p.cbf_mode != 1) return "cbf_mode must be 0 (collision) or 1 (field of view)";
+    if (p.cbf_mode == 1) {
+        if (!(p.fov_beta > 0 && p.fov_beta <= 2 * M_PI + 1e-9)) return "fov must be in (0, 2 pi]";
+        if (!(p.fov_Ds >= 0) || !(p.fov_Rs > 0)) return "FoV safety distance must be >= 0 and range > 0";
+        if (p.continuity_upto_degree < 1) return "FoV controller needs bezier_continuity_upto_degree >= 1";
+    }
     return "";
 }
 
@@ -259,8 +265,11 @@ Operators build_operators(const mpccbf_params& p, bool keep_redundant) {
     std::vector<std::vector<double>> eq;
     for (int d = 0; d <= 1; d++)
         for (int dim = 0; dim < DIM; dim++) eq.push_back(cv.row_at(0.0, dim, d));
+    // C^d continuity: d <= degree (ConnectivityIMPCCBF.cpp:126-131), d < degree for the FoV
+    // controller (FovBezierIMPCCBF.cpp:107-113)
+    const int dmax = p.cbf_mode == 1 ? p.continuity_upto_degree - 1 : p.continuity_upto_degree;
     for (int pc = 0; pc + 1 < cv.P; pc++)
-        for (int d = 0; d <= p.continuity_upto_degree; d++)
+        for (int d = 0; d <= dmax; d++)
             for (int dim = 0; dim < DIM; dim++) {
                 std::vector<double> a = cv.row_local(pc, cv.T, dim, d);
                 std::vector<double> b = cv.row_local(pc + 1, 0.0, dim, d);
@@ -468,6 +477,14 @@ Operators build_operators(const mpccbf_params& p, bool keep_redundant) {
             }
         op.AZ = E * op.Z;
         op.AS = E * op.Xs;
+    }
+    if (p.cbf_mode == 1) {
+        for (int j = 0; j < cv.C; j++) {
+            Mat E(2, n);
+            for (int d = 0; d < 2; d++) E(d, 0 * cv.n_piece + d * cv.C + j) = 1.0;
+            op.VZ.push_back(E * op.Z);
+            op.VS.push_back(E * op.Xs);
+        }
     }
     for (int d = 0; d < DIM; d++) {
         op.a_lo[d] = p.a_min[d];

@@ -23,7 +23,15 @@ struct DevOps {
     // [g0, g1, Gs(6), lo, hi] (SEP_ROW doubles), 16 rows per channel (unused: inert g = 0, [-1, 1])
     int32_t sep, nzd, sep_rows_per_dim;
     int32_t o_Gsep;
+    // FoV controller (cbf_mode 1, impc_fov_kernel): Voronoi operators VZ (C x 2 x nz), VS (C x 2 x 6),
+    // box rows as dense 16-wide rows [g(16) | Gs(6) | lo | hi] (WBOX_ROW doubles), P and its
+    // Cholesky factor padded to 16 x 16 with the identity
+    int32_t cbf_mode, C;
+    double fov_beta, fov_Ds, fov_Rs, bbox[3];
+    int32_t o_VZ, o_VS, o_Wbox, o_P16, o_LP16;
 };
+
+constexpr int WBOX_ROW = 16 + 6 + 2;
 
 constexpr int SEP_ROW = 10;
 constexpr int SEP_NZD_HOST = 2;  // reduced variables per channel the separable kernel handles
@@ -36,7 +44,8 @@ struct GridArgs {
     uint32_t mask;
     double inv_cell;
     double radius;
-    int32_t k;  // keep the k nearest within radius
+    int32_t k;     // keep the k nearest within radius
+    double cone;   // > 0: keep only agents whose bearing is within +-cone of the ego yaw (FoV)
 };
 
 constexpr int NB_CAP = 64;  // grid-mode candidate capacity per agent (LDS)

@@ -1,0 +1,370 @@
+// impc_common.hpp — device steps shared by the IMPC kernels (impc_kernel.hip, impc_fov.hip):
+// the collision HOCBF row, the in-kernel neighbour query, the state-dependent linear term, the
+// constant-row check, CBF-row staging, objective and output writes, diagnostics stamps.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "group.hpp"
+#include "impc.hpp"
+
+namespace mpccbf {
+namespace dev {
+
+__device__ __forceinline__ const double* opp(const double* buf, int off) { return buf + off; }
+
+// Safety HOCBF row of ConnectivityCBF::initSafetyCBF (cbf/src/detail/ConnectivityCBF.cpp:152-198)
+// evaluated at (ego e, neighbour nb): a = L_g L_f h = (2dx, 2dy, 0),
+// b = L_f^2 h + L_f alpha(h) + alpha(L_f h + alpha(h)), alpha(x) = 5 x^3 (gamma = 5, :62, :19-21),
+// where L_f alpha differentiates the ego position only (f = A x, :171-184).
+__device__ __forceinline__ void safety_cbf(const double e[6], double npx, double npy, double nvx,
+                                           double nvy, double dmin, double a[3], double& b) {
+    constexpr double gamma = 5.0;
+    const double dx = e[0] - npx, dy = e[1] - npy;
+    const double dvx = e[3] - nvx, dvy = e[4] - nvy;
+    const double hh = dx * dx + dy * dy - dmin * dmin;
+    const double lfh = 2.0 * (dx * dvx + dy * dvy);
+    const double lf2h = 2.0 * (dvx * dvx + dvy * dvy);
+    const double alpha_h = gamma * hh * hh * hh;
+    const double lf_alpha = 3.0 * gamma * hh * hh * (2.0 * dx * e[3] + 2.0 * dy * e[4]);
+    const double psi = lfh + alpha_h;
+    b = lf2h + lf_alpha + gamma * psi * psi * psi;
+    a[0] = 2.0 * dx;
+    a[1] = 2.0 * dy;
+    a[2] = 0.0;
+}
+
+// Per-group LDS scratch of the grid neighbour query.
+struct NbScratch {
+    int32_t idx[NB_CAP];   // candidate / final neighbour indices
+    int32_t tmp[NB_CAP];   // sorted output
+    double d2[NB_CAP];     // candidate squared distances
+    int32_t keep[NB_CAP];  // k-nearest flags
+};
+
+// k nearest other agents (planar distance, ties by index) within the radius, found through the
+// spatial hash; the result is left in sc.idx sorted by agent index. Returns the count, or -1 if
+// more than NB_CAP candidates lie within the radius. Distance-only test: agents of a colliding
+// cell that share a bucket are still filtered by distance, and a bucket reached from two of the
+// 9 cells is scanned once.
+template <int G>
+__device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double py, NbScratch& sc,
+                              int gl, double yaw = 0.0) {
+    const GridArgs& gr = args.grid;
+    const long long cx = (long long)floor(px * gr.inv_cell), cy = (long long)floor(py * gr.inv_cell);
+    const double r2 = gr.radius * gr.radius;
+    uint32_t hs[9], b0[9], b1[9];
+#pragma unroll
+    for (int c = 0; c < 9; c++) {
+        hs[c] = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
+        b0[c] = gr.start[hs[c]];
+        b1[c] = gr.start[hs[c] + 1];
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int c = 0; c < 9; c++) {
+        bool dup = false;
+#pragma unroll
+        for (int p = 0; p < c; p++) dup = dup || (hs[p] == hs[c]);
+        if (dup) continue;
+        for (uint32_t base = b0[c]; base < b1[c]; base += G) {
+            const uint32_t e = base + gl;
+            bool keep = false;
+            int j = -1;
+            double d2 = 0.0;
+            if (e < b1[c]) {
+                j = (int)gr.sorted[e];
+                const double ex = args.states[(size_t)j * 6] - px;
+                const double ey = args.states[(size_t)j * 6 + 1] - py;
+                d2 = ex * ex + ey * ey;
+                keep = (j != self) && (d2 <= r2);
+                if (keep && gr.cone > 0.0) {  // inside the field of view (strict)
+                    double off = atan2(ey, ex) - yaw;
+                    off -= 6.283185307179586 * rint(off * 0.15915494309189535);
+                    keep = fabs(off) < gr.cone;
+                }
+            }
+            const unsigned long long msk = grp_ballot<G>(keep);
+            const int slot = cnt + __popcll(msk & ((1ull << gl) - 1ull));
+            if (keep && slot < NB_CAP) {
+                sc.idx[slot] = j;
+                sc.d2[slot] = d2;
+            }
+            cnt += __popcll(msk);
+        }
+    }
+    if (cnt > NB_CAP) return -1;
+    wave_lds_sync();
+    // rank by (d2, index): keep the k nearest
+    const int k = gr.k;
+    for (int i = gl; i < cnt; i += G) {
+        const double di = sc.d2[i];
+        const int ji = sc.idx[i];
+        int rank = 0;
+        for (int m = 0; m < cnt; m++) {
+            const double dm = sc.d2[m];
+            rank += (dm < di || (dm == di && sc.idx[m] < ji)) ? 1 : 0;
+        }
+        sc.keep[i] = rank < k ? 1 : 0;
+    }
+    const int nk = cnt < k ? cnt : k;
+    wave_lds_sync();
+    // order the kept set by agent index
+    for (int i = gl; i < cnt; i += G) {
+        if (sc.keep[i]) {
+            const int ji = sc.idx[i];
+            int pos = 0;
+            for (int m = 0; m < cnt; m++) pos += (sc.keep[m] && sc.idx[m] < ji) ? 1 : 0;
+            sc.tmp[pos] = ji;
+        }
+    }
+    wave_lds_sync();
+    for (int i = gl; i < nk; i += G) sc.idx[i] = sc.tmp[i];
+    wave_lds_sync();
+    return nk;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Steps shared by both layouts
+// ---------------------------------------------------------------------------------------------
+
+// q = Qs s0 + Qt t (or Qs s0 + Qr ref tail) and the objective constant.
+template <int NZ>
+__device__ __forceinline__ void agent_linear_term(const DevOps& op, const double* buf,
+                                                  const ImpcArgs& args, int ai, const double (&s0)[6],
+                                                  double (&q)[NZ], double& kconst) {
+    const double* Qs = opp(buf, op.o_Qs);
+    const double* Ks = opp(buf, op.o_Ks);
+    kconst = 0.0;
+#pragma unroll
+    for (int i = 0; i < NZ; i++) {
+        double v = 0.0;
+#pragma unroll
+        for (int s = 0; s < 6; s++) v = fma(Qs[i * 6 + s], s0[s], v);
+        q[i] = v;
+    }
+#pragma unroll
+    for (int s = 0; s < 6; s++) {
+        double v = 0.0;
+#pragma unroll
+        for (int u = 0; u < 6; u++) v = fma(Ks[s * 6 + u], s0[u], v);
+        kconst = fma(s0[s], v, kconst);
+    }
+    if (args.targets) {
+        const double* Qt = opp(buf, op.o_Qt);
+        const double* Kt = opp(buf, op.o_Kt);
+        double t[3];
+#pragma unroll
+        for (int d = 0; d < 3; d++) t[d] = args.targets[(size_t)ai * 3 + d];
+#pragma unroll
+        for (int i = 0; i < NZ; i++)
+#pragma unroll
+            for (int d = 0; d < 3; d++) q[i] = fma(Qt[i * 3 + d], t[d], q[i]);
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) v = fma(Kt[d * 6 + s], s0[s], v);
+            kconst = fma(t[d], v, kconst);
+        }
+    } else {
+        const double* Qr = opp(buf, op.o_Qr);
+        const double* Kr = opp(buf, op.o_Kr);
+        const int nr = 3 * op.spd_f;
+        const double* rt = args.refs + (size_t)ai * 3 * op.K + 3 * (op.K - op.spd_f);
+        for (int j = 0; j < nr; j++) {
+            const double rv = rt[j];
+#pragma unroll
+            for (int i = 0; i < NZ; i++) q[i] = fma(Qr[i * nr + j], rv, q[i]);
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) v = fma(Kr[j * 6 + s], s0[s], v);
+            kconst = fma(rv, v, kconst);
+        }
+    }
+}
+
+// Constant rows (zero in y): pure feasibility checks on s0, group-uniform result.
+template <int G>
+__device__ __forceinline__ bool constant_rows_infeasible(const DevOps& op, const double* buf,
+                                                         const double (&s0)[6], int gl) {
+    const double* Cs = opp(buf, op.o_Cs);
+    const double* clo = opp(buf, op.o_clo);
+    const double* chi = opp(buf, op.o_chi);
+    bool bad = false;
+    for (int i = gl; i < op.mc; i += G) {
+        double v = 0.0;
+#pragma unroll
+        for (int s = 0; s < 6; s++) v = fma(Cs[i * 6 + s], s0[s], v);
+        if (v < clo[i] - op.feas_tol || v > chi[i] + op.feas_tol) bad = true;
+    }
+    return grp_ballot<G>(bad) != 0ull;
+}
+
+// Ego state the CBF rows are evaluated at: s0 (iteration 0) or the previous curve at
+// h_samples(k) (iteration 1, ConnectivityIMPCCBF.cpp:161-168).
+template <int NZ>
+__device__ __forceinline__ void cbf_ego_state(const DevOps& op, const double* buf, int it, int k,
+                                              const double (&s0)[6], const double (&y)[NZ], double (&e)[6]) {
+    if (it == 0) {
+#pragma unroll
+        for (int s = 0; s < 6; s++) e[s] = s0[s];
+        return;
+    }
+    const double* PZ = opp(buf, op.o_PZ) + (size_t)k * 6 * NZ;
+    const double* PS = opp(buf, op.o_PS) + (size_t)k * 36;
+#pragma unroll
+    for (int s = 0; s < 6; s++) {
+        double v = 0.0;
+#pragma unroll
+        for (int u = 0; u < 6; u++) v = fma(PS[s * 6 + u], s0[u], v);
+#pragma unroll
+        for (int j = 0; j < NZ; j++) v = fma(PZ[s * NZ + j], y[j], v);
+        e[s] = v;
+    }
+}
+
+// CBF rows of one IMPC iteration, filtered and compacted into `stage` ((NZ + 1) doubles per
+// row: coefficients then upper bound). Returns the group-uniform row count; *infeasible is set
+// when a single row already excludes every acceleration in the box.
+template <int NZ, int G>
+__device__ int stage_cbf_rows(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
+                              const double (&s0)[6], const double (&y)[NZ], bool grid_mode,
+                              const int32_t* nbl, int nb0, int nnb, double* stage, int cap, int gl,
+                              bool* infeasible) {
+    const double* UZ = opp(buf, op.o_UZ);
+    const double* US = opp(buf, op.o_US);
+    const int nk = (it == 0) ? 1 : op.cbf_h;
+    int count = 0;
+    bool row_infeasible = false;
+    for (int k = 0; k < nk; k++) {
+        double e[6];
+        cbf_ego_state<NZ>(op, buf, it, k, s0, y, e);
+        // U_k s0 part of the acceleration at sample k
+        const double* UZk = UZ + (size_t)k * 3 * NZ;
+        const double* USk = US + (size_t)k * 18;
+        double us[3];
+#pragma unroll
+        for (int d = 0; d < 3; d++) {
+            double v = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) v = fma(USk[d * 6 + s], s0[s], v);
+            us[d] = v;
+        }
+        for (int base = 0; base < nnb; base += G) {
+            const int j = base + gl;
+            bool keep = false;
+            double a[3] = {0.0, 0.0, 0.0}, b = 0.0;
+            if (j < nnb) {
+                const int nbi = grid_mode ? nbl[j] : args.nb_col[nb0 + j];
+                const double* ns = args.states + (size_t)nbi * 6;
+                safety_cbf(e, ns[0], ns[1], ns[3], ns[4], op.d_min, a, b);
+                // max / min of -a^T u over the acceleration box at sample k (those box rows
+                // are part of every QP): b >= max  -> the row is implied (exactly redundant);
+                // b < min - tol -> no acceleration satisfies it (infeasible).
+                double bmax = 0.0, bmin = 0.0;
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    const double v1 = -a[d] * op.a_lo[d], v2 = -a[d] * op.a_hi[d];
+                    bmax += fmax(v1, v2);
+                    bmin += fmin(v1, v2);
+                }
+                keep = !(op.cbf_filter && b >= bmax);
+                if (b < bmin - op.feas_tol) row_infeasible = true;
+            }
+            const unsigned long long msk = grp_ballot<G>(keep);
+            const int slot = count + __popcll(msk & ((1ull << gl) - 1ull));
+            if (keep && slot < cap) {
+                double* dst = stage + (size_t)slot * (NZ + 1);
+                // row: -a^T (US_k s0 + UZ_k y) <= b
+#pragma unroll
+                for (int jz = 0; jz < NZ; jz++)
+                    dst[jz] = -(a[0] * UZk[jz] + a[1] * UZk[NZ + jz] + a[2] * UZk[2 * NZ + jz]);
+                dst[NZ] = b + (a[0] * us[0] + a[1] * us[1] + a[2] * us[2]);
+            }
+            count += __popcll(msk);
+        }
+    }
+    *infeasible = grp_ballot<G>(row_infeasible) != 0ull;
+    wave_lds_sync();
+    return count;
+}
+
+// Objective value 1/2 y^T P y + q^T y + k at the solution (x^T H x + c^T x of the full QP).
+template <int NZ>
+__device__ __forceinline__ double reduced_objective(const DevOps& op, const double* buf,
+                                                   const double (&q)[NZ], const double (&y)[NZ],
+                                                   double kconst) {
+    const double* Pr = opp(buf, op.o_Pr);
+    double v = kconst;
+#pragma unroll
+    for (int i = 0; i < NZ; i++) {
+        double pyi = 0.0;
+#pragma unroll
+        for (int j = 0; j < NZ; j++) pyi = fma(Pr[i * NZ + j], y[j], pyi);
+        v = fma(y[i], 0.5 * pyi + q[i], v);
+    }
+    return v;
+}
+
+// Control points of the kept curve and the closed-loop next state (curve at t = h).
+template <int NZ, int G>
+__device__ __forceinline__ void write_agent_outputs(const DevOps& op, const double* buf,
+                                                    const ImpcArgs& args, int ai, int gl,
+                                                    const double (&s0)[6], const double (&yk)[NZ],
+                                                    bool have_curve) {
+    if (args.x) {
+        const double* Z = opp(buf, op.o_Z);
+        const double* Xs = opp(buf, op.o_Xs);
+        for (int i = gl; i < op.n; i += G) {
+            double v = 0.0;
+            if (have_curve) {
+#pragma unroll
+                for (int s = 0; s < 6; s++) v = fma(Xs[i * 6 + s], s0[s], v);
+#pragma unroll
+                for (int j = 0; j < NZ; j++) v = fma(Z[i * NZ + j], yk[j], v);
+            } else {
+                v = __builtin_nan("");
+            }
+            args.x[(size_t)ai * op.n + i] = v;
+        }
+    }
+    if (args.next_states && gl < 6) {
+        double v = 0.0;
+        if (have_curve) {
+            const double* AZ = opp(buf, op.o_AZ);
+            const double* AS = opp(buf, op.o_AS);
+#pragma unroll
+            for (int s = 0; s < 6; s++) v = fma(AS[gl * 6 + s], s0[s], v);
+#pragma unroll
+            for (int j = 0; j < NZ; j++) v = fma(AZ[gl * NZ + j], yk[j], v);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 6; s++)
+                if (s == gl) v = s0[s];
+        }
+        args.next_states[(size_t)ai * 6 + gl] = v;
+    }
+}
+
+// diagnostics: wall-clock stamp (s_memrealtime, 100 MHz, chip-wide) of phase `k` of agent ai
+__device__ __forceinline__ void stamp(const ImpcArgs& args, int ai, int gl, int k) {
+    if (args.stamps) {
+        const long long t = (long long)__builtin_amdgcn_s_memrealtime();
+        if (gl == 0) args.stamps[(size_t)ai * NSTAMP + k] = t;
+    }
+}
+
+__device__ __forceinline__ void write_iteration(const ImpcArgs& args, size_t oi, int gl, int st,
+                                                double obj, int iters) {
+    if (gl == 0) {
+        if (args.status) args.status[oi] = st;
+        if (args.obj) args.obj[oi] = obj;
+        if (args.iters) args.iters[oi] = iters;
+    }
+}
+
+}  // namespace dev
+}  // namespace mpccbf

@@ -1,0 +1,291 @@
+// impc_fov.hip — FovBezierIMPCCBF::optimize (mpc_cbf/src/controller/FovBezierIMPCCBF.cpp:44-223)
+// for a batch of agents, one agent per wavefront (BASELINE config 5).
+//
+// Per agent and IMPC iteration the QP has 15 free variables (4 Bezier pieces, C^0..C^2
+// continuity eliminated), the shared box rows (two-sided), and per observed neighbour
+//   * 4 Voronoi rows on the piece-0 control points (separating_hyperplanes::voronoi shifted by
+//     the robot box, hyperplaneConstraintAll, epsilon 1e-8), in both iterations, and
+//   * 4 FoV HOCBF rows (safety, left / right FoV border, range; FovCBF.cpp:152-535) at the
+//     current state (iteration 0) or at each predicted state (iteration 1), with the exact
+//     acceleration-box redundancy filter of the collision path.
+// Rows are staged as a dense 16-wide image in LDS and solved by pdip_wave.hpp (MFMA Gram).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "impc.hpp"
+#include "impc_common.hpp"
+#include "pdip_wave.hpp"
+
+namespace mpccbf {
+namespace dev {
+
+// FoV HOCBF rows at ego e against target (tx, ty): closed form of FovCBF::init*CBF with
+// alpha(x) = 0.1 x^5 (see oracle/oracle.cpp fov_rows for the derivation). present = false for
+// the vacuous border rows of a 360-degree field of view.
+__device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double tx, double ty, double fov,
+                                            double Ds, double Rs, double a[3], double& b, bool& present) {
+    constexpr double gamma = 0.1;
+    const double vx = e[3], vy = e[4], w = e[5];
+    const double dx = tx - e[0], dy = ty - e[1];
+    double sn, cs;
+    sincos(e[2], &sn, &cs);
+    const double rx = cs * dx + sn * dy, ry = -sn * dx + cs * dy;
+    double bval, lf2;
+    present = true;
+    if (kind == 0 || kind == 3) {
+        const double sgn = kind == 0 ? 1.0 : -1.0;  // safety: |d|^2 - Ds^2, range: Rs^2 - |d|^2
+        a[0] = -2.0 * sgn * dx;
+        a[1] = -2.0 * sgn * dy;
+        a[2] = 0.0;
+        bval = kind == 0 ? dx * dx + dy * dy - Ds * Ds : Rs * Rs - dx * dx - dy * dy;
+        lf2 = 2.0 * sgn * (vx * vx + vy * vy);
+    } else {
+        double kap, sig;
+        const bool left = kind == 1;
+        if (fov < M_PI) {
+            kap = tan(0.5 * fov);
+            sig = left ? 1.0 : -1.0;
+        } else if (fov == M_PI) {
+            kap = 1.0;
+            sig = 0.0;
+        } else if (fabs(fov - 2.0 * M_PI) <= 1e-9 * 2.0 * M_PI) {
+            a[0] = a[1] = a[2] = 0.0;
+            b = 1.7976931348623157e308;
+            present = false;
+            return;
+        } else {
+            kap = tan(0.5 * (2.0 * M_PI - fov));
+            sig = left ? -1.0 : 1.0;
+        }
+        bval = kap * rx + sig * ry;
+        a[0] = -kap * cs + sig * sn;
+        a[1] = -kap * sn - sig * cs;
+        a[2] = kap * ry - sig * rx;
+        lf2 = 2.0 * w * ((kap * sn + sig * cs) * vx + (-kap * cs + sig * sn) * vy) - w * w * bval;
+    }
+    const double lf = a[0] * vx + a[1] * vy + a[2] * w;
+    const double b2 = bval * bval, b4 = b2 * b2;
+    const double psi = lf + gamma * b4 * bval;
+    const double p2 = psi * psi;
+    b = lf2 + 5.0 * gamma * b4 * lf + gamma * p2 * p2 * psi;
+}
+
+constexpr int FOV_NB_CAP = 16;  // observed neighbours per agent
+
+__global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const double* __restrict__ buf,
+                                                       const ImpcArgs args) {
+    constexpr int NZ = 15;
+    const int lane = threadIdx.x;
+    const int ai = blockIdx.x;
+    if (ai >= args.num_agents) return;
+    stamp(args, ai, lane, 0);
+    __shared__ double Gimg[WROWS * WNZ];
+    __shared__ double rlo[WROWS], rhi[WROWS], rml[WROWS];
+    __shared__ WaveScratch sc;
+    __shared__ NbScratch nb_scratch;
+    __shared__ int32_t row_count;
+
+    const int self = args.agent_first + ai;
+    double s0[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) s0[k] = args.states[(size_t)self * 6 + k];
+    double q15[NZ], kconst;
+    agent_linear_term<NZ>(op, buf, args, ai, s0, q15, kconst);
+    double q[WNZ];
+#pragma unroll
+    for (int j = 0; j < NZ; j++) q[j] = q15[j];
+    q[WNZ - 1] = 0.0;
+
+    // ---- shared box rows into the image (rows 0 .. mb-1), bounds shifted by Gs s0
+    const int mb = op.m;
+    {
+        const double* W = opp(buf, op.o_Wbox);
+        for (int r = lane; r < mb; r += 64) {
+            const double* src = W + (size_t)r * WBOX_ROW;
+            double sh = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; k++) sh = fma(src[WNZ + k], s0[k], sh);
+#pragma unroll
+            for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = src[j];
+            rlo[r] = src[WNZ + 6] - sh;
+            rhi[r] = src[WNZ + 7] - sh;
+            rml[r] = 1.0;
+        }
+    }
+    const bool infeasible = constant_rows_infeasible<64>(op, buf, s0, lane);
+    stamp(args, ai, lane, 1);
+
+    const bool grid_mode = args.nb_row_ptr == nullptr;
+    int nb0 = 0, nnb = 0;
+    if (!grid_mode) {
+        nb0 = args.nb_row_ptr[ai];
+        nnb = args.nb_row_ptr[ai + 1] - nb0;
+    } else {
+        nnb = grid_neighbors<64>(args, self, s0[0], s0[1], nb_scratch, lane, s0[2]);
+    }
+    const bool nb_overflow = nnb < 0 || nnb > FOV_NB_CAP;
+    if (nb_overflow) nnb = 0;
+    stamp(args, ai, lane, 2);
+
+    double y[WNZ], ykeep[NZ];
+#pragma unroll
+    for (int j = 0; j < WNZ; j++) y[j] = 0.0;
+#pragma unroll
+    for (int j = 0; j < NZ; j++) ykeep[j] = 0.0;
+    bool have_curve = false, success = true;
+    const PdipCfg cfg{op.maxit, op.tol};
+    const int C = op.C;
+
+    for (int it = 0; it < op.impc_iter; it++) {
+        const size_t oi = (size_t)ai * op.impc_iter + it;
+        if (!success) {
+            write_iteration(args, oi, lane, ST_UNKNOWN, __builtin_nan(""), 0);
+            continue;
+        }
+        // ---- Voronoi rows: rows mb .. mb + nnb*C - 1 (same in every iteration)
+        const int nvor = nnb * C;
+        for (int v = lane; v < nvor; v += 64) {
+            const int i = v / C, j = v % C;
+            const int nbi = grid_mode ? nb_scratch.idx[i] : args.nb_col[nb0 + i];
+            const double ox = args.states[(size_t)nbi * 6], oy = args.states[(size_t)nbi * 6 + 1];
+            double nx = ox - s0[0], ny = oy - s0[1];
+            const double nrm = sqrt(nx * nx + ny * ny);
+            if (nrm > 0.0) {
+                nx /= nrm;
+                ny /= nrm;
+            }
+            const double off = -(nx * 0.5 * (s0[0] + ox) + ny * 0.5 * (s0[1] + oy)) +
+                               op.bbox[0] * fabs(nx) + op.bbox[1] * fabs(ny);
+            const double* VZ = opp(buf, op.o_VZ) + (size_t)j * 2 * NZ;
+            const double* VS = opp(buf, op.o_VS) + (size_t)j * 12;
+            const int r = mb + v;
+            double sh = 0.0;
+#pragma unroll
+            for (int k = 0; k < 6; k++) sh = fma(nx * VS[k] + ny * VS[6 + k], s0[k], sh);
+#pragma unroll
+            for (int jz = 0; jz < NZ; jz++) Gimg[r * WNZ + jz] = nx * VZ[jz] + ny * VZ[NZ + jz];
+            Gimg[r * WNZ + NZ] = 0.0;
+            rlo[r] = 0.0;
+            rml[r] = 0.0;
+            rhi[r] = -off - 1e-8 - sh;
+        }
+        // ---- FoV CBF rows, compacted after the Voronoi rows
+        const int nk = (it == 0) ? 1 : op.cbf_h;
+        const int base = mb + nvor;
+        int count = 0;
+        bool row_infeasible = false;
+        const double* UZ = opp(buf, op.o_UZ);
+        const double* US = opp(buf, op.o_US);
+        const int ntask = nnb * 4 * nk;
+        for (int t0 = 0; t0 < ntask; t0 += 64) {
+            const int task = t0 + lane;
+            bool keep = false;
+            double a[3] = {0.0, 0.0, 0.0}, bb = 0.0, us[3] = {0.0, 0.0, 0.0};
+            int k = 0;
+            if (task < ntask) {
+                // order of FovBezierIMPCCBF.cpp:150-210: per neighbour, per kind, per k
+                const int i = task / (4 * nk), kind = (task / nk) % 4;
+                k = task % nk;
+                const int nbi = grid_mode ? nb_scratch.idx[i] : args.nb_col[nb0 + i];
+                double e[6];
+                cbf_ego_state<NZ>(op, buf, it, k, s0, ykeep, e);
+                bool present;
+                fov_cbf_row(kind, e, args.states[(size_t)nbi * 6], args.states[(size_t)nbi * 6 + 1],
+                            op.fov_beta, op.fov_Ds, op.fov_Rs, a, bb, present);
+                double bmax = 0.0, bmin = 0.0;
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    const double v1 = -a[d] * op.a_lo[d], v2 = -a[d] * op.a_hi[d];
+                    bmax += fmax(v1, v2);
+                    bmin += fmin(v1, v2);
+                }
+                keep = present && !(op.cbf_filter && bb >= bmax);
+                if (present && bb < bmin - op.feas_tol) row_infeasible = true;
+                const double* USk = US + (size_t)k * 18;
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int s = 0; s < 6; s++) v = fma(USk[d * 6 + s], s0[s], v);
+                    us[d] = v;
+                }
+            }
+            const unsigned long long msk = __ballot(keep);
+            const int slot = count + __popcll(msk & ((1ull << lane) - 1ull));
+            if (keep && base + slot < WROWS) {
+                const int r = base + slot;
+                const double* UZk = UZ + (size_t)k * 3 * NZ;
+#pragma unroll
+                for (int jz = 0; jz < NZ; jz++)
+                    Gimg[r * WNZ + jz] = -(a[0] * UZk[jz] + a[1] * UZk[NZ + jz] + a[2] * UZk[2 * NZ + jz]);
+                Gimg[r * WNZ + NZ] = 0.0;
+                rlo[r] = 0.0;
+                rml[r] = 0.0;
+                rhi[r] = bb + a[0] * us[0] + a[1] * us[1] + a[2] * us[2];
+            }
+            count += __popcll(msk);
+        }
+        row_infeasible = __ballot(row_infeasible) != 0ull;
+        const int mtot = base + count;
+        const int nchunk = (mtot + 3) / 4;
+        // zero the image rows that complete the last chunk
+        for (int r = mtot + lane; r < 4 * nchunk && r < WROWS; r += 64)
+#pragma unroll
+            for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = 0.0;
+        wave_lds_sync();
+        if (it < 2) stamp(args, ai, lane, 3 + 2 * it);
+        int st;
+        int nit = 0;
+        if (mtot > WROWS || nb_overflow) {
+            st = ST_ERROR;  // capacity (rows per agent / observed neighbours)
+        } else if (infeasible || row_infeasible) {
+            st = ST_INFEASIBLE;
+        } else {
+            WaveRows rw;
+#pragma unroll
+            for (int s = 0; s < WR; s++) {
+                const int r = wave_owner_row(lane, s);
+                const bool on = r < mtot;
+#pragma unroll
+                for (int j = 0; j < WNZ; j++) rw.g[s][j] = on ? Gimg[r * WNZ + j] : 0.0;
+                rw.lo[s] = on ? rlo[r] : -1.0;
+                rw.hi[s] = on ? rhi[r] : 1.0;
+                rw.ml[s] = on ? rml[r] : 1.0;
+            }
+            const PdipOut po = pdip_solve_wave(rw, Gimg, nchunk, sc, opp(buf, op.o_P16), opp(buf, op.o_LP16),
+                                               q, y, cfg, lane);
+            st = po.status;
+            nit = po.iters;
+            if (st != ST_OPTIMAL) {
+                const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);
+                if (tstar > op.feas_tol) st = ST_INFEASIBLE;
+            }
+        }
+        double objv = __builtin_nan("");
+        if (st == ST_OPTIMAL) {
+#pragma unroll
+            for (int j = 0; j < NZ; j++) ykeep[j] = y[j];
+            objv = reduced_objective<NZ>(op, buf, q15, ykeep, kconst);
+            have_curve = true;
+        } else {
+            success = false;
+        }
+        write_iteration(args, oi, lane, st, objv, nit);
+        if (it < 2) stamp(args, ai, lane, 4 + 2 * it);
+        wave_lds_sync();
+    }
+    write_agent_outputs<NZ, 64>(op, buf, args, ai, lane, s0, ykeep, have_curve);
+    stamp(args, ai, lane, 7);
+}
+
+}  // namespace dev
+
+hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
+    if (a.num_agents <= 0) return hipSuccess;
+    if (op.nz != 15 || op.m > dev::WROWS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(dev::impc_fov_kernel, dim3(a.num_agents), dim3(64), 0, s, op, buf, a);
+    return hipGetLastError();
+}
+
+}  // namespace mpccbf

@@ -1125,8 +1125,28 @@ struct Solution {
     double kkt[4];
 };
 
-Solution solve(const DenseQP& q) {
+// Rows whose finite bound dwarfs any attainable activity (FoV HOCBF bounds reach 1e30+ through
+// alpha(x) = 0.1 x^5) wreck the interior-point scaling; dividing such a row by a positive
+// constant leaves the feasible set unchanged. Rows with |bound| > 1e6 are scaled to |bound| 1e6.
+static DenseQP scale_huge_rows(const DenseQP& q) {
+    DenseQP r = q;
+    for (int i = 0; i < r.m; i++) {
+        if (r.lo[i] == r.hi[i]) continue;
+        double b = 0.0;
+        if (!is_neg_inf(r.lo[i])) b = std::max(b, std::fabs(r.lo[i]));
+        if (!is_pos_inf(r.hi[i])) b = std::max(b, std::fabs(r.hi[i]));
+        if (!(b > 1e6)) continue;
+        const double f = 1e6 / b;
+        for (int j = 0; j < r.n; j++) r.A[(size_t)i * r.n + j] *= f;
+        if (!is_neg_inf(r.lo[i])) r.lo[i] *= f;
+        if (!is_pos_inf(r.hi[i])) r.hi[i] *= f;
+    }
+    return r;
+}
+
+Solution solve(const DenseQP& q_in) {
     Solution out;
+    const DenseQP q = scale_huge_rows(q_in);
     Solver s(q);
     Solver::Result r = s.pdip(200, 1e-10);
     if (r.status == ORC_OPTIMAL) s.polish(r);

@@ -259,3 +259,39 @@ def test_run_steps_with_single_rank_communicator(mpclib):
     torch.cuda.synchronize()
     comm.close()
     np.testing.assert_array_equal(r["final"].cpu().numpy(), ref_states)
+
+
+@pytest.mark.parametrize("scale,n_agents", [(1.0, 64), (0.7, 100)])
+def test_fov_controller_matches_oracle(mpclib, scale, n_agents):
+    """BASELINE config 5 (FovBezierIMPCCBF): FoV + Voronoi rows, 15 free variables, MFMA
+    Newton matrix (impc_fov_kernel) against the oracle on the same observed-neighbour lists."""
+    torch = _torch()
+    cfg = swarm.fov_config(20)
+    states, targets = swarm.heading_swarm(n_agents, seed=2)
+    states[:, :2] *= scale
+    rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+    ctx = mpclib.Context(cfg)
+    assert ctx.kernel_name == "impc_fov_kernel"
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    agents = list(range(n_agents))
+    ref = run_oracle(cfg, states, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
+
+
+def test_fov_grid_neighbours_match_csr(mpclib):
+    """Device FoV neighbour query (grid + field-of-view cone) == the CPU observed-neighbour lists."""
+    torch = _torch()
+    cfg = swarm.fov_config(20)
+    states, targets = swarm.heading_swarm(400, seed=6)
+    states[:, :2] *= 0.7
+    rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+    ctx = mpclib.Context(cfg)
+    g_csr = run_gpu(ctx, states, targets, rp, col, torch)
+    dev = torch.device("cuda", 0)
+    out = ctx.alloc_outputs(len(states))
+    ctx.impc_solve(torch.tensor(states, device=dev), targets=torch.tensor(targets, device=dev),
+                   knn_k=8, knn_radius=cfg["fov_Rs"], **out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), g_csr["status"])
+    ok = g_csr["status"] == 0
+    np.testing.assert_allclose(out["obj"].cpu().numpy()[ok], g_csr["obj"][ok], rtol=1e-10, atol=1e-9)
