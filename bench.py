@@ -35,9 +35,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--agents-per-gpu", type=int, default=4096)
+    ap.add_argument("--workload", choices=["collision", "fov"], default="collision",
+                    help="collision: BASELINE config 3/4 (ConnectivityIMPCCBF); fov: config 5 "
+                         "(FovBezierIMPCCBF, horizon 20, 4 Bezier pieces)")
+    ap.add_argument("--agents-per-gpu", type=int, default=0,
+                    help="default 4096 (collision), 512 (fov: config 5 = 4096 agents on 8 GPUs)")
     ap.add_argument("--agents-total", type=int, default=0, help="strong scaling: fixed total")
-    ap.add_argument("--k-hor", type=int, default=15)
+    ap.add_argument("--k-hor", type=int, default=0, help="default 15 (collision), 20 (fov)")
     ap.add_argument("--knn", type=int, default=8)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--cpu-baseline-agents", type=int, default=-1,
@@ -90,13 +94,24 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
+    fov = args.workload == "fov"
+    if args.agents_per_gpu <= 0:
+        args.agents_per_gpu = 512 if fov else 4096
+    if args.k_hor <= 0:
+        args.k_hor = 20 if fov else 15
     total = args.agents_total if args.agents_total > 0 else args.agents_per_gpu * world
     per = total // world
     assert per * world == total, "agents must divide evenly over ranks"
     first = rank * per
-    cfg = swarm.config(args.k_hor)
-    radius = 3.0 * cfg["d_min"]
-    states_h, targets_h = swarm.lattice_swarm(total)
+    if fov:
+        cfg = swarm.fov_config(args.k_hor)
+        radius = cfg["fov_Rs"]  # observed neighbours: inside the FoV cone and the sensing range
+        states_h, targets_h = swarm.heading_swarm(total)
+        states_h[:, :2] *= 0.7  # 3.5 m lattice: 2-4 observed neighbours per agent
+    else:
+        cfg = swarm.config(args.k_hor)
+        radius = 3.0 * cfg["d_min"]
+        states_h, targets_h = swarm.lattice_swarm(total)
     ctx = Context(cfg, device=local)
     ctx.set_variant(args.variant)
 
@@ -232,10 +247,14 @@ def main():
             "dtype": "f64",
             "data": "synthetic (jittered-lattice swarm, seed 20251015)",
             "config": {
-                "workload": (f"config3: {total} agents, horizon {cfg['k_hor']}, pairwise collision "
-                             f"CBF, knn{args.knn} r={radius:g}m ({args.neighbours}), base_config.json; 2 IMPC QPs/agent/step"
-                             if world == 1 else
-                             f"{total} agents ({per}/GPU), horizon {cfg['k_hor']}, RCCL all-gather of states"),
+                "workload": (
+                    (f"config5: {total} agents ({per}/GPU), FoV 120 deg + Voronoi CBF, horizon "
+                     f"{cfg['k_hor']}, 4 Bezier pieces, {args.knn} nearest observed within {radius:g} m"
+                     if fov else
+                     f"config3: {total} agents, horizon {cfg['k_hor']}, pairwise collision CBF, "
+                     f"knn{args.knn} r={radius:g}m ({args.neighbours})")
+                    + ", base_config.json; 2 IMPC QPs/agent/step"
+                    + ("" if world == 1 else f"; {per}/GPU, RCCL all-gather of states")),
                 "agents_total": total,
                 "agents_per_gpu": per,
                 "k_hor": cfg["k_hor"],
@@ -258,13 +277,13 @@ def main():
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args)
+            res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args, radius)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def cpu_baseline(cfg, states_h, targets_h, args):
+def cpu_baseline(cfg, states_h, targets_h, args, radius):
     """The oracle (CPU restatement of the reference assembly + dense QP solve, standing in for
     CPLEX which cannot run here) on a bounded sample of the same workload, 1 thread (CPLEX
     Threads=1, CPLEX.cpp:158)."""
@@ -273,7 +292,10 @@ def cpu_baseline(cfg, states_h, targets_h, args):
     from mpccbf import swarm
     p = O.make_params(cfg)
     refs = swarm.refs_from_targets(targets_h, cfg["k_hor"])
-    rp, col = swarm.knn_csr(states_h, args.knn, 3.0 * cfg["d_min"])
+    if cfg.get("cbf_mode", 0) == 1:
+        rp, col = swarm.fov_csr(states_h, args.knn, radius, cfg["fov_beta"])
+    else:
+        rp, col = swarm.knn_csr(states_h, args.knn, radius)
     n = len(states_h)
     count = args.cpu_baseline_agents if args.cpu_baseline_agents > 0 else None
     if count is None:

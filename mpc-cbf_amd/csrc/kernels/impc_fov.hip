@@ -80,22 +80,32 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     const int ai = blockIdx.x;
     if (ai >= args.num_agents) return;
     stamp(args, ai, lane, 0);
-    __shared__ double Gimg[WROWS * WNZ];
+    const double* zero_row = nullptr;
+    double kconst;
+    __shared__ double Gimg[(WROWS + 1) * WNZ];  // + one all-zero row for unused slots
     __shared__ double rlo[WROWS], rhi[WROWS], rml[WROWS];
     __shared__ WaveScratch sc;
     __shared__ NbScratch nb_scratch;
-    __shared__ int32_t row_count;
 
     const int self = args.agent_first + ai;
     double s0[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) s0[k] = args.states[(size_t)self * 6 + k];
-    double q15[NZ], kconst;
-    agent_linear_term<NZ>(op, buf, args, ai, s0, q15, kconst);
-    double q[WNZ];
+    __shared__ double ykeep_s[WNZ], q_s[WNZ];  // wave-uniform vectors kept out of the registers
+    {
+        double q15[NZ], kconst0;
+        agent_linear_term<NZ>(op, buf, args, ai, s0, q15, kconst0);
+        if (lane == 0) {
 #pragma unroll
-    for (int j = 0; j < NZ; j++) q[j] = q15[j];
-    q[WNZ - 1] = 0.0;
+            for (int j = 0; j < NZ; j++) {
+                q_s[j] = q15[j];
+                ykeep_s[j] = 0.0;
+            }
+            q_s[WNZ - 1] = 0.0;
+            ykeep_s[WNZ - 1] = 0.0;
+        }
+        kconst = kconst0;
+    }
 
     // ---- shared box rows into the image (rows 0 .. mb-1), bounds shifted by Gs s0
     const int mb = op.m;
@@ -113,6 +123,8 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             rml[r] = 1.0;
         }
     }
+    if (lane < WNZ) Gimg[WROWS * WNZ + lane] = 0.0;
+    zero_row = &Gimg[WROWS * WNZ];
     const bool infeasible = constant_rows_infeasible<64>(op, buf, s0, lane);
     stamp(args, ai, lane, 1);
 
@@ -128,11 +140,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     if (nb_overflow) nnb = 0;
     stamp(args, ai, lane, 2);
 
-    double y[WNZ], ykeep[NZ];
-#pragma unroll
-    for (int j = 0; j < WNZ; j++) y[j] = 0.0;
-#pragma unroll
-    for (int j = 0; j < NZ; j++) ykeep[j] = 0.0;
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
     const int C = op.C;
@@ -188,8 +195,10 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 const int i = task / (4 * nk), kind = (task / nk) % 4;
                 k = task % nk;
                 const int nbi = grid_mode ? nb_scratch.idx[i] : args.nb_col[nb0 + i];
-                double e[6];
-                cbf_ego_state<NZ>(op, buf, it, k, s0, ykeep, e);
+                double e[6], yk[NZ];
+#pragma unroll
+                for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
+                cbf_ego_state<NZ>(op, buf, it, k, s0, yk, e);
                 bool present;
                 fov_cbf_row(kind, e, args.states[(size_t)nbi * 6], args.states[(size_t)nbi * 6 + 1],
                             op.fov_beta, op.fov_Ds, op.fov_Rs, a, bb, present);
@@ -228,11 +237,12 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         }
         row_infeasible = __ballot(row_infeasible) != 0ull;
         const int mtot = base + count;
-        const int nchunk = (mtot + 3) / 4;
+        const int nchunk = ((mtot + 15) / 16) * 4;  // whole groups of 4 chunks (WCH = 48 is one)
         // zero the image rows that complete the last chunk
         for (int r = mtot + lane; r < 4 * nchunk && r < WROWS; r += 64)
 #pragma unroll
             for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = 0.0;
+        if (lane < WNZ) sc.q[lane] = q_s[lane];
         wave_lds_sync();
         if (it < 2) stamp(args, ai, lane, 3 + 2 * it);
         int st;
@@ -247,14 +257,20 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             for (int s = 0; s < WR; s++) {
                 const int r = wave_owner_row(lane, s);
                 const bool on = r < mtot;
-#pragma unroll
-                for (int j = 0; j < WNZ; j++) rw.g[s][j] = on ? Gimg[r * WNZ + j] : 0.0;
+                rw.g[s] = on ? &Gimg[r * WNZ] : zero_row;
                 rw.lo[s] = on ? rlo[r] : -1.0;
                 rw.hi[s] = on ? rhi[r] : 1.0;
                 rw.ml[s] = on ? rml[r] : 1.0;
             }
+#ifdef MPCCBF_PDIP_STAMPS
+            long long* dbg = (args.stamps && it == 0)
+                                 ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 16
+                                 : nullptr;
+#else
+            long long* dbg = nullptr;
+#endif
             const PdipOut po = pdip_solve_wave(rw, Gimg, nchunk, sc, opp(buf, op.o_P16), opp(buf, op.o_LP16),
-                                               q, y, cfg, lane);
+                                               cfg, lane, dbg);
             st = po.status;
             nit = po.iters;
             if (st != ST_OPTIMAL) {
@@ -264,9 +280,15 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         }
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {
+            double yk[NZ], q15[NZ];
 #pragma unroll
-            for (int j = 0; j < NZ; j++) ykeep[j] = y[j];
-            objv = reduced_objective<NZ>(op, buf, q15, ykeep, kconst);
+            for (int j = 0; j < NZ; j++) {
+                yk[j] = sc.y[j];
+                q15[j] = q_s[j];
+            }
+            objv = reduced_objective<NZ>(op, buf, q15, yk, kconst);
+            wave_lds_sync();
+            if (lane < NZ) ykeep_s[lane] = sc.y[lane];
             have_curve = true;
         } else {
             success = false;
@@ -275,7 +297,12 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         if (it < 2) stamp(args, ai, lane, 4 + 2 * it);
         wave_lds_sync();
     }
-    write_agent_outputs<NZ, 64>(op, buf, args, ai, lane, s0, ykeep, have_curve);
+    {
+        double yk[NZ];
+#pragma unroll
+        for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
+        write_agent_outputs<NZ, 64>(op, buf, args, ai, lane, s0, yk, have_curve);
+    }
     stamp(args, ai, lane, 7);
 }
 

@@ -18,18 +18,6 @@
 
 #include "pdip.hpp"
 
-// Profiling build only (make prof): cycle stamps at the phase boundaries of Newton step 2.
-#ifdef MPCCBF_PDIP_STAMPS
-#define PSTAMP(k)                                                             \
-    do {                                                                      \
-        if (dbg && it == 2) dbg[k] = (long long)__builtin_amdgcn_s_memtime(); \
-    } while (0)
-#else
-#define PSTAMP(k) \
-    do {          \
-    } while (0)
-#endif
-
 namespace mpccbf {
 namespace dev {
 

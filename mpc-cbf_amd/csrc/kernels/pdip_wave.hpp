@@ -5,18 +5,22 @@
 // channels), where a per-lane packed normal matrix (120 entries) would not fit the registers.
 //
 // Layouts (64 lanes, lane = 16 q + p):
-//   rows   row r lives in slot s = r / 64 of lane 16 (r % 4) + (r / 4) % 16 ("owner"); the owner
-//          keeps the row's 16 coefficients, bounds, slacks and duals in registers.
-//   G      all rows, 16 doubles each, in the wave's LDS image; chunk c (rows 4c .. 4c+3) feeds one
-//          v_mfma_f64_16x16x4f64 with A = G_chunk^T (lane: G[4c + q][p]) and
-//          B = diag(D) G_chunk (lane: D_{4c+q} G[4c + q][p]); D_{4c+q} reaches lane (q, p) from
-//          its owner (q, c % 16) by a DPP row broadcast. Column 15 of B carries the right-hand
-//          side weights instead (the padded 16th variable has G[.][15] = 0), so one MFMA chain
-//          yields M = G^T D G and G^T w.
-//   rows-of-M  the 16x16 result is transposed through LDS so that lane i (of every 16-lane
-//          row) holds row i of M; Cholesky (left-looking, DPP broadcasts of row j) and both
-//          triangular solves run on that layout, and every solve ends with the solution in
-//          every lane.
+//   rows    row r lives in slot s = r / 64 of lane 16 (r % 4) + (r / 4) % 16 ("owner"); the owner
+//           keeps the row's bounds, slacks and duals in registers and reads its 16 coefficients
+//           from the wave's LDS row image (G, 16 doubles per row, padded column 15 = 0).
+//   vectors of the reduced dimension (iterate, directions, right-hand sides) live on the row
+//           layout: lane i (of every 16-lane row) holds element i — one register per vector.
+//           Where a row needs a whole vector (row activities g.y) it is published to LDS and
+//           read back as a wave-uniform broadcast.
+//   G^T v   lane (q, p) accumulates G[4c + q][p] v[4c + q] over the chunks c, then two
+//           permlane swaps sum the four q-groups: the product arrives on the row layout.
+//   Gram    chunk c (rows 4c .. 4c+3) feeds one v_mfma_f64_16x16x4f64 with A = G_chunk^T
+//           (lane: G[4c + q][p]) and B = diag(D) G_chunk (lane: D_{4c+q} G[4c + q][p]); column
+//           15 of B carries the right-hand side weights instead (G[.][15] = 0), so one MFMA chain
+//           yields M = G^T D G and G^T w. Per-row weights reach the chunk lanes through LDS.
+//   rows-of-M  the 16x16 result is transposed through LDS so that lane i holds row i of M;
+//           Cholesky (left-looking, DPP broadcasts of row j) and both triangular solves run on
+//           that layout (L's columns for the backward solve are read from LDS).
 // Phase 1 (feasibility) reuses the machinery with the padded variable as the violation t.
 #pragma once
 
@@ -37,6 +41,7 @@ typedef double wd4 __attribute__((ext_vector_type(4)));
 __host__ __device__ constexpr int wave_row_owner(int r) { return 16 * (r & 3) + ((r >> 2) & 15); }
 __host__ __device__ constexpr int wave_owner_row(int lane, int slot) { return 64 * slot + 4 * (lane & 15) + (lane >> 4); }
 
+// ---- 64-lane collectives -------------------------------------------------------------------
 // ---- 64-lane collectives -------------------------------------------------------------------
 template <int SRC>
 __device__ __forceinline__ double bcast16(double v) {  // row_newbcast:SRC (inside each 16-lane row)
@@ -94,44 +99,108 @@ __device__ __forceinline__ double wave_reduce(double v) {
     return xrow32<OP>(v);
 }
 
-// all-reduce (sum) of a 16-vector over the wave, stage-major
-__device__ __forceinline__ void wave_sum16(double (&v)[WNZ]) {
-    grp_sum_vec<16, WNZ>(v);
-#pragma unroll
-    for (int i = 0; i < WNZ; i++) v[i] = xrow16<Op::Sum>(v[i]);
-#pragma unroll
-    for (int i = 0; i < WNZ; i++) v[i] = xrow32<Op::Sum>(v[i]);
+
+// two independent all-reductions, stage-interleaved
+template <Op OA, Op OB>
+__device__ __forceinline__ void wave_reduce2(double& a, double& b) {
+    a = combine<OA>(a, dpp_mov<DPP_XOR1>(a));
+    b = combine<OB>(b, dpp_mov<DPP_XOR1>(b));
+    a = combine<OA>(a, dpp_mov<DPP_XOR2>(a));
+    b = combine<OB>(b, dpp_mov<DPP_XOR2>(b));
+    a = combine<OA>(a, dpp_mov<DPP_HALF_MIRROR>(a));
+    b = combine<OB>(b, dpp_mov<DPP_HALF_MIRROR>(b));
+    a = combine<OA>(a, dpp_mov<DPP_MIRROR>(a));
+    b = combine<OB>(b, dpp_mov<DPP_MIRROR>(b));
+    a = xrow16<OA>(a);
+    b = xrow16<OB>(b);
+    a = xrow32<OA>(a);
+    b = xrow32<OB>(b);
 }
 
-// element (lane & 15) of a wave-uniform 16-vector
-__device__ __forceinline__ double lane_pick16(const double (&u)[WNZ], int i) {
-    double v = u[0];
+// ---- LDS workspace -------------------------------------------------------------------------
+struct WaveScratch {      // per-wave LDS besides the row image
+    double M[WNZ * WNZ];  // Gram transpose, then L (row-major) for the backward solves
+    double Dv[WROWS];     // per-row Newton weight
+    double wv[WROWS];     // per-row right-hand side weight (Gram column 15)
+    double cv[WROWS];     // per-row weights of a G^T v product
+    double y[WNZ];        // iterate, wave-uniform copy (caller: result of pdip_solve_wave)
+    double d[WNZ];        // current direction, wave-uniform copy
+    double q[WNZ];        // linear term (caller fills; q[15] = 0)
+};
+
+// Row storage of one lane (owner layout). Every row has an upper side; ml = 1 adds the lower.
+// Unused slots hold inert rows (g = 0, -1 <= 0 <= 1). g[s] points at the slot's row in the LDS
+// image (an all-zero row for unused slots).
+struct WaveRows {
+    const double* g[WR];
+    double lo[WR], hi[WR], ml[WR];
+};
+
+// a . b over 16 entries, both in LDS (b wave-uniform: broadcast reads)
+__device__ __forceinline__ double dotl(const double* a, const double* b) {
+    double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-    for (int k = 1; k < WNZ; k++) v = (i == k) ? u[k] : v;
-    return v;
+    for (int j = 0; j < WNZ; j += 2) {
+        s0 = fma(a[j], b[j], s0);
+        s1 = fma(a[j + 1], b[j + 1], s1);
+    }
+    return s0 + s1;
 }
 
-// ---- Gram matrix on the matrix cores -------------------------------------------------------
-// acc = G^T diag(D) G with column 15 replaced by G^T w (rows beyond nchunk*4 skipped).
-// Gs: the wave's LDS row image (WROWS x 16); D, w: per owned slot.
-__device__ __forceinline__ wd4 wave_gram(const double* __restrict__ Gs, int nchunk, const double (&D)[WR],
-                                         const double (&w)[WR], int lane) {
+__device__ __forceinline__ double dotr(const double (&a)[WNZ], const double* b) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < WNZ; j += 2) {
+        s0 = fma(a[j], b[j], s0);
+        s1 = fma(a[j + 1], b[j + 1], s1);
+    }
+    return s0 + s1;
+}
+
+// (G^T v)_i on the row layout; v: one weight per image row (LDS). nchunk is a multiple of 4
+// (the caller zeroes the image rows that complete the last group of chunks). Fully unrolled
+// over the 12 groups with wave-uniform guards: a runtime loop would carry the accumulators
+// through copies.
+__device__ __forceinline__ double wave_gt(const double* __restrict__ Gs, const double* __restrict__ v,
+                                          int nchunk, int lane) {
     const int q = lane >> 4, p = lane & 15;
-    wd4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int c = 0; c < WCH; c++) {
-        if (c < nchunk) {  // wave-uniform
-            const double g = Gs[(4 * c + q) * WNZ + p];
-            const double Dq = bcast16v(c, D[c >> 4]);
-            const double wq = bcast16v(c, w[c >> 4]);
-            const double b = (p == WNZ - 1) ? wq : Dq * g;
-            if (c & 1)
-                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(g, b, acc1, 0, 0, 0);
-            else
-                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(g, b, acc0, 0, 0, 0);
+    for (int c = 0; c < WCH; c += 4) {
+        if (c < nchunk) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int r = 4 * (c + u) + q;
+                a[u] = fma(Gs[r * WNZ + p], v[r], a[u]);
+            }
         }
     }
-    return acc0 + acc1;
+    return xrow32<Op::Sum>(xrow16<Op::Sum>((a[0] + a[1]) + (a[2] + a[3])));
+}
+
+// acc = G^T diag(D) G with column 15 replaced by G^T w. nchunk: a multiple of 4.
+__device__ __forceinline__ wd4 wave_gram(const double* __restrict__ Gs, const double* __restrict__ Dv,
+                                         const double* __restrict__ wv, int nchunk, int lane) {
+    const int q = lane >> 4, p = lane & 15;
+    const double rhs_col = (p == WNZ - 1) ? 1.0 : 0.0;  // G[.][15] = 0: column 15 takes w only
+    wd4 acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc[u] = wd4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < WCH; c += 4) {
+        if (c < nchunk) {
+            double g[4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int r = 4 * (c + u) + q;
+                g[u] = Gs[r * WNZ + p];
+                b[u] = fma(rhs_col, wv[r], Dv[r] * g[u]);  // branch-free
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(g[u], b[u], acc[u], 0, 0, 0);
+        }
+    }
+    return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 // Transpose the MFMA result (lane (q, p): M[q + 4i][p]) into rows: lane -> row (lane & 15).
@@ -148,104 +217,84 @@ __device__ __forceinline__ void gram_rows(const wd4 acc, double* __restrict__ Mb
 }
 
 // Left-looking Cholesky on the row layout: lane i holds row i of M (k <= i used) and gets row i
-// of L; inv[j] = 1 / L_jj (wave-uniform). Returns false if a pivot is not positive.
-__device__ __forceinline__ bool chol_rows(const double (&M)[WNZ], double (&L)[WNZ], double (&inv)[WNZ], int i) {
+// of L and inv_i = 1 / L_ii; L's rows are then stored to Mbuf (row-major) for the backward
+// solves. Returns false if a pivot is not positive.
+__device__ __forceinline__ bool chol_rows(const double (&M)[WNZ], double (&L)[WNZ], double& inv_i,
+                                          double* __restrict__ Mbuf, int lane) {
+    const int i = lane & 15;
     bool ok = true;
+    inv_i = 0.0;
 #pragma unroll
     for (int j = 0; j < WNZ; j++) {
-        double v = M[j];
+        double part[4] = {M[j], 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < j; k++) v = fma(-L[k], bcast16v(j, L[k]), v);
+        for (int k = 0; k < j; k++) part[k & 3] = fma(-L[k], bcast16v(j, L[k]), part[k & 3]);
+        const double v = (part[0] + part[1]) + (part[2] + part[3]);
         const double d = bcast16v(j, v);
         ok = ok && (d > 0.0);
         const double r = rsqrt(d > 0.0 ? d : 1e-300);
-        inv[j] = r;
+        inv_i = (i == j) ? r : inv_i;
         L[j] = (i >= j) ? v * r : 0.0;
     }
-    return ok;
-}
-
-// Column layout of L through LDS: lane i gets Lc[k] = L[k][i].
-__device__ __forceinline__ void chol_cols(const double (&L)[WNZ], double* __restrict__ Mbuf, int lane,
-                                          double (&Lc)[WNZ]) {
-    const int i = lane & 15;
-    if (lane < 16) {
+    if (lane < WNZ) {
 #pragma unroll
         for (int k = 0; k < WNZ; k++) Mbuf[i * WNZ + k] = L[k];
     }
     wave_lds_sync();
-#pragma unroll
-    for (int k = 0; k < WNZ; k++) Lc[k] = Mbuf[k * WNZ + i];
-    wave_lds_sync();
+    return ok;
 }
 
-// Solve L L^T x = b, b given on the row layout (lane i: b_i); x returned wave-uniform.
-__device__ __forceinline__ void solve_rows(const double (&L)[WNZ], const double (&Lc)[WNZ],
-                                           const double (&inv)[WNZ], double b, int i, double (&x)[WNZ]) {
+// Solve L L^T x = b on the row layout (lane i: b_i in, x_i out). L: row i of L (registers),
+// Lm: L row-major (LDS, or global for the start factor), inv_i = 1 / L_ii.
+__device__ __forceinline__ double solve_rows(const double (&L)[WNZ], const double* __restrict__ Lm,
+                                             double inv_i, double b, int i) {
     double res = b, wl = 0.0;
 #pragma unroll
     for (int k = 0; k < WNZ; k++) {
-        const double wk = bcast16v(k, res) * inv[k];
+        const double wk = bcast16v(k, res * inv_i);
         res = fma(-L[k], wk, res);
         wl = (i == k) ? wk : wl;
     }
     res = wl;
+    double xl = 0.0;
 #pragma unroll
     for (int k = WNZ - 1; k >= 0; k--) {
-        const double xk = bcast16v(k, res) * inv[k];
-        res = fma(-Lc[k], xk, res);
-        x[k] = xk;
+        const double xk = bcast16v(k, res * inv_i);
+        res = fma(-Lm[k * WNZ + i], xk, res);
+        xl = (i == k) ? xk : xl;
     }
+    return xl;
 }
 
-// Row storage of one lane (owner layout). Every row has an upper side; ml = 1 adds the lower.
-// Unused slots hold inert rows (g = 0, -1 <= 0 <= 1).
-struct WaveRows {
-    double g[WR][WNZ];
-    double lo[WR], hi[WR], ml[WR];
-};
-
-__device__ __forceinline__ double dot16(const double (&a)[WNZ], const double (&b)[WNZ]) {
-    double s = 0.0;
-#pragma unroll
-    for (int j = 0; j < WNZ; j++) s = fma(a[j], b[j], s);
-    return s;
+// publish a row-layout vector as a wave-uniform LDS copy
+__device__ __forceinline__ void publish16(double* __restrict__ dst, double v, int lane) {
+    if (lane < WNZ) dst[lane] = v;
+    wave_lds_sync();
 }
 
-struct WaveScratch {     // per-wave LDS besides the row image
-    double M[WNZ * WNZ];
-};
-
-// Main solve. P, LP: 16x16 row-major, padded with the identity (uniform, global). q, y uniform.
-// nz: true reduced dimension (<= 15; the 16th variable is padding). nchunk: row chunks in use.
+// Main solve. P, LP: 16x16 row-major, padded with the identity (uniform, global). sc.q: linear
+// term; on return sc.y holds the iterate. nchunk: row chunks in use.
 __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
                                    WaveScratch& sc, const double* __restrict__ P,
-                                   const double* __restrict__ LP, const double (&q)[WNZ],
-                                   double (&y)[WNZ], const PdipCfg cfg, int lane) {
+                                   const double* __restrict__ LP, const PdipCfg cfg, int lane,
+                                   long long* dbg = nullptr) {
+    (void)dbg;
     const int i = lane & 15;
-    // ---- start: y0 = -P^{-1} q (uniform triangular solves with LP)
+    const double qi = sc.q[i];
+    double L[WNZ], inv_i;
+    // ---- start: y0 = -P^{-1} q with the factor of P
     {
-        double w[WNZ];
 #pragma unroll
-        for (int r = 0; r < WNZ; r++) {
-            double v = -q[r];
-#pragma unroll
-            for (int k = 0; k < r; k++) v = fma(-LP[r * WNZ + k], w[k], v);
-            w[r] = v * rcp(LP[r * WNZ + r]);
-        }
-#pragma unroll
-        for (int r = WNZ - 1; r >= 0; r--) {
-            double v = w[r];
-#pragma unroll
-            for (int k = r + 1; k < WNZ; k++) v = fma(-LP[k * WNZ + r], y[k], v);
-            y[r] = v * rcp(LP[r * WNZ + r]);
-        }
+        for (int k = 0; k < WNZ; k++) L[k] = (k <= i) ? LP[i * WNZ + k] : 0.0;
+        inv_i = rcp(LP[i * WNZ + i]);
     }
+    double yi = solve_rows(L, LP, inv_i, -qi, i);
+    publish16(sc.y, yi, lane);
     double sl[WR], su[WR], zl[WR], zu[WR], pl[WR], pu[WR];
     double nloc = 0.0;
 #pragma unroll
     for (int s = 0; s < WR; s++) {
-        const double t = dot16(rw.g[s], y);
+        const double t = dotl(rw.g[s], sc.y);
         sl[s] = rw.ml[s] > 0.0 ? fmax(t - rw.lo[s], 1.0) : 1.0;
         su[s] = fmax(rw.hi[s] - t, 1.0);
         zl[s] = rw.ml[s] * rcp(sl[s]);
@@ -255,73 +304,59 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         nloc += rw.ml[s] + 1.0;
     }
     const double inv_ns = rcp(wave_reduce<Op::Sum>(nloc));
-    double qn = 0.0;
-#pragma unroll
-    for (int j = 0; j < WNZ; j++) qn = fmax(qn, fabs(q[j]));
-    const double inv_qn = rcp(1.0 + qn);
-    // P row i (row layout) for P y
-    double Prow[WNZ];
+    const double inv_qn = rcp(1.0 + grp_max<16>(fabs(qi)));
+    double Prow[WNZ];  // row i of P
 #pragma unroll
     for (int k = 0; k < WNZ; k++) Prow[k] = P[i * WNZ + k];
-    const double qi = lane_pick16(q, i);
 
     PdipOut out{ST_UNKNOWN, 0};
     double mu0 = 1.0, rd_track = 1e300;
     bool rd_exact = true;
     for (int it = 0;; it++) {
-        double rl[WR], ru[WR], il[WR], iu[WR], D[WR], wv[WR];
+        PSTAMP(0);
+        double rl[WR], ru[WR], il[WR], iu[WR];
         double mloc = 0.0, rp = 0.0;
-        double dz[WNZ];
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) dz[j] = 0.0;
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            const double t = dot16(rw.g[s], y);
+            const double t = dotl(rw.g[s], sc.y);
             rl[s] = rw.ml[s] * (t - rw.lo[s] - sl[s]);
             ru[s] = rw.hi[s] - t - su[s];
             il[s] = rcp(sl[s]);
             iu[s] = rcp(su[s]);
             const double Dl = zl[s] * il[s], Du = zu[s] * iu[s];
-            D[s] = Dl + Du;
-            wv[s] = Du * ru[s] - Dl * rl[s];
+            const int r = wave_owner_row(lane, s);
+            sc.Dv[r] = Dl + Du;
+            sc.wv[r] = Du * ru[s] - Dl * rl[s];
+            sc.cv[r] = zu[s] - zl[s];
             mloc = fma(sl[s], zl[s], fma(su[s], zu[s], mloc));
             rp = fmax(rp, fmax(fabs(rl[s]) * pl[s], fabs(ru[s]) * pu[s]));
-            if (rd_exact) {
-#pragma unroll
-                for (int j = 0; j < WNZ; j++) dz[j] = fma(rw.g[s][j], zu[s] - zl[s], dz[j]);
-            }
         }
-        const wd4 acc = wave_gram(Gs, nchunk, D, wv, lane);
+        PSTAMP(1);
+        wave_lds_sync();
+        const wd4 acc = wave_gram(Gs, sc.Dv, sc.wv, nchunk, lane);
         double Mr[WNZ];
         gram_rows(acc, sc.M, lane, Mr);
         const double rhs_i = Mr[WNZ - 1];  // G^T w (column 15)
+        PSTAMP(2);
 #pragma unroll
         for (int k = 0; k < WNZ; k++) Mr[k] = (k == WNZ - 1 && i != WNZ - 1 ? 0.0 : Mr[k]) + Prow[k];
-        const double mu = wave_reduce<Op::Sum>(mloc) * inv_ns;
-        rp = wave_reduce<Op::Max>(rp);
-        const double py_i = dot16(Prow, y) + qi;  // (P y + q)_i
+        wave_reduce2<Op::Sum, Op::Max>(mloc, rp);
+        const double mu = mloc * inv_ns;
+        const double py_i = dotr(Prow, sc.y) + qi;  // (P y + q)_i
+        bool rd_fresh = false;
         if (rd_exact) {
-            wave_sum16(dz);
-            rd_track = grp_max<16>(fabs(py_i + lane_pick16(dz, i))) * inv_qn;
+            rd_track = grp_max<16>(fabs(py_i + wave_gt(Gs, sc.cv, nchunk, lane))) * inv_qn;
             rd_exact = false;
+            rd_fresh = true;
         }
         out.iters = it;
         const bool finite = isfinite(rp) && isfinite(rd_track) && isfinite(mu) && isfinite(Mr[0]);
-        if (finite && rp <= cfg.tol && mu <= cfg.tol * 0.1) {
+        if (finite && rp <= cfg.tol && mu <= cfg.tol * 0.1 && rd_track <= cfg.tol) {
+            if (!rd_fresh)  // the tracked dual residual is a prediction: confirm it exactly
+                rd_track = grp_max<16>(fabs(py_i + wave_gt(Gs, sc.cv, nchunk, lane))) * inv_qn;
             if (rd_track <= cfg.tol) {
-                double chk[WNZ];
-#pragma unroll
-                for (int j = 0; j < WNZ; j++) chk[j] = 0.0;
-#pragma unroll
-                for (int s = 0; s < WR; s++)
-#pragma unroll
-                    for (int j = 0; j < WNZ; j++) chk[j] = fma(rw.g[s][j], zu[s] - zl[s], chk[j]);
-                wave_sum16(chk);
-                rd_track = grp_max<16>(fabs(py_i + lane_pick16(chk, i))) * inv_qn;
-                if (rd_track <= cfg.tol) {
-                    out.status = ST_OPTIMAL;
-                    break;
-                }
+                out.status = ST_OPTIMAL;
+                break;
             }
         }
         if (it == 0) mu0 = mu;
@@ -329,21 +364,22 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             out.status = ST_UNKNOWN;
             break;
         }
+        PSTAMP(3);
         // ---- factor
-        double L[WNZ], Lc[WNZ], inv[WNZ];
-        if (!chol_rows(Mr, L, inv, i)) {
+        if (!chol_rows(Mr, L, inv_i, sc.M, lane)) {
             out.status = ST_UNKNOWN;
             break;
         }
-        chol_cols(L, sc.M, lane, Lc);
+        PSTAMP(4);
         // ---- predictor
-        double dya[WNZ];
-        solve_rows(L, Lc, inv, rhs_i - py_i, i, dya);
+        const double dya_i = solve_rows(L, sc.M, inv_i, rhs_i - py_i, i);
+        publish16(sc.d, dya_i, lane);
+        PSTAMP(5);
         double dsl[WR], dsu[WR], dzl[WR], dzu[WR];
         double rs = 0.0, rz = 0.0;
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            const double td = dot16(rw.g[s], dya);
+            const double td = dotl(rw.g[s], sc.d);
             dsl[s] = rw.ml[s] * (td + rl[s]);
             dsu[s] = ru[s] - td;
             const double ql = dsl[s] * il[s], qu = dsu[s] * iu[s];
@@ -352,8 +388,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             rs = fmax(rs, fmax(-ql, -qu));
             rz = fmax(rz, fmax(rw.ml[s] * (1.0 + ql), 1.0 + qu));
         }
-        rs = wave_reduce<Op::Max>(rs);
-        rz = wave_reduce<Op::Max>(rz);
+        wave_reduce2<Op::Max, Op::Max>(rs, rz);
         const double ap = rcp(fmax(1.0, rs)), ad = rcp(fmax(1.0, rz));
         double mua = 0.0;
 #pragma unroll
@@ -365,27 +400,25 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         double sig = mu > 0.0 ? mua * rcp(mu) : 0.0;
         sig = fmin(sig * sig * sig, 1.0);
         const double smu = sig * mu;
+        PSTAMP(6);
         // ---- corrector right-hand side G^T (kl/sl - ku/su)
-        double kl[WR], ku[WR], vc[WNZ];
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) vc[j] = 0.0;
+        double kl[WR], ku[WR];
 #pragma unroll
         for (int s = 0; s < WR; s++) {
             kl[s] = rw.ml[s] * (smu - dsl[s] * dzl[s]);
             ku[s] = smu - dsu[s] * dzu[s];
-            const double wgt = kl[s] * il[s] - ku[s] * iu[s];
-#pragma unroll
-            for (int j = 0; j < WNZ; j++) vc[j] = fma(rw.g[s][j], wgt, vc[j]);
+            sc.cv[wave_owner_row(lane, s)] = kl[s] * il[s] - ku[s] * iu[s];
         }
-        wave_sum16(vc);
-        double dyc[WNZ], dy[WNZ];
-        solve_rows(L, Lc, inv, lane_pick16(vc, i), i, dyc);
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) dy[j] = dya[j] + dyc[j];
+        wave_lds_sync();
+        const double vc_i = wave_gt(Gs, sc.cv, nchunk, lane);
+        PSTAMP(7);
+        const double dy_i = dya_i + solve_rows(L, sc.M, inv_i, vc_i, i);
+        publish16(sc.d, dy_i, lane);
+        PSTAMP(8);
         double rmax = 0.0;
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            const double td = dot16(rw.g[s], dy);
+            const double td = dotl(rw.g[s], sc.d);
             dsl[s] = rw.ml[s] * (td + rl[s]);
             dsu[s] = ru[s] - td;
             dzl[s] = (kl[s] - sl[s] * zl[s] - zl[s] * dsl[s]) * il[s];
@@ -396,8 +429,9 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         }
         rmax = wave_reduce<Op::Max>(rmax);
         const double alpha = 0.99 * rcp(fmax(0.99, rmax));
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) y[j] = fma(alpha, dy[j], y[j]);
+        PSTAMP(9);
+        yi = fma(alpha, dy_i, yi);
+        publish16(sc.y, yi, lane);
 #pragma unroll
         for (int s = 0; s < WR; s++) {
             sl[s] = fmax(fma(alpha, dsl[s], sl[s]), 1e-300);
@@ -405,7 +439,9 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             zl[s] = rw.ml[s] * fmax(fma(alpha, dzl[s], zl[s]), 1e-300);
             zu[s] = fmax(fma(alpha, dzu[s], zu[s]), 1e-300);
         }
+        PSTAMP(10);
         rd_track *= (1.0 - alpha);
+        PSTAMP(11);
         if (it % 8 == 7) rd_exact = true;
     }
     return out;
@@ -416,14 +452,14 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
 // (lower: (-g, -1) v <= -lo; upper: (g, -1) v <= hi), so the Newton matrix is
 //   [G^T (Dl + Du) G + eps I , G^T (Dl - Du) ; . , sum (Dl + Du) + Dt]
 // — the first block on the matrix cores (column 15 = G^T (Dl - Du)), the corner by a reduction.
-// The t >= 0 bound is one more side. Returns t* (>= 0), 1e300 on numerical failure.
+// The t >= 0 bound is one more side. Uses sc.y / sc.d / sc.M. Returns t* (>= 0), 1e300 on
+// numerical failure.
 __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
                                    WaveScratch& sc, int nz, const PdipCfg cfg, int lane) {
     constexpr double eps = 1e-10;
     const int i = lane & 15;
-    double y[WNZ];
-#pragma unroll
-    for (int j = 0; j < WNZ; j++) y[j] = 0.0;
+    double vi = 0.0;  // y_i (i < 15) on the row layout
+    publish16(sc.y, 0.0, lane);
     double viol = 0.0, nloc = 0.0;
 #pragma unroll
     for (int s = 0; s < WR; s++) {
@@ -442,35 +478,33 @@ __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict_
     }
     double zt = rcp(t);
     for (int it = 0; it < 2 * cfg.maxit; it++) {
-        double rsl[WR], rsu[WR], il[WR], iu[WR], Dl[WR], Du[WR], Ds[WR], Dd[WR];
+        double rsl[WR], rsu[WR], il[WR], iu[WR], Dl[WR], Du[WR];
         double rp = 0.0, mloc = 0.0, dsum = 0.0, tcorner = 0.0;
-        double rhs[WNZ];
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) rhs[j] = 0.0;
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            const double gy = dot16(rw.g[s], y);
+            const double gy = dotl(rw.g[s], sc.y);
             rsl[s] = rw.ml[s] * (gy + t - rw.lo[s] - sl[s]);
             rsu[s] = rw.hi[s] - gy + t - su[s];
             il[s] = rcp(sl[s]);
             iu[s] = rcp(su[s]);
             Dl[s] = zl[s] * il[s];
             Du[s] = zu[s] * iu[s];
-            Ds[s] = Dl[s] + Du[s];
-            Dd[s] = Dl[s] - Du[s];
             const double wl = -Dl[s] * rsl[s], wu = -Du[s] * rsu[s];
-#pragma unroll
-            for (int j = 0; j < WNZ; j++) rhs[j] = fma(rw.g[s][j], wl - wu, rhs[j]);
+            const int r = wave_owner_row(lane, s);
+            sc.Dv[r] = Dl[s] + Du[s];
+            sc.wv[r] = Dl[s] - Du[s];
+            sc.cv[r] = wl - wu;
             tcorner += wl + wu;
-            dsum += Ds[s];
+            dsum += Dl[s] + Du[s];
             mloc = fma(sl[s], zl[s], fma(su[s], zu[s], mloc));
             rp = fmax(rp, fmax(fabs(rsl[s]) * rw.ml[s] * rcp(1.0 + fabs(rw.lo[s])),
                                fabs(rsu[s]) * rcp(1.0 + fabs(rw.hi[s]))));
         }
-        const wd4 acc = wave_gram(Gs, nchunk, Ds, Dd, lane);
+        wave_lds_sync();
+        const wd4 acc = wave_gram(Gs, sc.Dv, sc.wv, nchunk, lane);
         double Mr[WNZ];
         gram_rows(acc, sc.M, lane, Mr);  // column 15 = G^T (Dl - Du)
-        wave_sum16(rhs);
+        const double rhs_i = wave_gt(Gs, sc.cv, nchunk, lane);
         tcorner = wave_reduce<Op::Sum>(tcorner);
         dsum = wave_reduce<Op::Sum>(dsum);
         rp = wave_reduce<Op::Max>(rp);
@@ -485,13 +519,10 @@ __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict_
 #pragma unroll
         for (int k = 0; k < WNZ - 1; k++) row[k] = (i < WNZ - 1) ? Mr[k] + (i == k ? eps : 0.0) : 0.0;
         row[WNZ - 1] = (i < WNZ - 1) ? c15 : dsum + Dt;
-        // the t-row (lane 15) needs the column 15 entries of the other rows: gather them
-        double col15[WNZ];
 #pragma unroll
-        for (int k = 0; k < WNZ; k++) col15[k] = bcast16v(k, c15);
-        if (i == WNZ - 1) {
-#pragma unroll
-            for (int k = 0; k < WNZ - 1; k++) row[k] = col15[k];
+        for (int k = 0; k < WNZ - 1; k++) {  // the t-row (lane 15) takes column 15 of the others
+            const double ck = bcast16v(k, c15);
+            row[k] = (i == WNZ - 1) ? ck : row[k];
         }
 #pragma unroll
         for (int k = 0; k < WNZ - 1; k++)  // padding variables: identity rows / columns
@@ -500,28 +531,26 @@ __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict_
 #pragma unroll
             for (int k = 0; k < WNZ; k++) row[k] = (k == i) ? 1.0 : 0.0;
         }
-        double L[WNZ], Lc[WNZ], inv[WNZ];
-        if (!chol_rows(row, L, inv, i)) return 1e300;
-        chol_cols(L, sc.M, lane, Lc);
+        double L[WNZ], inv_i;
+        if (!chol_rows(row, L, inv_i, sc.M, lane)) return 1e300;
         // rhs: y part -eps y + G^T(wl - wu); t part -1 + sum(wl + wu)
-        double b_i = (i < WNZ - 1) ? fma(-eps, lane_pick16(y, i), lane_pick16(rhs, i)) : -1.0 + tcorner;
+        double b_i = (i < WNZ - 1) ? fma(-eps, vi, rhs_i) : -1.0 + tcorner;
         if (i >= nz && i < WNZ - 1) b_i = 0.0;
-        double dv[WNZ];
-        solve_rows(L, Lc, inv, b_i, i, dv);
+        double dv_i = solve_rows(L, sc.M, inv_i, b_i, i);
+        publish16(sc.d, dv_i, lane);
+        const double dsta = sc.d[WNZ - 1];
         double ap = 1.0, ad = 1.0, dsla[WR], dzla[WR], dsua[WR], dzua[WR];
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            double dgy = 0.0;
-#pragma unroll
-            for (int j = 0; j < WNZ - 1; j++) dgy = fma(rw.g[s][j], dv[j], dgy);
-            dsla[s] = rw.ml[s] * (dgy + dv[WNZ - 1] + rsl[s]);
-            dsua[s] = -dgy + dv[WNZ - 1] + rsu[s];
+            const double dgy = dotl(rw.g[s], sc.d);  // g[15] = 0: the y part only
+            dsla[s] = rw.ml[s] * (dgy + dsta + rsl[s]);
+            dsua[s] = -dgy + dsta + rsu[s];
             dzla[s] = -zl[s] - Dl[s] * dsla[s];
             dzua[s] = -zu[s] - Du[s] * dsua[s];
             ap = fmin(ap, fmin(step_bound(sl[s], dsla[s], 1.0), step_bound(su[s], dsua[s], 1.0)));
             ad = fmin(ad, fmin(step_bound(zl[s], dzla[s], 1.0), step_bound(zu[s], dzua[s], 1.0)));
         }
-        const double dsta = dv[WNZ - 1], dzta = -zt - Dt * dsta;
+        const double dzta = -zt - Dt * dsta;
         ap = fmin(wave_reduce<Op::Min>(ap), step_bound(t, dsta, 1.0));
         ad = fmin(wave_reduce<Op::Min>(ad), step_bound(zt, dzta, 1.0));
         double mua = 0.0;
@@ -534,46 +563,40 @@ __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict_
         double sig = mu > 0.0 ? mua * rcp(mu) : 0.0;
         sig = fmin(sig * sig * sig, 1.0);
         const double smu = sig * mu;
-        double vc[WNZ], vct = 0.0, cl[WR], cu[WR];
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) vc[j] = 0.0;
+        double vct = 0.0, cl[WR], cu[WR];
 #pragma unroll
         for (int s = 0; s < WR; s++) {
             cl[s] = rw.ml[s] * (smu - dsla[s] * dzla[s]);
             cu[s] = smu - dsua[s] * dzua[s];
             const double a = cl[s] * il[s], b = cu[s] * iu[s];
-#pragma unroll
-            for (int j = 0; j < WNZ; j++) vc[j] = fma(rw.g[s][j], a - b, vc[j]);
+            sc.cv[wave_owner_row(lane, s)] = a - b;
             vct += a + b;
         }
-        wave_sum16(vc);
+        wave_lds_sync();
+        const double vc_i = wave_gt(Gs, sc.cv, nchunk, lane);
         const double ct = smu - dsta * dzta;
         vct = wave_reduce<Op::Sum>(vct) + ct * rcp(t);
-        double bc_i = (i < WNZ - 1) ? lane_pick16(vc, i) : vct;
+        double bc_i = (i < WNZ - 1) ? vc_i : vct;
         if (i >= nz && i < WNZ - 1) bc_i = 0.0;
-        double dvc[WNZ];
-        solve_rows(L, Lc, inv, bc_i, i, dvc);
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) dv[j] += dvc[j];
+        dv_i += solve_rows(L, sc.M, inv_i, bc_i, i);
+        publish16(sc.d, dv_i, lane);
+        const double dst = sc.d[WNZ - 1];
         double amax = 1e300, dsl[WR], dzl[WR], dsu[WR], dzu[WR];
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            double dgy = 0.0;
-#pragma unroll
-            for (int j = 0; j < WNZ - 1; j++) dgy = fma(rw.g[s][j], dv[j], dgy);
-            dsl[s] = rw.ml[s] * (dgy + dv[WNZ - 1] + rsl[s]);
-            dsu[s] = -dgy + dv[WNZ - 1] + rsu[s];
+            const double dgy = dotl(rw.g[s], sc.d);
+            dsl[s] = rw.ml[s] * (dgy + dst + rsl[s]);
+            dsu[s] = -dgy + dst + rsu[s];
             dzl[s] = (cl[s] - sl[s] * zl[s] - zl[s] * dsl[s]) * il[s];
             dzu[s] = (cu[s] - su[s] * zu[s] - zu[s] * dsu[s]) * iu[s];
             amax = fmin(amax, fmin(step_bound(sl[s], dsl[s], 1e300), step_bound(su[s], dsu[s], 1e300)));
             amax = fmin(amax, fmin(step_bound(zl[s], rw.ml[s] * dzl[s], 1e300), step_bound(zu[s], dzu[s], 1e300)));
         }
-        const double dst = dv[WNZ - 1];
         const double dzt = (ct - t * zt - zt * dst) * rcp(t);
         amax = fmin(wave_reduce<Op::Min>(amax), fmin(step_bound(t, dst, 1e300), step_bound(zt, dzt, 1e300)));
         const double alpha = fmin(1.0, 0.99 * amax);
-#pragma unroll
-        for (int j = 0; j < WNZ - 1; j++) y[j] = fma(alpha, dv[j], y[j]);
+        if (i < WNZ - 1) vi = fma(alpha, dv_i, vi);
+        publish16(sc.y, vi, lane);
         t = fmax(fma(alpha, dst, t), 1e-300);
         zt = fmax(fma(alpha, dzt, zt), 1e-300);
 #pragma unroll
@@ -587,7 +610,7 @@ __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict_
     double worst = 0.0;
 #pragma unroll
     for (int s = 0; s < WR; s++) {
-        const double gy = dot16(rw.g[s], y);
+        const double gy = dotl(rw.g[s], sc.y);
         worst = fmax(worst, fmax(rw.ml[s] * (rw.lo[s] - gy), gy - rw.hi[s]));
     }
     return wave_reduce<Op::Max>(worst);

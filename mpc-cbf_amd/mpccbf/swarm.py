@@ -137,14 +137,22 @@ def fov_csr(states: np.ndarray, k: int, radius: float, fov: float):
     return row_ptr, col
 
 
-def heading_swarm(n_agents: int, d_min: float = 2.0, seed: int = SEED, v_range: float = 0.5,
-                  target_radius: float = 3.0):
-    """lattice_swarm with every agent's yaw drawn uniformly (the FoV controller observes the
-    neighbours inside its heading cone)."""
-    states, targets = lattice_swarm(n_agents, d_min, seed, v_range, target_radius)
+def heading_swarm(n_agents: int, d_min: float = 2.0, seed: int = SEED, speed: float = 0.3,
+                  target_dist: float = 3.0):
+    """Swarm for the FoV controller: lattice positions as lattice_swarm, every agent with a random
+    heading, moving along it at `speed`, with its target ahead (within +-30 deg of the heading,
+    up to `target_dist`), so the robots it observes can stay in view while it travels."""
+    states, targets = lattice_swarm(n_agents, d_min, seed)
     rng = np.random.default_rng(seed + 1)
-    states[:, 2] = rng.uniform(-math.pi, math.pi, n_agents)
-    targets[:, 2] = states[:, 2]
+    yaw = rng.uniform(-math.pi, math.pi, n_agents)
+    states[:, 2] = yaw
+    states[:, 3] = speed * np.cos(yaw)
+    states[:, 4] = speed * np.sin(yaw)
+    ang = yaw + rng.uniform(-math.pi / 6, math.pi / 6, n_agents)
+    r = target_dist * np.sqrt(rng.uniform(0.25, 1.0, n_agents))
+    targets[:, 0] = states[:, 0] + r * np.cos(ang)
+    targets[:, 1] = states[:, 1] + r * np.sin(ang)
+    targets[:, 2] = yaw
     return states, targets
 
 

@@ -797,7 +797,16 @@ struct Solver {
         for (int e = 0; e < me; e++) rhs[n + e] = rhs_e[e];
         std::vector<double> b = rhs;
         lu.solve(b);
-        (void)M0;
+        for (int pass = 0; pass < 2; pass++) {  // iterative refinement against M0 (no ridge)
+            std::vector<double> r = rhs;
+            for (int i = 0; i < N; i++) {
+                double v = 0;
+                for (int j = 0; j < N; j++) v += M0[(size_t)i * N + j] * b[j];
+                r[i] -= v;
+            }
+            lu.solve(r);
+            for (int i = 0; i < N; i++) b[i] += r[i];
+        }
         dx.assign(b.begin(), b.begin() + n);
         dl.assign(b.begin() + n, b.end());
         return lu.ok;

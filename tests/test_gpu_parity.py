@@ -278,6 +278,30 @@ def test_fov_controller_matches_oracle(mpclib, scale, n_agents):
     compare(cfg, g, ref, agents)
 
 
+def test_fov_controller_matches_oracle_after_closed_loop(mpclib):
+    """Config 5 on states the closed loop produced (40 device steps of a crowded swarm): observed
+    neighbours close in, so the batch mixes optimal solves with FoV/Voronoi-infeasible ones, each
+    checked against the oracle."""
+    torch = _torch()
+    cfg = swarm.fov_config(20)
+    states, targets = swarm.heading_swarm(100, seed=3)
+    states[:, :2] *= 0.6
+    targets[:, :2] *= 0.6
+    dev = torch.device("cuda", 0)
+    ctx = mpclib.Context(cfg)
+    a, b = torch.tensor(states, device=dev), torch.empty((100, 6), dtype=torch.float64, device=dev)
+    r = ctx.run_steps(a, b, 40, targets=torch.tensor(targets, device=dev), knn_k=8,
+                      knn_radius=cfg["fov_Rs"])
+    torch.cuda.synchronize()
+    evolved = r["final"].cpu().numpy()
+    rp, col = swarm.fov_csr(evolved, 8, cfg["fov_Rs"], cfg["fov_beta"])
+    g = run_gpu(ctx, evolved, targets, rp, col, torch)
+    agents = list(range(100))
+    ref = run_oracle(cfg, evolved, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
+    assert np.any(g["status"] == O.INFEASIBLE) and np.any(g["status"][:, 0] == O.OPTIMAL)
+
+
 def test_fov_grid_neighbours_match_csr(mpclib):
     """Device FoV neighbour query (grid + field-of-view cone) == the CPU observed-neighbour lists."""
     torch = _torch()

@@ -19,12 +19,18 @@ N = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 WARM = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 VARIANTS = [int(v) for v in sys.argv[3:]] or [0, 3]
 PH = ["setup", "neighbours", "cbf_rows0", "solve0", "cbf_rows1", "solve1", "outputs"]
-cfg = swarm.config(15)
-states_h, targets_h = swarm.lattice_swarm(N)
+FOV = os.environ.get("WORKLOAD", "") == "fov"
+if FOV:
+    cfg = swarm.fov_config(20)
+    states_h, targets_h = swarm.heading_swarm(N)
+    states_h[:, :2] *= float(os.environ.get("SCALE", "1.0"))
+else:
+    cfg = swarm.config(15)
+    states_h, targets_h = swarm.lattice_swarm(N)
 dev = torch.device("cuda", 0)
 st = torch.tensor(states_h, device=dev)
 tg = torch.tensor(targets_h, device=dev)
-radius = 3.0 * cfg["d_min"]
+radius = cfg["fov_Rs"] if FOV else 3.0 * cfg["d_min"]
 ctx = Context(cfg)
 out = ctx.alloc_outputs(N)
 for _ in range(WARM):
@@ -33,6 +39,8 @@ for _ in range(WARM):
 torch.cuda.synchronize()
 snap = st.clone()
 PDIP = os.environ.get("MPCCBF_LIB", "").find("prof") >= 0  # profiling build: in-loop stamps
+PPH_FOV = ["rows+LDS", "gram (MFMA)", "reduce+Py+rd", "cholesky", "pred solve", "pred rows+red",
+           "corr G^T v", "corr solve", "step rows+red", "update y", "tail"]
 PPH = ["rows+acc", "reduce acc", "rp/py/conv", "cholesky", "pred solve", "pred steps+min",
        "mua", "corr rows+vc", "corr solve", "corr steps+min", "update"]
 for v in VARIANTS:
@@ -50,7 +58,7 @@ for v in VARIANTS:
         tot = ps[okp, 11] - ps[okp, 0]
         print(f"variant {v}: Newton step 2 of solve 0, {okp.sum()} agents, cycles mean {tot.mean():.0f} "
               f"p50 {np.median(tot):.0f}")
-        for k, name in enumerate(PPH):
+        for k, name in enumerate(PPH_FOV if FOV else PPH):
             print(f"   {name:15s} mean {d[:, k].mean():7.0f}  p50 {np.median(d[:, k]):7.0f} cycles")
     status = out["status"].cpu().numpy()
     t0 = s[:, 0].min()
@@ -67,6 +75,11 @@ for v in VARIANTS:
             pass
         print(f"   {name:11s} mean {d.mean():7.2f} p50 {np.median(d):7.2f} p99 {np.percentile(d, 99):7.2f} "
               f"max {d.max():7.2f} us")
+    its = out["iters"].cpu().numpy()
+    ok0 = (status[:, 0] == 0) & (its[:, 0] > 0)
+    per = (s[ok0, 4] - s[ok0, 3]) / its[ok0, 0]
+    print(f"   solve0 per Newton iteration: mean {per.mean():.2f} p50 {np.median(per):.2f} us "
+          f"(iters mean {its[ok0, 0].mean():.1f})")
     crit = int(np.argmax(end))
     print(f"   critical agent {crit}: status {status[crit]}, start {start[crit]:.1f}, "
           f"phases {np.round(np.diff(s[crit]), 2)}")
