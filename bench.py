@@ -107,7 +107,7 @@ def main():
         cfg = swarm.fov_config(args.k_hor)
         radius = cfg["fov_Rs"]  # observed neighbours: inside the FoV cone and the sensing range
         states_h, targets_h = swarm.heading_swarm(total)
-        states_h[:, :2] *= 0.7  # 3.5 m lattice: 2-4 observed neighbours per agent
+        # 5 m lattice, sensing range 6 m: 1-3 observed neighbours per agent, steady closed loop
     else:
         cfg = swarm.config(args.k_hor)
         radius = 3.0 * cfg["d_min"]
@@ -232,6 +232,7 @@ def main():
         # average launch time (FP64-compute bound; bytes per launch are tiny)
         flops_per_launch = flops_rank0 / nsteps
         achieved_tf = flops_per_launch / (kern_avg * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic(kname)
         res = {
             "metric": "QP solves/sec (whole node) + p99 step latency, N-agent horizon-15 MPC-CBF",
             "value": qps,
@@ -269,7 +270,9 @@ def main():
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "kernel": kname,
                 "kernel_avg_us": kern_avg * 1e3,
                 "flops_per_launch": flops_per_launch,
@@ -281,6 +284,25 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kname: str):
+    """HBM bytes per launch of kernel `kname` from the newest committed PMC summary
+    (profiles/r*_pmc_summary.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
+    gfx950-corrected by tools/pmc_summary.py). The counters cannot be read from inside a timed
+    run, so the value comes from the separate counter pass of the same command; None if absent."""
+    import glob
+    key = kname.replace(" ", "")
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for name, v in d.items():
+            n = name.replace(" ", "").replace("void", "").replace("mpccbf::dev::", "")
+            if n == key and "hbm_bytes_per_launch_corrected" in v:
+                return float(v["hbm_bytes_per_launch_corrected"]), os.path.relpath(f, REPO)
+    return None, None
 
 
 def cpu_baseline(cfg, states_h, targets_h, args, radius):

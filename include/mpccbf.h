@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 5
+#define MPCCBF_ABI_VERSION 6
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -152,12 +152,25 @@ typedef struct mpccbf_batch {
     int32_t knn_k;
     double knn_radius;
     int64_t* stamps;
+    /* Closed-loop simulator semantics (MPCCBFFormationControl_example.cpp:150-221), optional.
+     * traj_t != NULL (device, num_agents): x is the persistent trajectory store — an agent whose
+     * optimize() yields a curve (trajs non-empty) gets it written to x and traj_t = 0; one
+     * without keeps its previous x; the next state is that curve (position, velocity) at
+     * t = min(traj_t + Ts * int(h / Ts), max parameter), which becomes the new traj_t. With no
+     * curve yet (traj_t < 0; initialise to -1) the agent holds its position at zero velocity.
+     * traj_t == NULL: next state = this step's curve at t = h, or the current state if none. */
+    double* traj_t;
+    double pos_std, vel_std;  /* Gaussian noise added to the next state's position / velocity
+                                 (math::addRandomNoise, Random.cpp:7-28); 0 = off */
+    uint64_t noise_seed;      /* counter-based: noise(seed, step_index, agent, component) */
+    int64_t step_index;       /* mpccbf_run_steps adds the step number */
 } mpccbf_batch;
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);
 
 /* ---- Closed-loop stepping (the MPCCBFFormationControl_example.cpp:131-231 loop: every agent
- * re-plans from the states the previous step produced, Jacobi update at t = h, no noise) ------
+ * re-plans from the states the previous step produced — a Jacobi sweep, where the reference
+ * updates robots one after another — with the batch's fallback / noise semantics) ------------
  *
  * mpccbf_run_steps enqueues num_steps control steps back to back on the stream. Step s reads
  * table T_s (T_0 = batch->states, then alternating with run->states_alt; both num_states x 6,

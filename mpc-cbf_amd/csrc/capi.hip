@@ -91,6 +91,10 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     if (grid && (b->knn_k < 1 || !(b->knn_radius > 0)))
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
     if (!b->targets && !b->refs) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "targets or refs required");
+    if (b->traj_t && !b->x)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "traj_t (closed-loop fallback) needs the persistent x buffer");
+    if (!(b->pos_std >= 0.0) || !(b->vel_std >= 0.0))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "noise standard deviations must be >= 0");
     ImpcArgs a;
     std::memset(&a, 0, sizeof(a));
     HIP_TRY(hipSetDevice(c->device));
@@ -130,6 +134,11 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.iters = b->iters;
     a.next_states = b->next_states;
     a.stamps = b->stamps;
+    a.traj_t = b->traj_t;
+    a.pos_std = b->pos_std;
+    a.vel_std = b->vel_std;
+    a.noise_seed = b->noise_seed;
+    a.step_index = b->step_index;
     if (ev0) HIP_TRY(hipEventRecord(ev0, stream));
     hipError_t e = c->dev.cbf_mode == 1 ? launch_impc_fov(c->dev, c->dbuf, a, stream)
                                         : launch_impc(c->dev, c->dbuf, a, c->variant, stream);
@@ -214,6 +223,11 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     pack(v, d.o_PS, o.PS);
     pack(v, d.o_AZ, o.AZ);
     pack(v, d.o_AS, o.AS);
+    d.P = p->num_pieces;
+    pack(v, d.o_EB0, o.EB0);
+    pack(v, d.o_EB1, o.EB1);
+    pack(v, d.o_cum, o.cum);
+    d.eval_step = o.eval_step;
     // separable layout: box rows regrouped by channel, 16 per channel (lanes of a group)
     d.sep = 0;
     d.o_Gsep = 0;
@@ -432,6 +446,7 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
         double* nxt = tables[(s & 1) ^ 1];
         sb.states = cur;
         sb.next_states = nxt + (size_t)first * 6;
+        sb.step_index = b->step_index + s;
         if (r->status_log) sb.status = r->status_log + (size_t)s * per_log;
         if (r->iters_log) sb.iters = r->iters_log + (size_t)s * per_log;
         if (!r->comm) {  // rows this batch does not solve (static agents) carry over

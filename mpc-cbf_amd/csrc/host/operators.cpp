@@ -478,6 +478,10 @@ Operators build_operators(const mpccbf_params& p, bool keep_redundant) {
         op.AZ = E * op.Z;
         op.AS = E * op.Xs;
     }
+    op.EB0 = bernstein_derivative_monomials(cv.C - 1, cv.T, 0);
+    op.EB1 = bernstein_derivative_monomials(cv.C - 1, cv.T, 1);
+    op.cum = cv.cum;
+    op.eval_step = p.Ts * (double)(int)(p.h / p.Ts);  // example :188-190, last sub-step
     if (p.cbf_mode == 1) {
         for (int j = 0; j < cv.C; j++) {
             Mat E(2, n);

@@ -46,6 +46,10 @@ struct Operators {
     // predicted states at h_samples(k), k < cbf_h: pos/vel rows, condensed
     std::vector<Mat> PZ, PS;  // cbf_h of (6 x nz), (6 x 6): rows 0..2 pos, 3..5 vel
     Mat AZ, AS;               // (6 x nz), (6 x 6): state at t = h (closed-loop update)
+    // closed-loop simulator (example :150-221): evaluate a stored curve at any t
+    Mat EB0, EB1;             // C x C monomial coefficients of the Bernstein basis / derivative
+    std::vector<double> cum;  // cumulative piece parameters (SingleParameterPiecewiseCurve)
+    double eval_step = 0.0;   // Ts * int(h / Ts): eval-time advance per control step
     // FoV controller (cbf_mode 1): Voronoi rows act on the piece-0 control points
     // (BezierQPOperations::hyperplaneConstraintAll, :270-285): control point j of dims x, y
     std::vector<Mat> VZ, VS;  // C of (2 x nz), (2 x 6)

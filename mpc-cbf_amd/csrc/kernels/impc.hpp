@@ -29,6 +29,10 @@ struct DevOps {
     int32_t cbf_mode, C;
     double fov_beta, fov_Ds, fov_Rs, bbox[3];
     int32_t o_VZ, o_VS, o_Wbox, o_P16, o_LP16;
+    // closed-loop simulator: stored-curve evaluation (EB0 / EB1: C x C Bernstein monomials of
+    // value / first derivative, cum: P cumulative piece parameters)
+    int32_t P, o_EB0, o_EB1, o_cum;
+    double eval_step;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;
@@ -79,6 +83,12 @@ struct ImpcArgs {
     int32_t* iters;
     double* next_states;
     int64_t* stamps;  // diagnostics: num_agents x NSTAMP shader-clock stamps, or nullptr
+    // closed-loop simulator semantics (traj_t != nullptr): x keeps the last successful curve,
+    // traj_t its evaluation time (-1: none yet); Gaussian noise on the next state
+    double* traj_t;
+    double pos_std, vel_std;
+    uint64_t noise_seed;
+    int64_t step_index;
 };
 
 constexpr int NSTAMP = 8;

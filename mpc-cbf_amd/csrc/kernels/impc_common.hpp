@@ -309,13 +309,73 @@ __device__ __forceinline__ double reduced_objective(const DevOps& op, const doub
     return v;
 }
 
-// Control points of the kept curve and the closed-loop next state (curve at t = h).
+// Counter-based normal samples for the closed-loop noise (math::addRandomNoise draws from a
+// std::mt19937 seeded by std::random_device, i.e. irreproducibly; here every sample is a pure
+// function of (seed, step, agent, component) so runs repeat): splitmix64 + Box-Muller.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double normal_sample(uint64_t seed, int64_t step, int64_t agent, int comp) {
+    uint64_t k = mix64(seed);
+    k = mix64(k ^ (uint64_t)step);
+    k = mix64(k ^ ((uint64_t)agent * 8u + (uint64_t)comp));
+    const double u1 = (double)((k >> 11) + 1) * 0x1.0p-53;  // (0, 1]
+    const double u2 = (double)(mix64(k) >> 11) * 0x1.0p-53;
+    return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+}
+
+// Component comp (0..2 position x/y/yaw, 3..5 velocity) at parameter t of a piecewise Bezier
+// curve (SingleParameterPiecewiseCurve::eval, SingleParameterPiecewiseCurve.cpp:94-127:
+// lower_bound piece lookup, local parameter min(T, t - cum[i-1]); Bezier::eval with the
+// monomial Bernstein basis). The control points come from xrow (stored curve) or, when xrow is
+// null, from x = Xs s0 + Z y of this step's solution.
+template <int NZ>
+__device__ double curve_component(const DevOps& op, const double* buf, const double* xrow,
+                                  const double (&s0)[6], const double (&yk)[NZ], double t, int comp) {
+    const double* cum = opp(buf, op.o_cum);
+    int piece = 0;
+    while (piece < op.P - 1 && cum[piece] < t) piece++;
+    const double par = piece == 0 ? t : fmin(cum[0], t - cum[piece - 1]);
+    const int d = comp % 3;
+    const double* EB = opp(buf, comp < 3 ? op.o_EB0 : op.o_EB1);
+    const double* Z = opp(buf, op.o_Z);
+    const double* Xs = opp(buf, op.o_Xs);
+    const int C = op.C;
+    double v = 0.0;
+    for (int cp = 0; cp < C; cp++) {
+        const int idx = piece * 3 * C + d * C + cp;
+        double xv;
+        if (xrow) {
+            xv = xrow[idx];
+        } else {
+            xv = 0.0;
+#pragma unroll
+            for (int s = 0; s < 6; s++) xv = fma(Xs[idx * 6 + s], s0[s], xv);
+#pragma unroll
+            for (int j = 0; j < NZ; j++) xv = fma(Z[idx * NZ + j], yk[j], xv);
+        }
+        double b = 0.0, tp = 1.0;
+        for (int j = 0; j < C; j++, tp *= par) b = fma(EB[cp * C + j], tp, b);
+        v = fma(xv, b, v);
+    }
+    return v;
+}
+
+// Control points of the kept curve and the closed-loop next state.
+//   default: x = this step's curve (NaN if none), next state = that curve at t = h, or the
+//            current state when optimize() produced no curve;
+//   args.traj_t set (closed-loop simulator, MPCCBFFormationControl_example.cpp:150-221): x is
+//            the persistent last successful curve, next state = it at the advanced time.
 template <int NZ, int G>
 __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const double* buf,
                                                     const ImpcArgs& args, int ai, int gl,
                                                     const double (&s0)[6], const double (&yk)[NZ],
                                                     bool have_curve) {
-    if (args.x) {
+    const bool sim = args.traj_t != nullptr;
+    if (args.x && (have_curve || !sim)) {
         const double* Z = opp(buf, op.o_Z);
         const double* Xs = opp(buf, op.o_Xs);
         for (int i = gl; i < op.n; i += G) {
@@ -331,22 +391,36 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
             args.x[(size_t)ai * op.n + i] = v;
         }
     }
-    if (args.next_states && gl < 6) {
-        double v = 0.0;
-        if (have_curve) {
-            const double* AZ = opp(buf, op.o_AZ);
-            const double* AS = opp(buf, op.o_AS);
+    if (gl >= 6) return;
+    double v = 0.0;
+    if (sim) {
+        const double t_prev = have_curve ? 0.0 : args.traj_t[ai];
+        double t_new = t_prev;
+        if (have_curve || t_prev >= 0.0) {
+            t_new = fmin(t_prev + op.eval_step, opp(buf, op.o_cum)[op.P - 1]);  // example :190-193
+            v = curve_component<NZ>(op, buf, have_curve ? nullptr : args.x + (size_t)ai * op.n, s0, yk,
+                                    t_new, gl);
+        } else {  // no trajectory yet: hold position, zero velocity (example :210-216)
 #pragma unroll
-            for (int s = 0; s < 6; s++) v = fma(AS[gl * 6 + s], s0[s], v);
-#pragma unroll
-            for (int j = 0; j < NZ; j++) v = fma(AZ[gl * NZ + j], yk[j], v);
-        } else {
-#pragma unroll
-            for (int s = 0; s < 6; s++)
+            for (int s = 0; s < 3; s++)
                 if (s == gl) v = s0[s];
         }
-        args.next_states[(size_t)ai * 6 + gl] = v;
+        if (gl == 0) args.traj_t[ai] = t_new;  // every lane read t_prev above (same wave)
+    } else if (have_curve) {
+        const double* AZ = opp(buf, op.o_AZ);
+        const double* AS = opp(buf, op.o_AS);
+#pragma unroll
+        for (int s = 0; s < 6; s++) v = fma(AS[gl * 6 + s], s0[s], v);
+#pragma unroll
+        for (int j = 0; j < NZ; j++) v = fma(AZ[gl * NZ + j], yk[j], v);
+    } else {
+#pragma unroll
+        for (int s = 0; s < 6; s++)
+            if (s == gl) v = s0[s];
     }
+    const double sd = gl < 3 ? args.pos_std : args.vel_std;
+    if (sd > 0.0) v = fma(sd, normal_sample(args.noise_seed, args.step_index, args.agent_first + ai, gl), v);
+    if (args.next_states) args.next_states[(size_t)ai * 6 + gl] = v;
 }
 
 // diagnostics: wall-clock stamp (s_memrealtime, 100 MHz, chip-wide) of phase `k` of agent ai
