@@ -140,8 +140,12 @@ def main():
             dist.broadcast(uid, 0)
             comm = Comm(bytes(uid.cpu().tolist()), world, rank, local)
         tables = [full0, torch.empty_like(full0)]
+        # the example's closed loop: fallback to the last successful trajectory, state noise
+        # pos_std / vel_std of base_config.json physical_limits (example :150-221)
+        traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
         common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn,
-                      knn_radius=radius, x=out["x"], obj=out["obj"], comm=comm)
+                      knn_radius=radius, x=out["x"], obj=out["obj"], comm=comm, traj_t=traj_t,
+                      pos_std=0.001, vel_std=0.01, noise_seed=20251015)
         r = ctx.run_steps(tables[0], tables[1], args.warmup, status=out["status"],
                           iters=out["iters"], reserve_steps=nsteps, **common)
         if r["final"] is not tables[0]:
@@ -151,7 +155,7 @@ def main():
         # one event per step (p99 step latency); the IMPC kernel is bracketed by its own events on
         # every 16th step only (each event pair adds ~10 us of barrier packets to a step)
         r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=status_log, iters_log=iters_log,
-                          timing=True, solve_stride=16, **common)
+                          timing=True, solve_stride=16, step_index=args.warmup, **common)
         barrier_sync()
         t1 = time.perf_counter()
         step_ms, kern_ms = r["step_ms"].astype(np.float64), r["solve_ms"].astype(np.float64)
@@ -246,7 +250,10 @@ def main():
             "scaling": "weak" if args.agents_total <= 0 else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (jittered-lattice swarm, seed 20251015)",
+            "data": ("synthetic (jittered-lattice swarm, seed 20251015); closed loop with the "
+                     "example's trajectory fallback and state noise (pos 1e-3, vel 1e-2)"
+                     if args.loop == "native" and args.neighbours == "grid" else
+                     "synthetic (jittered-lattice swarm, seed 20251015); closed loop"),
             "config": {
                 "workload": (
                     (f"config5: {total} agents ({per}/GPU), FoV 120 deg + Voronoi CBF, horizon "
