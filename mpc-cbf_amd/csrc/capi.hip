@@ -224,6 +224,9 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     pack(v, d.o_AZ, o.AZ);
     pack(v, d.o_AS, o.AS);
     d.P = p->num_pieces;
+    d.slack_mode = p->slack_mode ? 1 : 0;
+    d.slack_cost = p->slack_cost;
+    d.slack_decay = p->slack_decay_rate;
     pack(v, d.o_EB0, o.EB0);
     pack(v, d.o_EB1, o.EB1);
     pack(v, d.o_cum, o.cum);

@@ -33,6 +33,10 @@ struct DevOps {
     // value / first derivative, cum: P cumulative piece parameters)
     int32_t P, o_EB0, o_EB1, o_cum;
     double eval_step;
+    // slack mode (collision controller): one slack variable per neighbour, cost
+    // slack_cost * slack_decay^rank (ConnectivityIMPCCBF.cpp:73-100)
+    int32_t slack_mode;
+    double slack_cost, slack_decay;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;

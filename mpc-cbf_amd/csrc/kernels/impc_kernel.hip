@@ -167,7 +167,77 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
 // ---------------------------------------------------------------------------------------------
 // Separable layout (x / y / yaw channels, 2 reduced variables each; pdip_sep.hpp)
 // ---------------------------------------------------------------------------------------------
-template <int SB, int CB>
+// Slack mode: lane j builds the CBF rows of neighbour j itself (slot k = sample k), so all rows
+// of one slack variable live in the lane that owns it. Filtered rows stay inert (ccv = 0).
+// Returns the group-uniform "some row is live" flag.
+template <int G, int CB>
+__device__ bool lane_cbf_rows(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
+                              const double (&s0)[6], const double (&y)[SEP_NZ], bool grid_mode,
+                              const int32_t* nbl, int nb0, int nnb, int gl, SepRows<1, CB>& rw) {
+    const double* UZ = opp(buf, op.o_UZ);
+    const double* US = opp(buf, op.o_US);
+    const int nk = (it == 0) ? 1 : op.cbf_h;
+    bool live = false;
+#pragma unroll
+    for (int k = 0; k < CB; k++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) rw.cg[k][j] = 0.0;
+        rw.chi[k] = 1.0;
+        rw.ccv[k] = 0.0;
+        if (k < nk && gl < nnb) {
+            double e[6];
+            cbf_ego_state<SEP_NZ>(op, buf, it, k, s0, y, e);
+            const int nbi = grid_mode ? nbl[gl] : args.nb_col[nb0 + gl];
+            const double* ns = args.states + (size_t)nbi * 6;
+            double a[3], b;
+            safety_cbf(e, ns[0], ns[1], ns[3], ns[4], op.d_min, a, b);
+            double bmax = 0.0;
+#pragma unroll
+            for (int d = 0; d < 3; d++) bmax += fmax(-a[d] * op.a_lo[d], -a[d] * op.a_hi[d]);
+            if (!(op.cbf_filter && b >= bmax)) {  // implied by the acceleration box: drop
+                const double* UZk = UZ + (size_t)k * 3 * SEP_NZ;
+                const double* USk = US + (size_t)k * 18;
+                double us = 0.0;
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int s = 0; s < 6; s++) v = fma(USk[d * 6 + s], s0[s], v);
+                    us = fma(a[d], v, us);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    rw.cg[k][j] = -(a[0] * UZk[j] + a[1] * UZk[SEP_NZ + j] + a[2] * UZk[2 * SEP_NZ + j]);
+                rw.chi[k] = b + us;
+                rw.ccv[k] = 1.0;
+                live = true;
+            }
+        }
+    }
+    return grp_ballot<G>(live) != 0ull;
+}
+
+// Slack weight of this lane's neighbour: slack_cost * decay^rank, rank by planar distance
+// (ConnectivityIMPCCBF.cpp:73-100; ties by list position — the reference's std::sort leaves
+// them unspecified). Lanes without a neighbour get cost 1 (their slack has no rows: v -> 0).
+template <int G>
+__device__ double lane_slack_weight(const DevOps& op, const ImpcArgs& args, const double (&s0)[6],
+                                    bool grid_mode, const int32_t* nbl, int nb0, int nnb, int gl) {
+    double dist = 0.0;
+    if (gl < nnb) {
+        const int nbi = grid_mode ? nbl[gl] : args.nb_col[nb0 + gl];
+        const double dx = args.states[(size_t)nbi * 6] - s0[0], dy = args.states[(size_t)nbi * 6 + 1] - s0[1];
+        dist = sqrt(dx * dx + dy * dy);
+    }
+    int rank = 0;
+    for (int k = 0; k < nnb; k++) {
+        const double dk = __shfl(dist, k, G);
+        rank += (dk < dist || (dk == dist && k < gl)) ? 1 : 0;
+    }
+    return gl < nnb ? op.slack_cost * pow(op.slack_decay, (double)rank) : 1.0;
+}
+
+template <int SB, int CB, bool SLACK>
 __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
                                                         const ImpcArgs args) {
     constexpr int G = 16;
@@ -180,7 +250,7 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
     if (ai >= args.num_agents) return;
     stamp(args, ai, gl, 0);
 
-    __shared__ double stage_all[GPB][cap * (NZ + 1)];
+    __shared__ double stage_all[GPB][SLACK ? 1 : cap * (NZ + 1)];
     double* stage = stage_all[gib];
 
     const int self = args.agent_first + ai;
@@ -221,8 +291,10 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
     } else {
         nnb = grid_neighbors<G>(args, self, s0[0], s0[1], nb_scratch[gib], gl);
     }
-    const bool nb_overflow = nnb < 0;
+    const bool nb_overflow = nnb < 0 || (SLACK && nnb > G);  // slack mode: one lane per neighbour
     if (nb_overflow) nnb = 0;
+    double wslack = 0.0, vslack = 0.0;
+    if constexpr (SLACK) wslack = lane_slack_weight<G>(op, args, s0, grid_mode, nb_scratch[gib].idx, nb0, nnb, gl);
     stamp(args, ai, gl, 2);
 
     double y[NZ], ykeep[NZ];
@@ -238,18 +310,27 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
             continue;
         }
         bool row_infeasible = false;
-        const int count = stage_cbf_rows<NZ, G>(op, buf, args, it, s0, y, grid_mode, nb_scratch[gib].idx,
-                                                nb0, nnb, stage, cap, gl, &row_infeasible);
-        if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
+        int count = 0;
+        bool live = false;
+        if constexpr (SLACK) {
+            // slack mode: rows stay in their neighbour's lane; a slack row is never infeasible
+            live = lane_cbf_rows<G, CB>(op, buf, args, it, s0, y, grid_mode, nb_scratch[gib].idx, nb0, nnb, gl, rw);
+        } else {
+            count = stage_cbf_rows<NZ, G>(op, buf, args, it, s0, y, grid_mode, nb_scratch[gib].idx,
+                                          nb0, nnb, stage, cap, gl, &row_infeasible);
+            live = count > 0;
 #pragma unroll
-        for (int c = 0; c < CB; c++) {
-            const int ci = c * G + gl;
-            const bool on = ci < count && ci < cap;
-            const double* src = stage + (size_t)(on ? ci : 0) * (NZ + 1);
+            for (int c = 0; c < CB; c++) {
+                const int ci = c * G + gl;
+                const bool on = ci < count && ci < cap;
+                const double* src = stage + (size_t)(on ? ci : 0) * (NZ + 1);
 #pragma unroll
-            for (int j = 0; j < 4; j++) rw.cg[c][j] = on ? src[j] : 0.0;  // yaw columns are 0
-            rw.chi[c] = on ? src[NZ] : 1.0;  // unused slot: inert row 0 <= 1
+                for (int j = 0; j < 4; j++) rw.cg[c][j] = on ? src[j] : 0.0;  // yaw columns are 0
+                rw.chi[c] = on ? src[NZ] : 1.0;  // unused slot: inert row 0 <= 1
+                rw.ccv[c] = 0.0;
+            }
         }
+        if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
         int st;
         int nit = 0;
         if (count > cap || nb_overflow) {
@@ -264,18 +345,31 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
 #else
             long long* dbg = nullptr;
 #endif
-            const PdipOut po = pdip_solve_sep<G, SB, CB>(rw, count > 0, opp(buf, op.o_Pr),
-                                                         opp(buf, op.o_LPr), q, y, cfg, dbg);
+            const PdipOut po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr),
+                                                                q, y, cfg, dbg, wslack, &vslack);
             st = po.status;
             nit = po.iters;
             if (st != ST_OPTIMAL) {
-                const double tstar = pdip_phase1_sep<G, SB, CB>(rw, cfg);
-                if (tstar > op.feas_tol) st = ST_INFEASIBLE;
+                SepRows<SB, CB> rp1 = rw;
+                if constexpr (SLACK) {  // slack rows are always satisfiable: certify the box rows
+#pragma unroll
+                    for (int c = 0; c < CB; c++) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) rp1.cg[c][j] = 0.0;
+                        rp1.chi[c] = 1.0;
+                    }
+                }
+                const double tstar = pdip_phase1_sep<G, SB, CB>(rp1, cfg);
+                if (tstar > op.feas_tol && tstar < 1e300) st = ST_INFEASIBLE;  // 1e300: phase 1 failed
+#ifdef MPCCBF_DEBUG_EXIT
+                nit += tstar >= 1e300 ? 10000 : 0;
+#endif
             }
         }
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {
             objv = reduced_objective<NZ>(op, buf, q, y, kconst);
+            if constexpr (SLACK) objv += grp_sum<G>(live ? wslack * vslack : 0.0);  // + w^T v
 #pragma unroll
             for (int i = 0; i < NZ; i++) ykeep[i] = y[i];
             have_curve = true;
@@ -302,17 +396,20 @@ static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcA
     return hipGetLastError();
 }
 
-template <int SB, int CB>
+template <int SB, int CB, bool SLACK>
 static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                     hipStream_t s) {
     constexpr int GPB = 256 / 16;
     const int blocks = (a.num_agents + GPB - 1) / GPB;
-    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB>), dim3(blocks), dim3(256), 0, s, op, buf, a);
+    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK>), dim3(blocks), dim3(256), 0, s, op, buf, a);
     return hipGetLastError();
 }
 
 // Instantiation launch_impc picks for (operators, variant); nullptr if none fits.
 const char* impc_kernel_name(const DevOps& op, int variant) {
+    if (op.slack_mode)  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2
+        return (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
+                   ? "impc_sep_kernel<1,2,slack>" : nullptr;
     if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1>";
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
@@ -330,8 +427,13 @@ const char* impc_kernel_name(const DevOps& op, int variant) {
 hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
                        hipStream_t s) {
     if (a.num_agents <= 0) return hipSuccess;
+    if (op.slack_mode) {
+        if (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
+            return launch_impc_sep_t<1, 2, true>(op, buf, a, s);
+        return hipErrorInvalidValue;
+    }
     if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)
-        return launch_impc_sep_t<1, 1>(op, buf, a, s);
+        return launch_impc_sep_t<1, 1, false>(op, buf, a, s);
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return launch_impc_t<6, 16, 4>(op, buf, a, s);
         if (variant == 1 && op.m < 64) return launch_impc_t<6, 64, 1>(op, buf, a, s);

@@ -425,7 +425,7 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
 #pragma unroll
         for (int i = 0; i < NZ; i++) M[S::idx(i, i)] += eps;
         M[S::idx(NZ, NZ)] += Dt;
-        if (!chol_packed<NV>(M, dinv)) return 1e300;
+        if (!chol_packed<NV>(M, dinv)) break;  // degenerate vertex: the iterate's violation stands
 #pragma unroll
         for (int i = 0; i < NZ; i++) rhs[i] = -eps * y[i] + acc[S::P + i];
         rhs[NZ] = -1.0 + acc[S::P + NZ];

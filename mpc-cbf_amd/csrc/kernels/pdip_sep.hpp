@@ -18,6 +18,10 @@
 
 #include "pdip.hpp"
 
+#ifndef MPCCBF_RELAX
+#define MPCCBF_RELAX 1
+#endif
+
 namespace mpccbf {
 namespace dev {
 
@@ -31,6 +35,7 @@ struct SepRows {
     double blo[SEP_D][SB], bhi[SEP_D][SB];
     double cg[CB][4];               // CBF rows: coefficients on (x0, x1, y0, y1); upper side only
     double chi[CB];
+    double ccv[CB];                 // slack mode: 1 if the row carries -v of this lane's neighbour
 };
 
 // accumulator layout of one Newton step
@@ -61,11 +66,23 @@ __device__ __forceinline__ void sep_solve(const double (&Mxy)[10], const double 
 // P: 6x6 row-major block-diagonal reduced Hessian, LP its lower Cholesky factor (uniform).
 // has_cbf: group-uniform flag (some CBF slot of the group is live); when false the CBF slots
 // are skipped entirely (and do not count as sides).
-template <int G, int SB, int CB>
+//
+// SLACK (slack_mode, MPCCBFQPGeneratorBase.cpp:28-130): lane l owns the slack variable v >= 0 of
+// neighbour l, with linear cost wv; its CBF rows read g^T y - v <= chi (ccv = 1). v couples
+// only to the (x, y) block and to its own rows, so it is eliminated per lane (Schur complement
+// of the scalar v-block d): the group still reduces the same 20 values, with
+//   M_xy -= u u^T / d,  rhs_xy -= u rhs_v / d,   u = -sum_rows D g,  d = sum_rows D + D_bound,
+// and dv = (rhs_v - u^T dy) / d is recovered lane-locally after each solve.
+template <int G, int SB, int CB, bool SLACK = false>
 __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                                   const double* __restrict__ LP, const double (&q)[SEP_NZ],
-                                  double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg = nullptr) {
+                                  double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg = nullptr,
+                                  double wv_cost = 0.0, double* v_out = nullptr) {
     (void)dbg;
+    const bool slk = SLACK && has_cbf;  // group-uniform
+    // slack variable, its bound's slack and dual; the dual starts at the linear cost it carries at
+    // the optimum (w = sum_rows z + z_bound with inactive rows)
+    double v = 1.0, sb = 1.0, zb = SLACK ? fmax(wv_cost, 1.0) : 1.0;
     // ---- start: unconstrained minimiser (block-diagonal P: per-channel 2x2 solves)
 #pragma unroll
     for (int d = 0; d < SEP_D; d++) {
@@ -96,11 +113,12 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         double t = 0.0;
 #pragma unroll
         for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
+        if (slk) t -= rw.ccv[c] * v;
         cs[c] = fmax(rw.chi[c] - t, 1.0);
         cz[c] = rcp(cs[c]);
         pc[c] = rcp(1.0 + fabs(rw.chi[c]));
     }
-    const double nsides = (double)(G * (2 * SEP_D * SB + (has_cbf ? CB : 0)));
+    const double nsides = (double)(G * (2 * SEP_D * SB + (has_cbf ? CB : 0) + (slk ? 1 : 0)));
     double qn = 0.0;
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) qn = fmax(qn, fabs(q[j]));
@@ -122,6 +140,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         // per side: residual r, 1/s, D = z/s
         double rl[SEP_D][SB], ru[SEP_D][SB], il[SEP_D][SB], iu[SEP_D][SB];
         double cr[CB], ci[CB];
+        double rb = 0.0, ib = 0.0, dS = 0.0;
+        double DcA[CB];  // slack mode: D of the live rows
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
@@ -152,9 +172,15 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 double t = 0.0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) t = fma(g[j], y[j], t);
+                if (slk) t -= rw.ccv[c] * v;
                 cr[c] = rw.chi[c] - t - cs[c];
                 ci[c] = rcp(cs[c]);
-                const double D = cz[c] * ci[c];
+                double D = cz[c] * ci[c];
+                DcA[c] = 0.0;
+                if (slk) {  // live slack rows enter through the stable Schur form below
+                    DcA[c] = D * rw.ccv[c];
+                    D -= DcA[c];
+                }
                 const double wv = D * cr[c];
                 acc_blk2(acc + A_MX, D, g[0], g[1]);
                 acc_blk2(acc + A_MY, D, g[2], g[3]);
@@ -172,8 +198,68 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 }
                 rp = fmax(rp, fabs(cr[c]) * pc[c]);
             }
+            if (slk) {
+                // bound v >= 0 (lower side, own slack sb). Eliminating v leaves, for the live rows
+                // a, b of this lane, W = diag(D) - D D^T / S (S = sum D + D_b) between their g's,
+                // accumulated in the Laplacian form
+                //   sum_{a<b} (D_a D_b / S) (g_a - g_b)(g_a - g_b)^T + sum_a (D_a D_b' / S) g_a g_a^T
+                // (D_b': the bound's weight): positive terms only, so nearly active rows (huge D)
+                // on nearly parallel g (samples k = 0, 1 of one neighbour) do not cancel.
+                rb = v - sb;
+                ib = rcp(sb);
+                const double Db = zb * ib;
+                dS = Db;
+#pragma unroll
+                for (int a = 0; a < CB; a++) dS += DcA[a];
+                const double iS = rcp(dS);
+#pragma unroll
+                for (int a = 0; a < CB; a++) {
+                    const double* g = rw.cg[a];
+                    const double wa = DcA[a] * Db * iS;
+                    acc_blk2(acc + A_MX, wa, g[0], g[1]);
+                    acc_blk2(acc + A_MY, wa, g[2], g[3]);
+                    acc[A_MC + 0] = fma(wa * g[0], g[2], acc[A_MC + 0]);
+                    acc[A_MC + 1] = fma(wa * g[0], g[3], acc[A_MC + 1]);
+                    acc[A_MC + 2] = fma(wa * g[1], g[2], acc[A_MC + 2]);
+                    acc[A_MC + 3] = fma(wa * g[1], g[3], acc[A_MC + 3]);
+                    const double f = DcA[a] * fma(Db, cr[a] - rb, -wv_cost) * iS;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) acc[A_RHS + j] = fma(g[j], f, acc[A_RHS + j]);
+#pragma unroll
+                    for (int b = a + 1; b < CB; b++) {
+                        double e[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) e[j] = g[j] - rw.cg[b][j];
+                        const double wab = DcA[a] * DcA[b] * iS;
+                        acc_blk2(acc + A_MX, wab, e[0], e[1]);
+                        acc_blk2(acc + A_MY, wab, e[2], e[3]);
+                        acc[A_MC + 0] = fma(wab * e[0], e[2], acc[A_MC + 0]);
+                        acc[A_MC + 1] = fma(wab * e[0], e[3], acc[A_MC + 1]);
+                        acc[A_MC + 2] = fma(wab * e[1], e[2], acc[A_MC + 2]);
+                        acc[A_MC + 3] = fma(wab * e[1], e[3], acc[A_MC + 3]);
+                        const double fab = wab * (cr[a] - cr[b]);
+#pragma unroll
+                        for (int j = 0; j < 4; j++) acc[A_RHS + j] = fma(e[j], fab, acc[A_RHS + j]);
+                    }
+                }
+                acc[A_MU] = fma(sb, zb, acc[A_MU]);
+                rp = fmax(rp, fabs(rb));
+            }
             PSTAMP(1);
             grp_sum_vec<G, A_N>(acc);
+#ifdef MPCCBF_DEBUG_EXIT
+            if (dbg) {  // is the reduced accumulator group-uniform?
+                double dvg = 0.0;
+#pragma unroll
+                for (int k = 0; k < A_N; k++) dvg = fmax(dvg, fabs(acc[k] - __shfl(acc[k], 0, G)));
+                dvg = grp_max<G>(dvg);
+                double* dd = (double*)dbg;
+                if (dvg > 0.0 && dd[13] == 0.0) {
+                    dd[12] = dvg;
+                    dd[13] = (double)(it + 1);
+                }
+            }
+#endif
         } else {
             // no CBF row in this group: the x-y coupling block stays zero
             double part[A_N - 4];
@@ -203,35 +289,51 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             double rdn = 0.0;
 #pragma unroll
             for (int i = 0; i < SEP_NZ; i++) rdn = fmax(rdn, fabs(py[i] + accr[i]));
+            if (slk) {  // v: w - sum_rows cz - zb (relative to the slack cost scale)
+                double rv = wv_cost - zb;
+#pragma unroll
+                for (int c = 0; c < CB; c++) rv = fma(-rw.ccv[c], cz[c], rv);
+                rdn = fmax(rdn, grp_max<G>(fabs(rv) * rcp(1.0 + fabs(wv_cost))) * (1.0 + qn));  // per-lane scale, then the group max
+            }
             rd_track = rdn * inv_qn;
             rd_exact = false;
         }
         out.iters = it;
         const bool finite = isfinite(rp) && isfinite(rd_track) && isfinite(mu) && isfinite(acc[0]);
+        // exact dual residual (relative), group-uniform
+        auto exact_rd = [&]() {
+            double chk[SEP_NZ];
+#pragma unroll
+            for (int i = 0; i < SEP_NZ; i++) chk[i] = 0.0;
+#pragma unroll
+            for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+                for (int k = 0; k < SB; k++) {
+                    const double dz = zu[d][k] - zl[d][k];
+                    chk[2 * d] = fma(rw.bg[d][k][0], dz, chk[2 * d]);
+                    chk[2 * d + 1] = fma(rw.bg[d][k][1], dz, chk[2 * d + 1]);
+                }
+            if (has_cbf) {
+#pragma unroll
+                for (int c = 0; c < CB; c++)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) chk[j] = fma(rw.cg[c][j], cz[c], chk[j]);
+            }
+            grp_sum_vec<G, SEP_NZ>(chk);
+            double rdn = 0.0;
+#pragma unroll
+            for (int i = 0; i < SEP_NZ; i++) rdn = fmax(rdn, fabs(py[i] + chk[i]));
+            if (slk) {
+                double rv = wv_cost - zb;
+#pragma unroll
+                for (int c = 0; c < CB; c++) rv = fma(-rw.ccv[c], cz[c], rv);
+                rdn = fmax(rdn, grp_max<G>(fabs(rv) * rcp(1.0 + fabs(wv_cost))) * (1.0 + qn));  // per-lane scale, then the group max
+            }
+            return rdn * inv_qn;
+        };
         if (finite && rp <= cfg.tol && mu <= cfg.tol * 0.1) {
             if (rd_track <= cfg.tol) {
-                double chk[SEP_NZ];
-#pragma unroll
-                for (int i = 0; i < SEP_NZ; i++) chk[i] = 0.0;
-#pragma unroll
-                for (int d = 0; d < SEP_D; d++)
-#pragma unroll
-                    for (int k = 0; k < SB; k++) {
-                        const double dz = zu[d][k] - zl[d][k];
-                        chk[2 * d] = fma(rw.bg[d][k][0], dz, chk[2 * d]);
-                        chk[2 * d + 1] = fma(rw.bg[d][k][1], dz, chk[2 * d + 1]);
-                    }
-                if (has_cbf) {
-#pragma unroll
-                    for (int c = 0; c < CB; c++)
-#pragma unroll
-                        for (int j = 0; j < 4; j++) chk[j] = fma(rw.cg[c][j], cz[c], chk[j]);
-                }
-                grp_sum_vec<G, SEP_NZ>(chk);
-                double rdn = 0.0;
-#pragma unroll
-                for (int i = 0; i < SEP_NZ; i++) rdn = fmax(rdn, fabs(py[i] + chk[i]));
-                rd_track = rdn * inv_qn;
+                rd_track = exact_rd();
                 if (rd_track <= cfg.tol) {
                     out.status = ST_OPTIMAL;
                     break;
@@ -240,7 +342,17 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         }
         if (it == 0) mu0 = mu;
         if (it >= cfg.maxit || !finite || mu > 1e8 * fmax(mu0, 1.0)) {
+            // out of iterations at a degenerate point the normal matrix can no longer resolve:
+            // the same relaxed KKT acceptance as at a factorisation breakdown (below)
+            if (MPCCBF_RELAX && finite && it >= cfg.maxit && rp <= 1e3 * cfg.tol && mu <= 1e2 * cfg.tol &&
+                exact_rd() <= 1e3 * cfg.tol) {
+                out.status = ST_OPTIMAL;
+                break;
+            }
             out.status = ST_UNKNOWN;
+#ifdef MPCCBF_DEBUG_EXIT  // diagnostics build: exit reason in the iteration count
+            out.iters = it + 1000 * (it >= cfg.maxit ? 1 : !finite ? 2 : 3);
+#endif
             break;
         }
         PSTAMP(3);
@@ -260,10 +372,67 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         Mw[0] = acc[A_MW + 0] + P[4 * 6 + 4];
         Mw[1] = acc[A_MW + 1] + P[4 * 6 + 5];
         Mw[2] = acc[A_MW + 2] + P[5 * 6 + 5];
-        const bool ok4 = chol_packed<4>(Mxy, dxy);
-        const bool ok2 = chol_packed<2>(Mw, dw);
+        bool ok4, ok2;
+        {
+            double M4[10], M2[3];
+#pragma unroll
+            for (int k = 0; k < 10; k++) M4[k] = Mxy[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) M2[k] = Mw[k];
+            ok4 = chol_packed<4>(Mxy, dxy);
+            ok2 = chol_packed<2>(Mw, dw);
+            if (MPCCBF_RELAX && !(ok4 && ok2)) {
+                // a pivot lost to cancellation (active rows' D = z/s ~1e20 against P ~1e5):
+                // retry with a diagonal shift of 1e-12 of the largest diagonal entry (inexact
+                // Newton; residuals and the convergence test stay exact)
+                double dmax = 0.0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) dmax = fmax(dmax, M4[S4::idx(i, i)]);
+#pragma unroll
+                for (int i = 0; i < 2; i++) dmax = fmax(dmax, M2[Sym<2>::idx(i, i)]);
+                const double tau = 1e-12 * dmax;
+#pragma unroll
+                for (int k = 0; k < 10; k++) Mxy[k] = M4[k];
+#pragma unroll
+                for (int k = 0; k < 3; k++) Mw[k] = M2[k];
+#pragma unroll
+                for (int i = 0; i < 4; i++) Mxy[S4::idx(i, i)] += tau;
+#pragma unroll
+                for (int i = 0; i < 2; i++) Mw[Sym<2>::idx(i, i)] += tau;
+                ok4 = chol_packed<4>(Mxy, dxy);
+                ok2 = chol_packed<2>(Mw, dw);
+            }
+        }
         if (!(ok4 && ok2)) {
+            // Breakdown at a degenerate near-optimal point (D = z/s of the active rows ~1e20
+            // swamps P in the normal matrix): keep the iterate if it meets the KKT conditions to
+            // a relaxed tolerance, as the oracle keeps its best iterate (oracle.cpp pdip).
+            if (MPCCBF_RELAX && finite && rp <= 1e3 * cfg.tol && mu <= 1e2 * cfg.tol && exact_rd() <= 1e3 * cfg.tol) {
+                out.status = ST_OPTIMAL;
+                break;
+            }
             out.status = ST_UNKNOWN;
+#ifdef MPCCBF_DEBUG_EXIT
+            out.iters = it + 4000;
+            if (dbg) {  // the matrices that failed (as bits), for tools/dbg_slack.py
+                using S4b = Sym<4>;
+                double* dd = (double*)dbg;
+                dd[0] = acc[A_MX + 0] + P[0];
+                dd[1] = acc[A_MX + 2] + P[7];
+                dd[2] = acc[A_MY + 0] + P[14];
+                dd[3] = acc[A_MY + 2] + P[21];
+                dd[4] = acc[A_MC + 0];
+                dd[5] = acc[A_MC + 3];
+                dd[6] = Mw[0];
+                dd[7] = Mw[2];
+                dd[8] = ok4 ? 1.0 : 0.0;
+                dd[9] = ok2 ? 1.0 : 0.0;
+                dd[10] = mu;
+                dd[11] = slk ? dS : 0.0;
+
+                (void)S4b::idx(0, 0);
+            }
+#endif
             break;
         }
         PSTAMP(4);
@@ -277,6 +446,23 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         // step to the boundary as their reciprocal
         double dsl[SEP_D][SB], dsu[SEP_D][SB], dzl[SEP_D][SB], dzu[SEP_D][SB], cds[CB], cdz[CB];
         double rs = 0.0, rz = 0.0;
+        double dv = 0.0, dsb = 0.0, dzb = 0.0;
+        if (slk) {  // dv = (rhs_v - u^T dy) / S = sum_a D_a (g_a dy - cr_a) / S - (D_b r_b + w) / S
+            dv = -(zb * ib) * rb - wv_cost;
+#pragma unroll
+            for (int a = 0; a < CB; a++) {
+                double gd = -cr[a];
+#pragma unroll
+                for (int j = 0; j < 4; j++) gd = fma(rw.cg[a][j], dya[j], gd);
+                dv = fma(DcA[a], gd, dv);
+            }
+            dv *= rcp(dS);
+            dsb = dv + rb;
+            const double qb = dsb * ib;
+            dzb = -zb * (1.0 + qb);
+            rs = fmax(rs, -qb);
+            rz = fmax(rz, 1.0 + qb);
+        }
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
@@ -296,6 +482,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 double td = 0.0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) td = fma(rw.cg[c][j], dya[j], td);
+                if (slk) td -= rw.ccv[c] * dv;
                 cds[c] = cr[c] - td;
                 const double qc = cds[c] * ci[c];
                 cdz[c] = -cz[c] * (1.0 + qc);
@@ -317,6 +504,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         if (has_cbf) {
 #pragma unroll
             for (int c = 0; c < CB; c++) mua = fma(cs[c] + ap * cds[c], cz[c] + ad * cdz[c], mua);
+            if (slk) mua = fma(sb + ap * dsb, zb + ad * dzb, mua);
         }
         mua = grp_sum<G>(mua) * inv_ns;
         double sig = mu > 0.0 ? mua * rcp(mu) : 0.0;
@@ -328,6 +516,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #pragma unroll
         for (int i = 0; i < SEP_NZ; i++) vc[i] = 0.0;
         double kl[SEP_D][SB], ku[SEP_D][SB], kc[CB];
+        double kb = 0.0, vcv = 0.0;
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
@@ -343,8 +532,32 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             for (int c = 0; c < CB; c++) {
                 kc[c] = smu - cds[c] * cdz[c];
                 const double w = -kc[c] * ci[c];
+                if (slk) vcv = fma(-rw.ccv[c], w, vcv);
+                const double wstd = slk ? w * (1.0 - rw.ccv[c]) : w;
 #pragma unroll
-                for (int j = 0; j < 4; j++) vc[j] = fma(rw.cg[c][j], w, vc[j]);
+                for (int j = 0; j < 4; j++) vc[j] = fma(rw.cg[c][j], wstd, vc[j]);
+            }
+            if (slk) {
+                // live rows: sum_a (w_a + D_a vcv / S) g_a in the same pairwise form:
+                //   sum_{a<b} (w_a D_b - D_a w_b)/S (g_a - g_b) + sum_a (w_a D_b' + D_a kb/sb)/S g_a
+                kb = smu - dsb * dzb;
+                vcv = fma(kb, ib, vcv);
+                const double iS = rcp(dS), Db = zb * ib;
+                double wl[CB];
+#pragma unroll
+                for (int a = 0; a < CB; a++) wl[a] = -kc[a] * ci[a] * rw.ccv[a];
+#pragma unroll
+                for (int a = 0; a < CB; a++) {
+                    const double f = fma(wl[a], Db, DcA[a] * kb * ib) * iS;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) vc[j] = fma(rw.cg[a][j], f, vc[j]);
+#pragma unroll
+                    for (int b = a + 1; b < CB; b++) {
+                        const double fab = fma(wl[a], DcA[b], -DcA[a] * wl[b]) * iS;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) vc[j] = fma(rw.cg[a][j] - rw.cg[b][j], fab, vc[j]);
+                    }
+                }
             }
         }
         grp_sum_vec<G, SEP_NZ>(vc);
@@ -356,6 +569,20 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         for (int i = 0; i < SEP_NZ; i++) dy[i] = dya[i] + dyc[i];
         // combined direction: ds from dy; dz = (k - s z - z ds) / s
         double rmax = 0.0;  // largest -ds/s, -dz/z over all sides
+        if (slk) {
+            dv = vcv - (zb * ib) * rb - wv_cost;
+#pragma unroll
+            for (int a = 0; a < CB; a++) {
+                double gd = -cr[a];
+#pragma unroll
+                for (int j = 0; j < 4; j++) gd = fma(rw.cg[a][j], dy[j], gd);
+                dv = fma(DcA[a], gd, dv);
+            }
+            dv *= rcp(dS);
+            dsb = dv + rb;
+            dzb = (kb - sb * zb - zb * dsb) * ib;
+            rmax = fmax(rmax, fmax(-dsb * ib, -dzb * rcp_fast(zb)));
+        }
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
@@ -374,6 +601,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 double td = 0.0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) td = fma(rw.cg[c][j], dy[j], td);
+                if (slk) td -= rw.ccv[c] * dv;
                 cds[c] = cr[c] - td;
                 cdz[c] = (kc[c] - cs[c] * cz[c] - cz[c] * cds[c]) * ci[c];
                 rmax = fmax(rmax, fmax(-cds[c] * ci[c], -cdz[c] * rcp_fast(cz[c])));
@@ -400,11 +628,36 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 cs[c] = fmax(fma(alpha, cds[c], cs[c]), 1e-300);
                 cz[c] = fmax(fma(alpha, cdz[c], cz[c]), 1e-300);
             }
+            if (slk) {
+                v = fma(alpha, dv, v);
+                sb = fmax(fma(alpha, dsb, sb), 1e-300);
+                zb = fmax(fma(alpha, dzb, zb), 1e-300);
+            }
         }
         rd_track *= (1.0 - alpha);
         if (it % 8 == 7) rd_exact = true;
         PSTAMP(11);
+#ifdef MPCCBF_DEBUG_EXIT
+        if (dbg) {  // lane divergence of the iterate (must stay 0: y is group-uniform)
+            double dvg = 0.0;
+#pragma unroll
+            for (int i = 0; i < SEP_NZ; i++) dvg = fmax(dvg, fabs(y[i] - __shfl(y[i], 0, G)));
+            dvg = grp_max<G>(dvg);
+            double* dd = (double*)dbg;
+            if (dvg > 0.0 && dd[15] == 0.0) {
+                dd[14] = dvg;
+                dd[15] = (double)(it + 1);
+            }
+        }
+#endif
     }
+    if (v_out) *v_out = slk ? v : 0.0;
+#ifdef MPCCBF_DEBUG_EXIT
+    if (dbg) {  // per-lane exit iteration (all lanes of a group must agree)
+        const int gl = threadIdx.x & (G - 1);
+        dbg[16 * 64 + gl] = out.iters;  // caller's buffer: + num_agents * 16 slots (see dbg_slack.py)
+    }
+#endif
     return out;
 }
 

@@ -532,7 +532,7 @@ __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict_
             for (int k = 0; k < WNZ; k++) row[k] = (k == i) ? 1.0 : 0.0;
         }
         double L[WNZ], inv_i;
-        if (!chol_rows(row, L, inv_i, sc.M, lane)) return 1e300;
+        if (!chol_rows(row, L, inv_i, sc.M, lane)) break;  // degenerate vertex: the iterate's violation stands
         // rhs: y part -eps y + G^T(wl - wu); t part -1 + sum(wl + wu)
         double b_i = (i < WNZ - 1) ? fma(-eps, vi, rhs_i) : -1.0 + tcorner;
         if (i >= nz && i < WNZ - 1) b_i = 0.0;

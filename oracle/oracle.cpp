@@ -863,12 +863,24 @@ struct Solver {
             for (int i = 0; i < n; i++) rx[i] = -c[i];
             for (int e = 0; e < me; e++) re[e] = be[e];
             kkt(D, P, rx, re, x, lam, 1e-8 * pscale);
+            // variables without curvature (slack variables: linear cost only) come out of the
+            // ridge-regularised start at -c / ridge; pull bounded variables into their bounds
+            for (int i = 0; i < n; i++) {
+                if (!is_neg_inf(qp->vlo[i])) x[i] = std::max(x[i], qp->vlo[i]);
+                if (!is_pos_inf(qp->vhi[i])) x[i] = std::min(x[i], qp->vhi[i]);
+            }
         }
         std::vector<double> s(ns), z(ns);
         for (int k = 0; k < ns; k++) {
             double v = sides[k].sg * (gdot(sides[k], x.data()) - sides[k].b);
             s[k] = std::max(v, 1.0);
             z[k] = 1.0 / s[k];
+            // a lower bound on a variable without curvature (slack variable) carries its linear
+            // cost at the optimum (w - sum_rows z = z_bound): start the dual there
+            if (sides[k].row < 0 && sides[k].sg > 0) {
+                const int i = -sides[k].row - 1;
+                if (P[(size_t)i * n + i] == 0.0 && c[i] > 0.0) z[k] = c[i];
+            }
         }
         lam.assign(me, 0.0);
         std::vector<double> rd(n), re(me), rs(ns), D(ns), rhs(n), nre(me), dsa(ns), dza(ns),
@@ -959,7 +971,7 @@ struct Solver {
             double mua = 0;
             for (int k = 0; k < ns; k++) mua += (s[k] + ap * dsa[k]) * (z[k] + ad * dza[k]);
             mua = ns ? mua / ns : 0;
-            double sigma = (mu > 0) ? std::pow(mua / mu, 3) : 0;
+            double sigma = (mu > 0) ? std::min(1.0, std::pow(mua / mu, 3)) : 0;
             for (int k = 0; k < ns; k++) rc[k] = sigma * mu - s[k] * z[k] - dsa[k] * dza[k];
             solve_dir(rc, dx, dl, ds, dz);
             double amax = 1.0 / 0.99;

@@ -319,3 +319,44 @@ def test_fov_grid_neighbours_match_csr(mpclib):
     np.testing.assert_array_equal(out["status"].cpu().numpy(), g_csr["status"])
     ok = g_csr["status"] == 0
     np.testing.assert_allclose(out["obj"].cpu().numpy()[ok], g_csr["obj"][ok], rtol=1e-10, atol=1e-9)
+
+
+@pytest.mark.parametrize("scale,k_hor", [(0.42, 15), (0.6, 10)])
+def test_slack_mode_matches_oracle(mpclib, scale, k_hor):
+    """slack_mode (ConnectivityIMPCCBF.cpp:73-119, MPCCBFQPGeneratorBase.cpp:28-130): one
+    nonnegative slack per neighbour on its CBF rows, linear cost slack_cost * decay^rank by
+    distance; the kernel eliminates the slacks per lane (Schur complement). A crowded swarm whose
+    plain CBF QPs are partly infeasible solves to optimality, with the oracle's objective (slack
+    cost included) and curve."""
+    torch = _torch()
+    cfg = swarm.config(k_hor, slack_mode=1)
+    states, targets = swarm.lattice_swarm(64, seed=21)
+    states[:, :2] *= scale
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    ctx = mpclib.Context(cfg)
+    assert ctx.kernel_name == "impc_sep_kernel<1,2,slack>"
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    agents = list(range(64))
+    ref = run_oracle(cfg, states, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
+    plain = run_oracle(swarm.config(k_hor), states, targets, rp, col, agents)
+    if scale < 0.5:  # without slack some of these QPs are infeasible; with slack none is
+        assert any(r["status"][0] == O.INFEASIBLE for r in plain)
+    assert np.all(g["status"][:, 0] == O.OPTIMAL)
+
+
+def test_very_crowded_swarm_statuses_match_oracle(mpclib):
+    """Agents 1.5 m apart (below d_min): most QPs are infeasible and their phase-1 LPs end at
+    degenerate vertices where the normal matrix loses its pivots; the certificate still agrees
+    with the oracle's, and the feasible ones match it."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(64, seed=21)
+    states[:, :2] *= 0.3
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    ctx = mpclib.Context(cfg)
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    agents = list(range(64))
+    ref = run_oracle(cfg, states, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
+    assert np.sum(g["status"][:, 0] == O.INFEASIBLE) > 16
