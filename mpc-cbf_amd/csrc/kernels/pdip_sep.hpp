@@ -18,8 +18,11 @@
 
 #include "pdip.hpp"
 
-#ifndef MPCCBF_RELAX
-#define MPCCBF_RELAX 1
+#ifndef MPCCBF_RELAX  // relaxed KKT acceptance at a factorisation breakdown / iteration limit
+#define MPCCBF_RELAX 0  // (off: the parity suite needs neither; costs ~2 us per launch)
+#endif
+#ifndef MPCCBF_SHIFT_RETRY  // re-factor with a diagonal shift after a breakdown (keeps the
+#define MPCCBF_SHIFT_RETRY 0  // accumulators live across the factorisation: ~10 % slower)
 #endif
 
 namespace mpccbf {
@@ -359,49 +362,34 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         // ---- factor: (x, y) 4x4 with the CBF coupling, yaw 2x2
         double Mxy[10], dxy[4], Mw[3], dw[2];
         using S4 = Sym<4>;
-        Mxy[S4::idx(0, 0)] = acc[A_MX + 0] + P[0 * 6 + 0];
-        Mxy[S4::idx(0, 1)] = acc[A_MX + 1] + P[0 * 6 + 1];
-        Mxy[S4::idx(1, 1)] = acc[A_MX + 2] + P[1 * 6 + 1];
-        Mxy[S4::idx(2, 2)] = acc[A_MY + 0] + P[2 * 6 + 2];
-        Mxy[S4::idx(2, 3)] = acc[A_MY + 1] + P[2 * 6 + 3];
-        Mxy[S4::idx(3, 3)] = acc[A_MY + 2] + P[3 * 6 + 3];
-        Mxy[S4::idx(0, 2)] = acc[A_MC + 0];
-        Mxy[S4::idx(0, 3)] = acc[A_MC + 1];
-        Mxy[S4::idx(1, 2)] = acc[A_MC + 2];
-        Mxy[S4::idx(1, 3)] = acc[A_MC + 3];
-        Mw[0] = acc[A_MW + 0] + P[4 * 6 + 4];
-        Mw[1] = acc[A_MW + 1] + P[4 * 6 + 5];
-        Mw[2] = acc[A_MW + 2] + P[5 * 6 + 5];
-        bool ok4, ok2;
-        {
-            double M4[10], M2[3];
-#pragma unroll
-            for (int k = 0; k < 10; k++) M4[k] = Mxy[k];
-#pragma unroll
-            for (int k = 0; k < 3; k++) M2[k] = Mw[k];
+        auto form = [&](double tau) {  // Newton matrix from the reduced accumulators (+ tau I)
+            Mxy[S4::idx(0, 0)] = acc[A_MX + 0] + P[0 * 6 + 0] + tau;
+            Mxy[S4::idx(0, 1)] = acc[A_MX + 1] + P[0 * 6 + 1];
+            Mxy[S4::idx(1, 1)] = acc[A_MX + 2] + P[1 * 6 + 1] + tau;
+            Mxy[S4::idx(2, 2)] = acc[A_MY + 0] + P[2 * 6 + 2] + tau;
+            Mxy[S4::idx(2, 3)] = acc[A_MY + 1] + P[2 * 6 + 3];
+            Mxy[S4::idx(3, 3)] = acc[A_MY + 2] + P[3 * 6 + 3] + tau;
+            Mxy[S4::idx(0, 2)] = acc[A_MC + 0];
+            Mxy[S4::idx(0, 3)] = acc[A_MC + 1];
+            Mxy[S4::idx(1, 2)] = acc[A_MC + 2];
+            Mxy[S4::idx(1, 3)] = acc[A_MC + 3];
+            Mw[0] = acc[A_MW + 0] + P[4 * 6 + 4] + tau;
+            Mw[1] = acc[A_MW + 1] + P[4 * 6 + 5];
+            Mw[2] = acc[A_MW + 2] + P[5 * 6 + 5] + tau;
+        };
+        form(0.0);
+        bool ok4 = chol_packed<4>(Mxy, dxy);
+        bool ok2 = chol_packed<2>(Mw, dw);
+        if (MPCCBF_SHIFT_RETRY && !(ok4 && ok2)) {
+            // a pivot lost to cancellation (active rows' D = z/s ~1e20 against P ~1e5): retry
+            // with a diagonal shift of 1e-12 of the largest diagonal entry (inexact Newton;
+            // residuals and the convergence test stay exact)
+            const double dmax = fmax(fmax(fmax(acc[A_MX + 0] + P[0], acc[A_MX + 2] + P[7]),
+                                          fmax(acc[A_MY + 0] + P[14], acc[A_MY + 2] + P[21])),
+                                     fmax(acc[A_MW + 0] + P[28], acc[A_MW + 2] + P[35]));
+            form(1e-12 * dmax);
             ok4 = chol_packed<4>(Mxy, dxy);
             ok2 = chol_packed<2>(Mw, dw);
-            if (MPCCBF_RELAX && !(ok4 && ok2)) {
-                // a pivot lost to cancellation (active rows' D = z/s ~1e20 against P ~1e5):
-                // retry with a diagonal shift of 1e-12 of the largest diagonal entry (inexact
-                // Newton; residuals and the convergence test stay exact)
-                double dmax = 0.0;
-#pragma unroll
-                for (int i = 0; i < 4; i++) dmax = fmax(dmax, M4[S4::idx(i, i)]);
-#pragma unroll
-                for (int i = 0; i < 2; i++) dmax = fmax(dmax, M2[Sym<2>::idx(i, i)]);
-                const double tau = 1e-12 * dmax;
-#pragma unroll
-                for (int k = 0; k < 10; k++) Mxy[k] = M4[k];
-#pragma unroll
-                for (int k = 0; k < 3; k++) Mw[k] = M2[k];
-#pragma unroll
-                for (int i = 0; i < 4; i++) Mxy[S4::idx(i, i)] += tau;
-#pragma unroll
-                for (int i = 0; i < 2; i++) Mw[Sym<2>::idx(i, i)] += tau;
-                ok4 = chol_packed<4>(Mxy, dxy);
-                ok2 = chol_packed<2>(Mw, dw);
-            }
         }
         if (!(ok4 && ok2)) {
             // Breakdown at a degenerate near-optimal point (D = z/s of the active rows ~1e20
