@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 6
+#define MPCCBF_ABI_VERSION 7
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -217,6 +217,39 @@ const char* mpccbf_kernel_name(const mpccbf_ctx* ctx);
 int mpccbf_build_neighbors(mpccbf_ctx* ctx, const double* states, int32_t num_states,
                            int32_t agent_first, int32_t num_agents, int32_t k, double radius,
                            int32_t* row_ptr, int32_t* col, void* hip_stream);
+
+/* ---- Batched CBF-only controller (FovControl::optimize, cbf/src/controller/FovControl.cpp:17-86)
+ * Per agent: min ||u - u_des||^2 over the control input u (3) subject to the 4 FoV HOCBF rows of
+ * every observed neighbour (FovQPGenerator.cpp:12-115), the velocity CBF rows
+ * u_d <= vmax_d - v_d and -u_d <= v_d - vmin_d (FovCBF.cpp:112-146, linear alpha) and
+ * u_min <= u <= u_max. No context needed; all pointers are device pointers, asynchronous on the
+ * stream. slack_mode is not supported yet (MPCCBF_ERR_INVALID_ARGUMENT). */
+typedef struct mpccbf_fov_control_params {
+    double fov, Ds, Rs;       /* FovCBF(fov, safety_dist, max_dist, ...) */
+    double v_min[3], v_max[3];
+    double u_min[3], u_max[3];
+    int32_t slack_mode;
+    double slack_cost, slack_decay_rate;
+    int32_t max_pdip_iters;   /* default 60 */
+    double tolerance;         /* default 1e-9 */
+} mpccbf_fov_control_params;
+
+typedef struct mpccbf_fov_control_batch {
+    int32_t num_agents;
+    const double* states;      /* num_agents x 6: ego (x, y, yaw, vx, vy, w) */
+    const double* desired_u;   /* num_agents x 3 */
+    const int32_t* nb_row_ptr; /* num_agents + 1: observed neighbours of agent i are */
+    const double* nb_xy;       /* rows nb_row_ptr[i] .. nb_row_ptr[i+1]-1 of nb_xy (x, y) */
+    double* u;                 /* out, num_agents x 3 (NaN when not OPTIMAL) */
+    int32_t* status;           /* out, num_agents (qpcpp::SolveStatus), or NULL */
+    double* obj;               /* out, ||u - u_des||^2, or NULL */
+    int32_t* iters;            /* out, PDIP iterations, or NULL */
+} mpccbf_fov_control_batch;
+
+/* Capacity: 4 * neighbours + 9 <= 64 rows per agent (13 observed neighbours); beyond it the
+ * agent's status is MPCCBF_ERROR. */
+int mpccbf_fov_control_solve(const mpccbf_fov_control_params* p, const mpccbf_fov_control_batch* b,
+                             int32_t device, void* hip_stream);
 
 /* Generic dense QP in the flattened CPLEX form (host pointers; synchronous):
  *   minimise  x^T H x + c^T x + c0        (H symmetric: sum_{i<=j} q_ij x_i x_j, CPLEX.cpp:122-147)

@@ -15,6 +15,7 @@
 #include "host/errors.hpp"
 #include "host/operators.hpp"
 #include "kernels/impc.hpp"
+#include "kernels/cbf_control.hpp"
 
 namespace mpccbf {
 
@@ -489,6 +490,60 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
             }
         }
     }
+    return MPCCBF_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int mpccbf_fov_control_solve(const mpccbf_fov_control_params* p, const mpccbf_fov_control_batch* b,
+                             int32_t device, void* stream) {
+    if (!p || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    if (p->slack_mode)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT,
+                    "FovControl slack_mode is not supported by this build yet (SURVEY.md §8f rank 3)");
+    if (!(p->fov > 0.0) || !(p->Rs > 0.0))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "fov and Rs must be positive");
+    for (int d = 0; d < 3; d++)
+        if (!(p->u_min[d] <= p->u_max[d]) || !(p->v_min[d] <= p->v_max[d]))
+            return fail(MPCCBF_ERR_INVALID_ARGUMENT, "bounds: min must not exceed max");
+    if (b->num_agents < 0) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "num_agents < 0");
+    if (b->num_agents == 0) return MPCCBF_OK;
+    if (!b->states || !b->desired_u || !b->nb_row_ptr || !b->u)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "states, desired_u, nb_row_ptr and u are required");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
+    HIP_TRY(hipSetDevice(device));
+    FovControlArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.num_agents = b->num_agents;
+    a.states = b->states;
+    a.desired_u = b->desired_u;
+    a.nb_row_ptr = b->nb_row_ptr;
+    a.nb_xy = b->nb_xy;
+    a.u = b->u;
+    a.status = b->status;
+    a.obj = b->obj;
+    a.iters = b->iters;
+    a.fov = p->fov;
+    a.Ds = p->Ds;
+    a.Rs = p->Rs;
+    for (int d = 0; d < 3; d++) {
+        a.vmin[d] = p->v_min[d];
+        a.vmax[d] = p->v_max[d];
+        a.umin[d] = p->u_min[d];
+        a.umax[d] = p->u_max[d];
+    }
+    a.maxit = p->max_pdip_iters > 0 ? p->max_pdip_iters : 60;
+    a.tol = p->tolerance > 0.0 ? p->tolerance : 1e-9;
+    a.feas_tol = 1e-6;  // CPLEX's default feasibility tolerance
+    for (int i = 0; i < 9; i++) {
+        a.P[i] = (i % 4 == 0) ? 2.0 : 0.0;  // ||u - u_des||^2 = 1/2 u^T (2 I) u - 2 u_des^T u + c
+        a.LP[i] = (i % 4 == 0) ? std::sqrt(2.0) : 0.0;
+    }
+    HIP_TRY(launch_fov_control(a, (hipStream_t)stream));
     return MPCCBF_OK;
 }
 

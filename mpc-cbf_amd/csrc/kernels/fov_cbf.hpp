@@ -1,0 +1,64 @@
+// fov_cbf.hpp — closed form of the FoV HOCBF rows (FovCBF::init*CBF, FovCBF.cpp:152-535), shared by
+// the FoV MPC kernel (impc_fov.hip) and the batched CBF-only controller (cbf_control.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+namespace mpccbf {
+namespace dev {
+
+// FoV HOCBF rows at ego e against target (tx, ty): closed form of FovCBF::init*CBF with
+// alpha(x) = 0.1 x^5 (see oracle/oracle.cpp fov_rows for the derivation). present = false for
+// the vacuous border rows of a 360-degree field of view.
+__device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double tx, double ty, double fov,
+                                            double Ds, double Rs, double a[3], double& b, bool& present) {
+    constexpr double gamma = 0.1;
+    const double vx = e[3], vy = e[4], w = e[5];
+    const double dx = tx - e[0], dy = ty - e[1];
+    double sn, cs;
+    sincos(e[2], &sn, &cs);
+    const double rx = cs * dx + sn * dy, ry = -sn * dx + cs * dy;
+    double bval, lf2;
+    present = true;
+    if (kind == 0 || kind == 3) {
+        const double sgn = kind == 0 ? 1.0 : -1.0;  // safety: |d|^2 - Ds^2, range: Rs^2 - |d|^2
+        a[0] = -2.0 * sgn * dx;
+        a[1] = -2.0 * sgn * dy;
+        a[2] = 0.0;
+        bval = kind == 0 ? dx * dx + dy * dy - Ds * Ds : Rs * Rs - dx * dx - dy * dy;
+        lf2 = 2.0 * sgn * (vx * vx + vy * vy);
+    } else {
+        double kap, sig;
+        const bool left = kind == 1;
+        if (fov < M_PI) {
+            kap = tan(0.5 * fov);
+            sig = left ? 1.0 : -1.0;
+        } else if (fov == M_PI) {
+            kap = 1.0;
+            sig = 0.0;
+        } else if (fabs(fov - 2.0 * M_PI) <= 1e-9 * 2.0 * M_PI) {
+            a[0] = a[1] = a[2] = 0.0;
+            b = 1.7976931348623157e308;
+            present = false;
+            return;
+        } else {
+            kap = tan(0.5 * (2.0 * M_PI - fov));
+            sig = left ? -1.0 : 1.0;
+        }
+        bval = kap * rx + sig * ry;
+        a[0] = -kap * cs + sig * sn;
+        a[1] = -kap * sn - sig * cs;
+        a[2] = kap * ry - sig * rx;
+        lf2 = 2.0 * w * ((kap * sn + sig * cs) * vx + (-kap * cs + sig * sn) * vy) - w * w * bval;
+    }
+    const double lf = a[0] * vx + a[1] * vy + a[2] * w;
+    const double b2 = bval * bval, b4 = b2 * b2;
+    const double psi = lf + gamma * b4 * bval;
+    const double p2 = psi * psi;
+    b = lf2 + 5.0 * gamma * b4 * lf + gamma * p2 * p2 * psi;
+}
+
+}  // namespace dev
+}  // namespace mpccbf

@@ -367,6 +367,46 @@ def dense_qp_solve_batch(qps):
 COMM_ID_BYTES = 128
 
 
+class FovControlParams(C.Structure):
+    _fields_ = [("fov", C.c_double), ("Ds", C.c_double), ("Rs", C.c_double),
+                ("v_min", C.c_double * 3), ("v_max", C.c_double * 3),
+                ("u_min", C.c_double * 3), ("u_max", C.c_double * 3),
+                ("slack_mode", C.c_int32), ("slack_cost", C.c_double),
+                ("slack_decay_rate", C.c_double), ("max_pdip_iters", C.c_int32),
+                ("tolerance", C.c_double)]
+
+
+class FovControlBatch(C.Structure):
+    _fields_ = [("num_agents", C.c_int32), ("states", C.c_void_p), ("desired_u", C.c_void_p),
+                ("nb_row_ptr", C.c_void_p), ("nb_xy", C.c_void_p), ("u", C.c_void_p),
+                ("status", C.c_void_p), ("obj", C.c_void_p), ("iters", C.c_void_p)]
+
+
+def fov_control_params(cfg: dict) -> FovControlParams:
+    """FovControl parameters from a config dict: fov_beta / fov_Ds / fov_Rs, v_min / v_max and the
+    control bounds u_min / u_max (default: the acceleration bounds a_min / a_max)."""
+    p = FovControlParams()
+    p.fov, p.Ds, p.Rs = cfg["fov_beta"], cfg["fov_Ds"], cfg["fov_Rs"]
+    for d in range(3):
+        p.v_min[d], p.v_max[d] = cfg["v_min"][d], cfg["v_max"][d]
+        p.u_min[d] = cfg.get("u_min", cfg["a_min"])[d]
+        p.u_max[d] = cfg.get("u_max", cfg["a_max"])[d]
+    p.slack_mode = int(cfg.get("control_slack_mode", 0))
+    p.slack_cost = cfg.get("slack_cost", 0.0)
+    p.slack_decay_rate = cfg.get("slack_decay_rate", 1.0)
+    return p
+
+
+def fov_control_solve(cfg: dict, states, desired_u, nb_row_ptr, nb_xy, u, status=None, obj=None,
+                      iters=None, device: int = 0, stream=None):
+    """Batched FovControl::optimize (mpccbf_fov_control_solve): device tensors in, u out."""
+    b = FovControlBatch(num_agents=states.shape[0], states=_ptr(states), desired_u=_ptr(desired_u),
+                        nb_row_ptr=_ptr(nb_row_ptr), nb_xy=_ptr(nb_xy), u=_ptr(u),
+                        status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters))
+    p = fov_control_params(cfg)
+    _check(load().mpccbf_fov_control_solve(C.byref(p), C.byref(b), device, _stream(stream)))
+
+
 def comm_unique_id() -> bytes:
     """RCCL unique id (mpccbf_comm_unique_id), created on one rank and shared with the others."""
     buf = C.create_string_buffer(COMM_ID_BYTES)

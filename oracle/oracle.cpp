@@ -1425,6 +1425,57 @@ int64_t orc_impc_batch(const orc_params* p, int32_t N, const double* states, con
     return solved.load();
 }
 
+int orc_fov_control(double fov, double Ds, double Rs, const double* vmin3, const double* vmax3,
+                    const double* umin3, const double* umax3, const double* st,
+                    const double* ud, int32_t nb, const double* nb_xy, double* u_out,
+                    double* obj_out) {
+    try {
+        orc::DenseQP q;
+        q.n = 3;
+        // addDesiredControlCost (CBFQPGeneratorBase.cpp:36-57): I, -2 u_des, |u_des|^2
+        q.H.assign(9, 0.0);
+        q.c.assign(3, 0.0);
+        for (int d = 0; d < 3; d++) {
+            q.H[d * 3 + d] = 1.0;
+            q.c[d] = -2.0 * ud[d];
+            q.c0 += ud[d] * ud[d];
+        }
+        auto add_row = [&](const double* g, double hi) {
+            for (int d = 0; d < 3; d++) q.A.push_back(g[d]);
+            q.lo.push_back(-std::numeric_limits<double>::max());
+            q.hi.push_back(hi);
+            q.m++;
+        };
+        for (int i = 0; i < nb; i++) {  // safety, left border, right border, range (:58-68)
+            orc::FovRow fr[4];
+            orc::fov_rows(st, nb_xy + 2 * i, fov, Ds, Rs, fr);
+            for (int r = 0; r < 4; r++) {
+                if (!fr[r].present) continue;  // 360-degree FoV: no border rows
+                const double g[3] = {-fr[r].a[0], -fr[r].a[1], -fr[r].a[2]};
+                add_row(g, fr[r].b);
+            }
+        }
+        for (int d = 0; d < 3; d++) {  // addMinVelConstraints: -(+e_d) u <= v_d - vmin_d
+            double g[3] = {0, 0, 0};
+            g[d] = -1.0;
+            add_row(g, st[3 + d] - vmin3[d]);
+        }
+        for (int d = 0; d < 3; d++) {  // addMaxVelConstraints: -(-e_d) u <= vmax_d - v_d
+            double g[3] = {0, 0, 0};
+            g[d] = 1.0;
+            add_row(g, vmax3[d] - st[3 + d]);
+        }
+        q.vlo.assign(umin3, umin3 + 3);
+        q.vhi.assign(umax3, umax3 + 3);
+        orc::Solution r = orc::solve(q);
+        for (int d = 0; d < 3; d++) u_out[d] = r.x.size() == 3 ? r.x[d] : 0.0;
+        if (obj_out) *obj_out = r.obj;
+        return r.status;
+    } catch (...) {
+        return ORC_ERROR;
+    }
+}
+
 int orc_eval_curve(const orc_params* p, const double* x, double t, int32_t d, double* out3) {
     try {
         orc::Assembler as(p, 0);

@@ -123,6 +123,16 @@ int64_t orc_impc_batch(const orc_params* p, int32_t num_agents, const double* st
 
 /* Curve evaluation of a solution vector (SingleParameterPiecewiseCurve::eval,
  * splines/src/curves/SingleParameterPiecewiseCurve.cpp:94-127): out3 = d-th derivative at t. */
+/* FovControl::optimize (cbf/src/controller/FovControl.cpp:17-86), non-slack: the CBF-only QP
+ * min ||u - u_des||^2 over u (3) s.t. per observed neighbour the 4 FoV rows -a^T u <= b
+ * (FovQPGenerator.cpp:12-115), the velocity CBF rows u_i <= vmax_i - v_i and
+ * -u_i <= v_i - vmin_i (FovCBF.cpp:112-146, 543-574, linear alpha), and the variable bounds
+ * u_min <= u <= u_max (CBFQPGeneratorBase.cpp:75-91). Returns the qpcpp status; u_out gets the
+ * solution (or the solver's last iterate), obj_out the objective with its constant. */
+int orc_fov_control(double fov, double Ds, double Rs, const double* vmin3, const double* vmax3,
+                    const double* umin3, const double* umax3, const double* state6,
+                    const double* desired_u3, int32_t num_neighbors, const double* nb_xy,
+                    double* u_out3, double* obj_out);
 int orc_eval_curve(const orc_params* p, const double* x, double t, int32_t deriv, double* out3);
 
 #ifdef __cplusplus

@@ -79,6 +79,8 @@ def lib():
         L.orc_apply_input.argtypes = [C.c_double, dp, dp, dp]
         L.orc_fov_cbf.argtypes = [dp, dp, C.c_double, C.c_double, C.c_double, dp, dp, ip]
         L.orc_prediction_matrices.argtypes = [C.c_double, C.c_int32, dp, dp]
+        L.orc_fov_control.argtypes = [C.c_double, C.c_double, C.c_double, dp, dp, dp, dp, dp, dp,
+                                      C.c_int32, dp, dp, dp]
         L.orc_num_vars.argtypes = [C.POINTER(OrcParams), C.c_int32]
         L.orc_assemble_qp.argtypes = [C.POINTER(OrcParams), dp, dp, C.c_int32, dp, dp, C.c_int32,
                                       dp, C.c_int32, dp, dp, dp, dp, dp, dp, dp, dp]
@@ -227,6 +229,22 @@ def fov_cbf(state, target, fov, Ds, Rs):
     pr = np.zeros(4, dtype=np.int32)
     lib().orc_fov_cbf(_d(st), _d(tg), fov, Ds, Rs, _d(a), _d(b), pr.ctypes.data_as(C.POINTER(C.c_int32)))
     return a.reshape(4, 3), b, pr
+
+
+def fov_control(cfg: dict, state, desired_u, nb_xy):
+    """FovControl::optimize restated (non-slack): (status, u (3,), objective incl. constant)."""
+    f = lambda v: np.ascontiguousarray(v, dtype=np.float64)  # noqa: E731
+    umin = cfg.get("u_min", cfg["a_min"])
+    umax = cfg.get("u_max", cfg["a_max"])
+    nb = np.ascontiguousarray(np.reshape(nb_xy, (-1, 2)), dtype=np.float64)
+    u = np.zeros(3)
+    obj = np.zeros(1)
+    vmin, vmax, umin, umax, st, ud = (f(cfg["v_min"]), f(cfg["v_max"]), f(umin), f(umax), f(state),
+                                      f(desired_u))
+    stt = lib().orc_fov_control(cfg["fov_beta"], cfg["fov_Ds"], cfg["fov_Rs"], _d(vmin), _d(vmax),
+                                _d(umin), _d(umax), _d(st), _d(ud), len(nb),
+                                _d(nb) if len(nb) else None, _d(u), _d(obj))
+    return stt, u, float(obj[0])
 
 
 def eval_curve(p: OrcParams, x, t, d):
