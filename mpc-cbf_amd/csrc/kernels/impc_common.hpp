@@ -55,45 +55,55 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
     const GridArgs& gr = args.grid;
     const long long cx = (long long)floor(px * gr.inv_cell), cy = (long long)floor(py * gr.inv_cell);
     const double r2 = gr.radius * gr.radius;
-    uint32_t hs[9], b0[9], b1[9];
+    // the 9 cells' buckets (a bucket reached from two cells is scanned once), concatenated: lane
+    // gl takes candidates gl, gl + G, ... of the whole list, so the dependent loads (bucket entry,
+    // then the agent's position) of all cells are in flight together
+    uint32_t hs[9], b0[9], nc[9];
 #pragma unroll
     for (int c = 0; c < 9; c++) {
         hs[c] = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
         b0[c] = gr.start[hs[c]];
-        b1[c] = gr.start[hs[c] + 1];
+        nc[c] = gr.start[hs[c] + 1] - b0[c];
     }
-    int cnt = 0;
+    uint32_t off[9], total = 0;
 #pragma unroll
     for (int c = 0; c < 9; c++) {
         bool dup = false;
 #pragma unroll
         for (int p = 0; p < c; p++) dup = dup || (hs[p] == hs[c]);
-        if (dup) continue;
-        for (uint32_t base = b0[c]; base < b1[c]; base += G) {
-            const uint32_t e = base + gl;
-            bool keep = false;
-            int j = -1;
-            double d2 = 0.0;
-            if (e < b1[c]) {
-                j = (int)gr.sorted[e];
-                const double ex = args.states[(size_t)j * 6] - px;
-                const double ey = args.states[(size_t)j * 6 + 1] - py;
-                d2 = ex * ex + ey * ey;
-                keep = (j != self) && (d2 <= r2);
-                if (keep && gr.cone > 0.0) {  // inside the field of view (strict)
-                    double off = atan2(ey, ex) - yaw;
-                    off -= 6.283185307179586 * rint(off * 0.15915494309189535);
-                    keep = fabs(off) < gr.cone;
-                }
+        if (dup) nc[c] = 0;
+        off[c] = total;
+        total += nc[c];
+    }
+    int cnt = 0;
+    for (uint32_t t0 = 0; t0 < total; t0 += G) {
+        const uint32_t t = t0 + gl;
+        bool keep = false;
+        int j = -1;
+        double d2 = 0.0;
+        if (t < total) {
+            uint32_t e = 0;
+#pragma unroll
+            for (int c = 0; c < 9; c++)  // last cell whose range starts at or before t
+                if (off[c] <= t && t - off[c] < nc[c]) e = b0[c] + (t - off[c]);
+            j = (int)gr.sorted[e];
+            const double ex = args.states[(size_t)j * 6] - px;
+            const double ey = args.states[(size_t)j * 6 + 1] - py;
+            d2 = ex * ex + ey * ey;
+            keep = (j != self) && (d2 <= r2);
+            if (keep && gr.cone > 0.0) {  // inside the field of view (strict)
+                double offa = atan2(ey, ex) - yaw;
+                offa -= 6.283185307179586 * rint(offa * 0.15915494309189535);
+                keep = fabs(offa) < gr.cone;
             }
-            const unsigned long long msk = grp_ballot<G>(keep);
-            const int slot = cnt + __popcll(msk & ((1ull << gl) - 1ull));
-            if (keep && slot < NB_CAP) {
-                sc.idx[slot] = j;
-                sc.d2[slot] = d2;
-            }
-            cnt += __popcll(msk);
         }
+        const unsigned long long msk = grp_ballot<G>(keep);
+        const int slot = cnt + __popcll(msk & ((1ull << gl) - 1ull));
+        if (keep && slot < NB_CAP) {
+            sc.idx[slot] = j;
+            sc.d2[slot] = d2;
+        }
+        cnt += __popcll(msk);
     }
     if (cnt > NB_CAP) return -1;
     wave_lds_sync();
