@@ -123,5 +123,64 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Value of lane k (0..15) of this lane's 16-lane row (DPP row_newbcast; k folds to a constant
+// after unrolling).
+template <int K>
+__device__ __forceinline__ double row_bcast_k(double v) {
+    return dpp_mov<0x150 + K>(v);
+}
+__device__ __forceinline__ double row_bcast(int k, double v) {
+    switch (k & 15) {
+        case 0: return row_bcast_k<0>(v);
+        case 1: return row_bcast_k<1>(v);
+        case 2: return row_bcast_k<2>(v);
+        case 3: return row_bcast_k<3>(v);
+        case 4: return row_bcast_k<4>(v);
+        case 5: return row_bcast_k<5>(v);
+        case 6: return row_bcast_k<6>(v);
+        case 7: return row_bcast_k<7>(v);
+        case 8: return row_bcast_k<8>(v);
+        case 9: return row_bcast_k<9>(v);
+        case 10: return row_bcast_k<10>(v);
+        case 11: return row_bcast_k<11>(v);
+        case 12: return row_bcast_k<12>(v);
+        case 13: return row_bcast_k<13>(v);
+        case 14: return row_bcast_k<14>(v);
+        default: return row_bcast_k<15>(v);
+    }
+}
+
+// The same all-reduce through LDS (16-lane groups of one wave, G = 16): every lane writes its N
+// values as one row of a padded 16 x (N + 1) table (odd row stride: the column reads hit distinct
+// banks), lane c sums column c (and c + 16), and the totals return by DPP row broadcasts. One LDS
+// round trip plus N broadcasts against the 4N DPP moves and adds of grp_sum_vec.
+// red: per-group scratch of 16 * (N + 1) doubles, private to the group.
+template <int N>
+__device__ __forceinline__ void grp_sum_vec_lds(double (&v)[N], double* __restrict__ red, int gl) {
+    static_assert(N <= 32, "two columns per lane at most");
+    constexpr int S = N + 1;
+#pragma unroll
+    for (int k = 0; k < N; k++) red[gl * S + k] = v[k];
+    wave_lds_sync();
+    double col[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int c = 16 * h + gl;
+        if (16 * h < N && c < N) {
+            double p[16];
+#pragma unroll
+            for (int l = 0; l < 16; l++) p[l] = red[l * S + c];
+#pragma unroll
+            for (int w = 8; w >= 1; w >>= 1)
+#pragma unroll
+                for (int l = 0; l < w; l++) p[l] += p[l + w];
+            col[h] = p[0];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < N; k++) v[k] = row_bcast(k, col[k >> 4]);
+    wave_lds_sync();  // the table is reused by the next reduction
+}
+
 }  // namespace dev
 }  // namespace mpccbf

@@ -252,6 +252,7 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
 
     __shared__ double stage_all[GPB][SLACK ? 1 : cap * (NZ + 1)];
     double* stage = stage_all[gib];
+    __shared__ double red_all[GPB][16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
 
     const int self = args.agent_first + ai;
     double s0[6];
@@ -346,7 +347,7 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
             long long* dbg = nullptr;
 #endif
             const PdipOut po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr),
-                                                                q, y, cfg, dbg, wslack, &vslack);
+                                                                q, y, cfg, dbg, wslack, &vslack, red_all[gib]);
             st = po.status;
             nit = po.iters;
             if (st != ST_OPTIMAL) {

@@ -80,7 +80,7 @@ template <int G, int SB, int CB, bool SLACK = false>
 __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                                   const double* __restrict__ LP, const double (&q)[SEP_NZ],
                                   double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg = nullptr,
-                                  double wv_cost = 0.0, double* v_out = nullptr) {
+                                  double wv_cost = 0.0, double* v_out = nullptr, double* red = nullptr) {
     (void)dbg;
     const bool slk = SLACK && has_cbf;  // group-uniform
     // slack variable, its bound's slack and dual; the dual starts at the linear cost it carries at
@@ -249,7 +249,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 rp = fmax(rp, fabs(rb));
             }
             PSTAMP(1);
-            grp_sum_vec<G, A_N>(acc);
+            if (red) grp_sum_vec_lds<A_N>(acc, red, threadIdx.x & (G - 1));
+            else grp_sum_vec<G, A_N>(acc);
 #ifdef MPCCBF_DEBUG_EXIT
             if (dbg) {  // is the reduced accumulator group-uniform?
                 double dvg = 0.0;
@@ -271,7 +272,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #pragma unroll
             for (int k = A_RHS; k < A_N; k++) part[k - 4] = acc[k];
             PSTAMP(1);
-            grp_sum_vec<G, A_N - 4>(part);
+            if (red) grp_sum_vec_lds<A_N - 4>(part, red, threadIdx.x & (G - 1));
+            else grp_sum_vec<G, A_N - 4>(part);
 #pragma unroll
             for (int k = 0; k < A_MC; k++) acc[k] = part[k];
 #pragma unroll
@@ -548,7 +550,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 }
             }
         }
-        grp_sum_vec<G, SEP_NZ>(vc);
+        grp_sum_vec<G, SEP_NZ>(vc);  // (6 values: the DPP butterfly beats the LDS round trip)
         PSTAMP(8);
         double dyc[SEP_NZ], dy[SEP_NZ];
         sep_solve(Mxy, dxy, Mw, dw, vc, dyc);
