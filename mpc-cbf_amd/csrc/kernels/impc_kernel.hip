@@ -410,8 +410,8 @@ static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const I
 const char* impc_kernel_name(const DevOps& op, int variant) {
     if (op.slack_mode)  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2
         return (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
-                   ? "impc_sep_kernel<1,2,slack>" : nullptr;
-    if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1>";
+                   ? "impc_sep_kernel<1,2,true>" : nullptr;
+    if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false>";
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
         if (variant == 1 && op.m < 64) return "impc_kernel<6,64,1>";

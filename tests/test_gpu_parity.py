@@ -334,7 +334,7 @@ def test_slack_mode_matches_oracle(mpclib, scale, k_hor):
     states[:, :2] *= scale
     rp, col = swarm.knn_csr(states, 8, 6.0)
     ctx = mpclib.Context(cfg)
-    assert ctx.kernel_name == "impc_sep_kernel<1,2,slack>"
+    assert ctx.kernel_name == "impc_sep_kernel<1,2,true>"
     g = run_gpu(ctx, states, targets, rp, col, torch)
     agents = list(range(64))
     ref = run_oracle(cfg, states, targets, rp, col, agents)
