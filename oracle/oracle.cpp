@@ -504,7 +504,7 @@ struct Assembler {
                 acc.addCostAddition(vars, quad.data(), zero.data(), 0);
             }
         }
-        // addSlackCost (MPCCBFQPGeneratorBase.cpp:473-488): plain addLinearTerm, no drop
+        // addSlackCost (MPCCBFQPGeneratorBase.cpp:121-130): plain addLinearTerm, no drop
         if (nslack > 0)
             for (int i = 0; i < nslack; i++) acc.lin[slack_vars[i]] += slack_w[i];
 
@@ -556,7 +556,6 @@ struct Assembler {
             addRow(qp, row, LOWEST, b + 0.0);     // slack_value = 0 (:138, :172)
         };
         if (p->cbf_mode == 1) {
-            if (nslack > 0) throw std::runtime_error("FoV slack mode not supported");
             // Voronoi rows on every control point of piece 0 (FovBezierIMPCCBF.cpp:130-147 ->
             // BezierQPOperations::hyperplaneConstraintAll :270-285, epsilon 1e-8)
             for (int i = 0; i < nb; i++) {
@@ -570,13 +569,17 @@ struct Assembler {
             }
             // FoV CBF rows: iter 0 at the current state (:150-171), later iterations at the
             // predicted states, per neighbour all k of one kind, then the next kind (:172-210)
-            auto fov_row = [&](const FovRow& fr, int k) {
+            // slack mode: every FoV row of neighbour i carries -1 on slack variable i
+            // (FovMPCCBFQPGenerator.cpp:110-207 *WithSlackVariables, slack_coefficients(i) = -1);
+            // the Voronoi rows above never do
+            auto fov_row = [&](const FovRow& fr, int k, int nbi) {
                 zero_row();
                 for (int j = 0; j < nc; j++) {
                     double sum = 0;
                     for (int d = 0; d < DIM; d++) sum += fr.a[d] * U[(k * DIM + d) * nc + j];
                     row[j] = -1.0 * sum;
                 }
+                if (nslack > 0) row[nc + nbi] = -1.0;
                 addRow(qp, row, LOWEST, fr.b + 0.0);
             };
             for (int i = 0; i < nb; i++) {
@@ -584,13 +587,13 @@ struct Assembler {
                 if (iter == 0) {
                     FovRow fr[4];
                     fov_rows(st, tg, p->fov_beta, p->fov_Ds, p->fov_Rs, fr);
-                    for (int r = 0; r < 4; r++) fov_row(fr[r], 0);
+                    for (int r = 0; r < 4; r++) fov_row(fr[r], 0, i);
                 } else {
                     std::vector<std::array<FovRow, 4>> per_k(p->cbf_horizon);
                     for (int k = 0; k < p->cbf_horizon; k++)
                         fov_rows(pred + 6 * k, tg, p->fov_beta, p->fov_Ds, p->fov_Rs, per_k[k].data());
                     for (int r = 0; r < 4; r++)
-                        for (int k = 0; k < p->cbf_horizon; k++) fov_row(per_k[k][r], k);
+                        for (int k = 0; k < p->cbf_horizon; k++) fov_row(per_k[k][r], k, i);
                 }
             }
         } else if (iter == 0) {
@@ -1194,16 +1197,64 @@ Solution solve(const DenseQP& q_in) {
     return out;
 }
 
-// ConnectivityIMPCCBF::optimize (mpc_cbf/src/controller/ConnectivityIMPCCBF.cpp:47-215)
+// FovBezierIMPCCBF::distanceToEllipse (mpc_cbf/src/controller/FovBezierIMPCCBF.cpp:226-280):
+// signed distance from the robot to the point of the 90 % confidence ellipse (s = 4.605) of the
+// target estimate at parametric angle (slope - theta), negative inside. cov = (cxx, cxy, cyy),
+// the 2x2 position block (:144-145). The reference diagonalises with Eigen::EigenSolver; the
+// result is invariant to the eigenpair order and eigenvector signs (a, b are swapped to
+// a >= b, theta is the major axis angle, and every term is a product of two sign flips), so the
+// closed-form symmetric 2x2 eigen-decomposition stands in for it.
+double distance_to_ellipse(const double* robot, const double* mean, const double* cov) {
+    if (std::isinf(cov[0])) return -5.0;  // (:229, :279)
+    const double cxx = cov[0], cxy = cov[1], cyy = cov[2];
+    const double hm = 0.5 * (cxx + cyy), hd = 0.5 * (cxx - cyy);
+    const double rt = std::sqrt(hd * hd + cxy * cxy);
+    const double lmax = hm + rt, lmin = hm - rt;
+    const double s = 4.605;
+    const double a = std::sqrt(s * lmax), b = std::sqrt(s * lmin);  // a >= b (:238-246)
+    // major-axis direction: eigenvector of lmax (:248-258); any sign / pi shift is equivalent
+    double theta = 0.0;
+    if (rt > 0.0) theta = 0.5 * std::atan2(2.0 * cxy, cxx - cyy);
+    if (theta < 0.0) theta += M_PI;
+    const double slope = std::atan2(-mean[1] + robot[1], -mean[0] + robot[0]);
+    const double xn = mean[0] + a * std::cos(slope - theta) * std::cos(theta) -
+                      b * std::sin(slope - theta) * std::sin(theta);
+    const double yn = mean[1] + a * std::cos(slope - theta) * std::sin(theta) +
+                      b * std::sin(slope - theta) * std::cos(theta);
+    const double dist = std::sqrt(std::pow(xn - robot[0], 2) + std::pow(yn - robot[1], 2));
+    if (std::isnan(dist)) return 5.0;  // (:266-269)
+    const double d = std::sqrt(std::pow(mean[0] - robot[0], 2) + std::pow(mean[1] - robot[1], 2));
+    const double range = std::sqrt(std::pow(mean[0] - xn, 2) + std::pow(mean[1] - yn, 2));
+    return d < range ? -dist : dist;  // (:271-277)
+}
+
+// ConnectivityIMPCCBF::optimize (mpc_cbf/src/controller/ConnectivityIMPCCBF.cpp:47-215), and
+// FovBezierIMPCCBF::optimize (FovBezierIMPCCBF.cpp:48-223) when p->cbf_mode == 1.
+// covs: num_states x 3 position covariances (cxx, cxy, cyy) of the neighbour estimates (FoV slack
+// weights only), or nullptr = unknown (infinite: distanceToEllipse returns -5 for every one).
 int impc(const orc_params* p, int N, const double* states, int self, int nb, const int* nbidx,
-         const double* ref, int* status, double* obj, double* x, int* qp_iters) {
+         const double* ref, int* status, double* obj, double* x, int* qp_iters,
+         const double* covs = nullptr) {
     Assembler as(p, nb);
     const double* st = states + 6 * self;
     std::vector<double> nbs(6 * nb);
     for (int i = 0; i < nb; i++) std::memcpy(&nbs[6 * i], states + 6 * nbidx[i], 6 * sizeof(double));
     // slack weights (:73-100): sort by planar distance, w * decay^rank
     std::vector<double> sw(nb, 0.0);
-    if (p->slack_mode) {
+    if (p->slack_mode && p->cbf_mode == 1) {
+        // FovBezierIMPCCBF.cpp:58-81: sort by distanceToEllipse (compareDist, :283-288), then the
+        // weight of neighbour i is w * decay^{idx[i]} — the sorted position's index, not the rank
+        // of i (reference quirk, kept). Ties keep the list order (std::sort is an insertion sort
+        // below 17 elements in libstdc++; the batch path allows at most 16 neighbours).
+        const double inf_cov[3] = {INFINITY, 0.0, INFINITY};
+        std::vector<double> de(nb);
+        for (int i = 0; i < nb; i++)
+            de[i] = distance_to_ellipse(st, &nbs[6 * i], covs ? covs + 3 * (size_t)nbidx[i] : inf_cov);
+        std::vector<size_t> idx(nb);
+        std::iota(idx.begin(), idx.end(), 0);
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return de[a] < de[b]; });
+        for (int i = 0; i < nb; i++) sw[i] = p->slack_cost * std::pow(p->slack_decay_rate, (double)idx[i]);
+    } else if (p->slack_mode) {
         std::vector<size_t> idx(nb);
         std::iota(idx.begin(), idx.end(), 0);
         std::vector<double> dist(nb);
@@ -1385,6 +1436,24 @@ int orc_impc_optimize(const orc_params* p, int32_t N, const double* states, int3
     } catch (...) {
         return -1;
     }
+}
+
+int orc_impc_optimize_cov(const orc_params* p, int32_t N, const double* states, int32_t self,
+                          int32_t nb, const int32_t* nbidx, const double* ref, const double* covs,
+                          int32_t* status, double* obj, double* x, int32_t* qp_iters) {
+    try {
+        for (int i = 0; i < p->impc_iter; i++) {
+            status[i] = ORC_UNKNOWN;
+            obj[i] = std::numeric_limits<double>::quiet_NaN();
+        }
+        return orc::impc(p, N, states, self, nb, nbidx, ref, status, obj, x, qp_iters, covs);
+    } catch (...) {
+        return -1;
+    }
+}
+
+double orc_distance_to_ellipse(const double* robot2, const double* mean2, const double* cov3) {
+    return orc::distance_to_ellipse(robot2, mean2, cov3);
 }
 
 int64_t orc_impc_batch(const orc_params* p, int32_t N, const double* states, const double* refs,

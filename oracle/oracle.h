@@ -112,6 +112,16 @@ int orc_impc_optimize(const orc_params* p, int32_t num_agents, const double* sta
                       const double* ref, int32_t* status, double* obj, double* x,
                       int32_t* qp_iters);
 
+/* orc_impc_optimize with the neighbour covariances of FovBezierIMPCCBF::optimize
+ * (FovBezierIMPCCBF.cpp:48-81; used for the slack weights only): covs = num_agents x 3
+ * (cxx, cxy, cyy) indexed like states, or NULL (unknown: every distance is -5). */
+int orc_impc_optimize_cov(const orc_params* p, int32_t num_agents, const double* states,
+                          int32_t self_idx, int32_t num_neighbors, const int32_t* neighbor_idx,
+                          const double* ref, const double* covs, int32_t* status, double* obj,
+                          double* x, int32_t* qp_iters);
+/* FovBezierIMPCCBF::distanceToEllipse (FovBezierIMPCCBF.cpp:226-280); cov3 = (cxx, cxy, cyy) */
+double orc_distance_to_ellipse(const double* robot2, const double* mean2, const double* cov3);
+
 /* Batched CPU baseline: agents [first, first+count) with neighbor CSR (row_ptr, col).
  * nthreads worker threads, one agent per task (CPLEX Threads=1 per solve, CPLEX.cpp:158).
  * x_last: n per agent (solution of the last OPTIMAL iteration). Returns total QPs solved. */

@@ -88,6 +88,10 @@ def lib():
                                          dp, dp, dp, ip, dp]
         L.orc_impc_optimize.argtypes = [C.POINTER(OrcParams), C.c_int32, dp, C.c_int32, C.c_int32,
                                         ip, dp, ip, dp, dp, ip]
+        L.orc_impc_optimize_cov.argtypes = [C.POINTER(OrcParams), C.c_int32, dp, C.c_int32,
+                                            C.c_int32, ip, dp, dp, ip, dp, dp, ip]
+        L.orc_distance_to_ellipse.restype = C.c_double
+        L.orc_distance_to_ellipse.argtypes = [dp, dp, dp]
         L.orc_impc_batch.restype = C.c_int64
         L.orc_impc_batch.argtypes = [C.POINTER(OrcParams), C.c_int32, dp, dp, ip, ip, C.c_int32,
                                      C.c_int32, C.c_int32, ip, dp, dp]
@@ -183,7 +187,14 @@ def solve_dense_qp(qp):
     return dict(status=st, x=x, obj=float(obj[0]), iters=int(iters[0]), kkt=kkt)
 
 
-def impc_optimize(p: OrcParams, states, self_idx, neighbor_idx, ref):
+def distance_to_ellipse(robot, mean, cov3):
+    """FovBezierIMPCCBF::distanceToEllipse; cov3 = (cxx, cxy, cyy)."""
+    return lib().orc_distance_to_ellipse(_d(robot), _d(mean), _d(cov3))
+
+
+def impc_optimize(p: OrcParams, states, self_idx, neighbor_idx, ref, covs=None):
+    """One agent's IMPC optimize; covs (num_states x 3: cxx, cxy, cyy) feeds the FoV slack
+    weights (FovBezierIMPCCBF.cpp:58-81), None = unknown covariances."""
     states = np.ascontiguousarray(states, dtype=np.float64)
     nbi = np.ascontiguousarray(neighbor_idx, dtype=np.int32)
     nb = len(nbi)
@@ -194,10 +205,12 @@ def impc_optimize(p: OrcParams, states, self_idx, neighbor_idx, ref):
     x = np.zeros((it_n, n))
     qi = np.zeros(it_n, dtype=np.int32)
     rf = np.ascontiguousarray(ref, dtype=np.float64)
-    att = lib().orc_impc_optimize(C.byref(p), len(states), _d(states), self_idx, nb,
-                                  nbi.ctypes.data_as(C.POINTER(C.c_int32)) if nb else None,
-                                  _d(rf), status.ctypes.data_as(C.POINTER(C.c_int32)), _d(obj),
-                                  _d(x), qi.ctypes.data_as(C.POINTER(C.c_int32)))
+    cv = None if covs is None else np.ascontiguousarray(covs, dtype=np.float64)
+    att = lib().orc_impc_optimize_cov(C.byref(p), len(states), _d(states), self_idx, nb,
+                                      nbi.ctypes.data_as(C.POINTER(C.c_int32)) if nb else None,
+                                      _d(rf), None if cv is None else _d(cv),
+                                      status.ctypes.data_as(C.POINTER(C.c_int32)), _d(obj),
+                                      _d(x), qi.ctypes.data_as(C.POINTER(C.c_int32)))
     if att < 0:
         raise RuntimeError("orc_impc_optimize failed")
     return dict(attempted=att, status=status, obj=obj, x=x, qp_iters=qi)

@@ -93,3 +93,103 @@ def test_fov_impc_oracle_solves_with_certificate(oracle):
             assert np.all(act[fin_lo] >= q["lo"][fin_lo] - 1e-6)
             assert np.all(act[fin_hi] <= q["hi"][fin_hi] + 1e-6)
     assert math.isclose(cfg["fov_beta"], 2 * math.pi / 3)
+
+
+# ---- slack mode (FovBezierIMPCCBF.cpp:58-81, 150-205; FovMPCCBFQPGenerator.cpp:110-207) ------
+
+def _dist_to_ellipse_eig(robot, mean, cov):
+    """Independent restatement of FovBezierIMPCCBF::distanceToEllipse (:226-280) through a general
+    (non-symmetric) eigen-solver, as the reference's Eigen::EigenSolver."""
+    if math.isinf(cov[0][0]):
+        return -5.0
+    w, V = np.linalg.eig(np.array(cov, dtype=np.float64)[:2, :2])
+    w, V = w.real, V.real
+    s = 4.605
+    with np.errstate(invalid="ignore"):
+        a, b = math.sqrt(s * w[0]) if s * w[0] >= 0 else math.nan, \
+            math.sqrt(s * w[1]) if s * w[1] >= 0 else math.nan
+    if a < b:
+        a, b = b, a
+    m = 1 if w[1] > w[0] else 0
+    th = math.atan2(V[1, m], V[0, m])
+    if th < 0:
+        th += math.pi
+    sl = math.atan2(-mean[1] + robot[1], -mean[0] + robot[0])
+    xn = mean[0] + a * math.cos(sl - th) * math.cos(th) - b * math.sin(sl - th) * math.sin(th)
+    yn = mean[1] + a * math.cos(sl - th) * math.sin(th) + b * math.sin(sl - th) * math.cos(th)
+    dist = math.hypot(xn - robot[0], yn - robot[1])
+    if math.isnan(dist):
+        return 5.0
+    d = math.hypot(mean[0] - robot[0], mean[1] - robot[1])
+    rng_ = math.hypot(mean[0] - xn, mean[1] - yn)
+    return -dist if d < rng_ else dist
+
+
+def test_distance_to_ellipse_matches_eigen_restatement(oracle):
+    rng = np.random.default_rng(7)
+    cases = [((3.0, 0.0), (0.0, 0.0), [[0.1, 0, 0], [0, 0.1, 0], [0, 0, 0.1]]),  # FoV example cov
+             ((0.2, 0.1), (0.0, 0.0), [[0.1, 0, 0], [0, 0.1, 0], [0, 0, 0.1]]),  # inside
+             ((1.0, 2.0), (0.5, -1.0), [[math.inf, 0, 0], [0, 1, 0], [0, 0, 1]]),  # unknown
+             ((1.0, 2.0), (0.5, -1.0), [[0.3, 0.5, 0], [0.5, 0.2, 0], [0, 0, 1]])]  # not PSD
+    for _ in range(40):
+        L = rng.normal(size=(2, 2))
+        c = L @ L.T * rng.uniform(0.01, 2.0)
+        cov = [[c[0, 0], c[0, 1], 0], [c[1, 0], c[1, 1], 0], [0, 0, 1]]
+        cases.append((tuple(rng.uniform(-5, 5, 2)), tuple(rng.uniform(-5, 5, 2)), cov))
+    for robot, mean, cov in cases:
+        want = _dist_to_ellipse_eig(robot, mean, cov)
+        got = O.distance_to_ellipse(robot, mean, [cov[0][0], cov[0][1], cov[1][1]])
+        assert abs(got - want) <= 1e-12 * max(1.0, abs(want)), (robot, mean, cov, got, want)
+    # isotropic: the nearest circle point; signed
+    s = math.sqrt(4.605 * 0.1)
+    assert abs(O.distance_to_ellipse((3.0, 0.0), (0.0, 0.0), [0.1, 0.0, 0.1]) - (3.0 - s)) < 1e-14
+    assert abs(O.distance_to_ellipse((0.2, 0.0), (0.0, 0.0), [0.1, 0.0, 0.1]) + (s - 0.2)) < 1e-14
+    assert O.distance_to_ellipse((1.0, 2.0), (0.5, -1.0), [0.3, 0.5, 0.2]) == 5.0
+
+
+def _fov_slack_weights(cfg, st, nbs, covs):
+    """slack_weights[i] = w * decay^{idx[i]}, idx = argsort by distanceToEllipse (stable)."""
+    de = [_dist_to_ellipse_eig(st, nb, [[c[0], c[1], 0], [c[1], c[2], 0], [0, 0, 1]])
+          for nb, c in zip(nbs, covs)]
+    idx = sorted(range(len(de)), key=lambda i: de[i])
+    return np.array([cfg["slack_cost"] * cfg["slack_decay_rate"] ** idx[i] for i in range(len(de))])
+
+
+def test_fov_slack_qp_structure_and_weights(oracle):
+    cfg = swarm.fov_config(20, slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.5)
+    p = O.make_params(cfg)
+    states = np.array([[0.0, 0.0, 0.3, 0.4, 0.1, 0.0],
+                       [2.6, 0.9, 0, 0, 0, 0], [1.2, 2.9, 0, 0, 0, 0], [3.5, -1.0, 0, 0, 0, 0],
+                       [0.9, 1.4, 0, 0, 0, 0]])
+    covs = np.array([[0.1, 0.0, 0.1], [0.5, 0.2, 0.3], [0.1, 0.0, 0.1], [2.0, -0.4, 0.2],
+                     [0.05, 0.01, 0.02]])
+    nb = np.array([1, 2, 3, 4], dtype=np.int32)
+    ref = np.tile([2.0, 1.0, 0.3], 20)
+    sw = _fov_slack_weights(cfg, states[0], states[nb], covs[nb])
+    # the quirk is visible here: weights are not a monotone function of the distance rank
+    assert sorted(sw.tolist(), reverse=True) != sw.tolist()
+    q = oracle.assemble_qp(p, states[0], ref, states[nb], it=0, slack_w=sw)
+    nc = 48
+    assert q["n"] == nc + 4
+    np.testing.assert_array_equal(q["vlo"][nc:], 0.0)
+    np.testing.assert_array_equal(q["c"][nc:], sw)
+    ineq = ~(q["lo"] == q["hi"])
+    A = q["A"][ineq]
+    # Voronoi rows (first 4 x 4) carry no slack; FoV row block of neighbour i carries -1 on slack i
+    assert np.all(A[:16, nc:] == 0)
+    for i in range(4):
+        blk = A[16 + 4 * i:16 + 4 * i + 4, nc:]
+        expect = np.zeros((4, 4))
+        expect[:, i] = -1.0
+        np.testing.assert_array_equal(blk, expect)
+    assert np.all(A[32:, nc:] == 0)  # box rows
+    # optimize() computes the same weights internally: its iteration-0 QP is this one
+    r = O.impc_optimize(p, states, 0, nb, ref, covs=covs)
+    sol = oracle.solve_dense_qp(q)
+    assert r["status"][0] == sol["status"] == O.OPTIMAL
+    assert abs(r["obj"][0] - sol["obj"]) <= 1e-9 * max(1, abs(sol["obj"]))
+    # without covariances every distance is -5: weights follow the list order
+    q2 = oracle.assemble_qp(p, states[0], ref, states[nb], it=0,
+                            slack_w=1000.0 * 0.5 ** np.arange(4))
+    r2 = O.impc_optimize(p, states, 0, nb, ref)
+    assert abs(r2["obj"][0] - oracle.solve_dense_qp(q2)["obj"]) <= 1e-9 * max(1, abs(r2["obj"][0]))
