@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 7
+#define MPCCBF_ABI_VERSION 8
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -164,6 +164,12 @@ typedef struct mpccbf_batch {
                                  (math::addRandomNoise, Random.cpp:7-28); 0 = off */
     uint64_t noise_seed;      /* counter-based: noise(seed, step_index, agent, component) */
     int64_t step_index;       /* mpccbf_run_steps adds the step number */
+    /* FoV controller in slack mode (FovBezierIMPCCBF::optimize's other_robot_covs,
+     * FovBezierIMPCCBF.cpp:48-81): device, num_states x 3 = (cxx, cxy, cyy), the position block
+     * of each agent's estimate covariance as its observers hold it; orders the neighbours by
+     * distanceToEllipse for the slack weights. NULL = unknown (infinite: every distance is -5,
+     * weights follow the neighbour list order). Ignored otherwise. */
+    const double* cov;
 } mpccbf_batch;
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);

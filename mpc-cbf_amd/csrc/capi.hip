@@ -140,6 +140,7 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.vel_std = b->vel_std;
     a.noise_seed = b->noise_seed;
     a.step_index = b->step_index;
+    a.cov = b->cov;
     if (ev0) HIP_TRY(hipEventRecord(ev0, stream));
     hipError_t e = c->dev.cbf_mode == 1 ? launch_impc_fov(c->dev, c->dbuf, a, stream)
                                         : launch_impc(c->dev, c->dbuf, a, c->variant, stream);
@@ -339,7 +340,7 @@ int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
 
 const char* mpccbf_kernel_name(const mpccbf_ctx* c) {
     if (!c) return "";
-    if (c->dev.cbf_mode == 1) return "impc_fov_kernel";
+    if (c->dev.cbf_mode == 1) return c->dev.slack_mode ? "impc_fov_kernel<true>" : "impc_fov_kernel<false>";
     const char* n = impc_kernel_name(c->dev, c->variant);
     return n ? n : "";
 }

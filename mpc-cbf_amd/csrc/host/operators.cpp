@@ -143,8 +143,8 @@ std::string validate_params(const mpccbf_params& p) {
         return "MPC sampling range exceeds Bezier curve parameter range";
     if (p.num_pieces < 1 || p.num_control_points < 1) return "num_pieces and num_control_points must be >= 1";
     if (p.continuity_upto_degree < 0) return "bezier_continuity_upto_degree must be >= 0";
-    if (p.slack_mode && p.cbf_mode == 1)
-        return "slack_mode for the FoV controller is not supported by this build yet (SURVEY.md §8f rank 2)";
+    if (p.slack_mode && p.cbf_mode == 1 && p.cbf_horizon > 2)
+        return "slack_mode for the FoV controller supports cbf_horizon <= 2 (8 rows per neighbour)";
     if (p.cbf_mode != 0 && p.cbf_mode != 1) return "cbf_mode must be 0 (collision) or 1 (field of view)";
     if (p.cbf_mode == 1) {
         if (!(p.fov_beta > 0 && p.fov_beta <= 2 * M_PI + 1e-9)) return "fov must be in (0, 2 pi]";

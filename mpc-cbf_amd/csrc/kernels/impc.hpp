@@ -33,8 +33,9 @@ struct DevOps {
     // value / first derivative, cum: P cumulative piece parameters)
     int32_t P, o_EB0, o_EB1, o_cum;
     double eval_step;
-    // slack mode (collision controller): one slack variable per neighbour, cost
-    // slack_cost * slack_decay^rank (ConnectivityIMPCCBF.cpp:73-100)
+    // slack mode: one slack variable per neighbour; collision controller: cost
+    // slack_cost * slack_decay^rank (ConnectivityIMPCCBF.cpp:73-100); FoV controller: by
+    // distanceToEllipse with the reference's idx[i] indexing (FovBezierIMPCCBF.cpp:58-81)
     int32_t slack_mode;
     double slack_cost, slack_decay;
 };
@@ -93,6 +94,9 @@ struct ImpcArgs {
     double pos_std, vel_std;
     uint64_t noise_seed;
     int64_t step_index;
+    // FoV slack weights: num_states x 3 position covariances (cxx, cxy, cyy) of the neighbour
+    // estimates, or nullptr (unknown)
+    const double* cov;
 };
 
 constexpr int NSTAMP = 8;

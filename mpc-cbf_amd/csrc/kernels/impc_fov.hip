@@ -23,6 +23,41 @@ namespace dev {
 
 constexpr int FOV_NB_CAP = 16;  // observed neighbours per agent
 
+// FovBezierIMPCCBF::distanceToEllipse (FovBezierIMPCCBF.cpp:226-280): signed distance from the
+// robot to the point of the target's 90 % confidence ellipse (s = 4.605) at parametric angle
+// slope - theta (negative inside); cov = (cxx, cxy, cyy). The closed-form symmetric 2x2
+// eigen-decomposition replaces Eigen::EigenSolver (the result does not depend on the eigenpair
+// order or the eigenvector signs).
+__device__ double distance_to_ellipse(double rx, double ry, double mx, double my, double cxx,
+                                      double cxy, double cyy) {
+    if (isinf(cxx)) return -5.0;
+    const double hm = 0.5 * (cxx + cyy), hd = 0.5 * (cxx - cyy);
+    const double rt = sqrt(hd * hd + cxy * cxy);
+    const double a = sqrt(4.605 * (hm + rt)), b = sqrt(4.605 * (hm - rt));
+    double th = rt > 0.0 ? 0.5 * atan2(2.0 * cxy, cxx - cyy) : 0.0;
+    if (th < 0.0) th += M_PI;
+    const double sl = atan2(ry - my, rx - mx);
+    const double c1 = cos(sl - th), s1 = sin(sl - th), ct = cos(th), st = sin(th);
+    const double xn = mx + a * c1 * ct - b * s1 * st;
+    const double yn = my + a * c1 * st + b * s1 * ct;
+    const double dist = sqrt((xn - rx) * (xn - rx) + (yn - ry) * (yn - ry));
+    if (isnan(dist)) return 5.0;
+    const double d = sqrt((mx - rx) * (mx - rx) + (my - ry) * (my - ry));
+    const double range = sqrt((mx - xn) * (mx - xn) + (my - yn) * (my - yn));
+    return d < range ? -dist : dist;
+}
+
+// LDS of the slack rows (slack mode only)
+struct FovSlackLds {
+    double Go[WSL_ROWS * WNZ];
+    double Gc[WSL_CROWS * WNZ];
+    double Dvs[WSL_CROWS], wvs[WSL_CROWS], cvs[WSL_CROWS], zvs[WSL_ROWS];
+    double h[WSL_ROWS], live[WSL_ROWS];
+    double Tn[WSL_NB], w[WSL_NB], dist[WSL_NB];
+    int32_t order[WSL_NB];
+};
+
+template <bool SLACK>
 __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const double* __restrict__ buf,
                                                        const ImpcArgs args) {
     constexpr int NZ = 15;
@@ -32,6 +67,11 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     stamp(args, ai, lane, 0);
     const double* zero_row = nullptr;
     double kconst;
+    FovSlackLds* slk = nullptr;
+    if constexpr (SLACK) {
+        __shared__ FovSlackLds slk_mem;
+        slk = &slk_mem;
+    }
     __shared__ double Gimg[(WROWS + 1) * WNZ];  // + one all-zero row for unused slots
     __shared__ double rlo[WROWS], rhi[WROWS], rml[WROWS];
     __shared__ WaveScratch sc;
@@ -86,8 +126,34 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     } else {
         nnb = grid_neighbors<64>(args, self, s0[0], s0[1], nb_scratch, lane, s0[2]);
     }
-    const bool nb_overflow = nnb < 0 || nnb > FOV_NB_CAP;
+    const bool nb_overflow = nnb < 0 || nnb > (SLACK ? WSL_NB : FOV_NB_CAP);
     if (nb_overflow) nnb = 0;
+    if constexpr (SLACK) {
+        // slack weights (FovBezierIMPCCBF.cpp:58-81): sort the neighbours by distanceToEllipse
+        // (ties keep the list order, as libstdc++'s insertion sort below 17 elements does); the
+        // weight of neighbour i is slack_cost * decay^{idx[i]}, idx = the sorted list of indices
+        // (the reference's indexing, kept). Unknown covariances (args.cov == NULL) are infinite.
+        if (lane < nnb) {
+            const int nbi = grid_mode ? nb_scratch.idx[lane] : args.nb_col[nb0 + lane];
+            const double* cv = args.cov ? args.cov + (size_t)nbi * 3 : nullptr;
+            slk->dist[lane] = cv ? distance_to_ellipse(s0[0], s0[1], args.states[(size_t)nbi * 6],
+                                                       args.states[(size_t)nbi * 6 + 1], cv[0], cv[1], cv[2])
+                                 : -5.0;
+        }
+        wave_lds_sync();
+        if (lane < nnb) {
+            const double di = slk->dist[lane];
+            int rank = 0;
+            for (int j = 0; j < nnb; j++) {
+                const double dj = slk->dist[j];
+                rank += (dj < di || (dj == di && j < lane)) ? 1 : 0;
+            }
+            slk->order[rank] = lane;
+        }
+        wave_lds_sync();
+        if (lane < nnb) slk->w[lane] = op.slack_cost * pow(op.slack_decay, (double)slk->order[lane]);
+        wave_lds_sync();
+    }
     stamp(args, ai, lane, 2);
 
     bool have_curve = false, success = true;
@@ -135,14 +201,30 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         const double* UZ = opp(buf, op.o_UZ);
         const double* US = opp(buf, op.o_US);
         const int ntask = nnb * 4 * nk;
+        if constexpr (SLACK) {
+            // slack mode: neighbour i's rows go to lanes 8 i .. 8 i + 7 of the slack images
+            // (WaveSlack), uncompacted; every row starts inert, pads stay zero
+            for (int e = lane; e < WSL_ROWS * WNZ; e += 64) slk->Go[e] = 0.0;
+            for (int e = lane; e < WSL_CROWS * WNZ; e += 64) slk->Gc[e] = 0.0;
+            for (int e = lane; e < WSL_CROWS; e += 64) {
+                slk->Dvs[e] = 0.0;
+                slk->wvs[e] = 0.0;
+                slk->cvs[e] = 0.0;
+            }
+            slk->zvs[lane] = 0.0;
+            slk->h[lane] = 1.0;
+            slk->live[lane] = 0.0;
+            wave_lds_sync();
+        }
         for (int t0 = 0; t0 < ntask; t0 += 64) {
             const int task = t0 + lane;
             bool keep = false;
             double a[3] = {0.0, 0.0, 0.0}, bb = 0.0, us[3] = {0.0, 0.0, 0.0};
-            int k = 0;
+            int k = 0, i = 0, kind = 0;
             if (task < ntask) {
                 // order of FovBezierIMPCCBF.cpp:150-210: per neighbour, per kind, per k
-                const int i = task / (4 * nk), kind = (task / nk) % 4;
+                i = task / (4 * nk);
+                kind = (task / nk) % 4;
                 k = task % nk;
                 const int nbi = grid_mode ? nb_scratch.idx[i] : args.nb_col[nb0 + i];
                 double e[6], yk[NZ];
@@ -159,8 +241,8 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                     bmax += fmax(v1, v2);
                     bmin += fmin(v1, v2);
                 }
-                keep = present && !(op.cbf_filter && bb >= bmax);
-                if (present && bb < bmin - op.feas_tol) row_infeasible = true;
+                keep = present && !(op.cbf_filter && bb >= bmax);  // (exact: v >= 0 only relaxes)
+                if (!SLACK && present && bb < bmin - op.feas_tol) row_infeasible = true;
                 const double* USk = US + (size_t)k * 18;
 #pragma unroll
                 for (int d = 0; d < 3; d++) {
@@ -169,6 +251,18 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                     for (int s = 0; s < 6; s++) v = fma(USk[d * 6 + s], s0[s], v);
                     us[d] = v;
                 }
+            }
+            if constexpr (SLACK) {
+                if (keep) {
+                    const int r = 8 * i + kind * nk + k;
+                    const double* UZk = UZ + (size_t)k * 3 * NZ;
+#pragma unroll
+                    for (int jz = 0; jz < NZ; jz++)
+                        slk->Go[r * WNZ + jz] = -(a[0] * UZk[jz] + a[1] * UZk[NZ + jz] + a[2] * UZk[2 * NZ + jz]);
+                    slk->h[r] = bb + a[0] * us[0] + a[1] * us[1] + a[2] * us[2];
+                    slk->live[r] = 1.0;
+                }
+                continue;
             }
             const unsigned long long msk = __ballot(keep);
             const int slot = count + __popcll(msk & ((1ull << lane) - 1ull));
@@ -197,6 +291,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         if (it < 2) stamp(args, ai, lane, 3 + 2 * it);
         int st;
         int nit = 0;
+        double vobj = 0.0;  // slack mode: sum_i w_i v_i (addSlackCost, MPCCBFQPGeneratorBase.cpp:121-130)
         if (mtot > WROWS || nb_overflow) {
             st = ST_ERROR;  // capacity (rows per agent / observed neighbours)
         } else if (infeasible || row_infeasible) {
@@ -219,10 +314,29 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
 #else
             long long* dbg = nullptr;
 #endif
-            const PdipOut po = pdip_solve_wave(rw, Gimg, nchunk, sc, opp(buf, op.o_P16), opp(buf, op.o_LP16),
-                                               cfg, lane, dbg);
+            WaveSlack sk{};
+            if constexpr (SLACK) {
+                wave_lds_sync();  // the slack rows written above
+                sk.Go = slk->Go;
+                sk.Gc = slk->Gc;
+                sk.Dvs = slk->Dvs;
+                sk.wvs = slk->wvs;
+                sk.cvs = slk->cvs;
+                sk.zvs = slk->zvs;
+                sk.Tn = slk->Tn;
+                sk.nnb = nnb;
+                sk.nchunk_c = ((9 * nnb + 15) / 16) * 4;
+                sk.nchunk_o = ((8 * nnb + 15) / 16) * 4;
+                sk.h = slk->h[lane];
+                sk.live = slk->live[lane];
+                sk.w = (lane >> 3) < nnb ? slk->w[lane >> 3] : 0.0;
+            }
+            const PdipOut po = pdip_solve_wave<SLACK>(rw, Gimg, nchunk, sc, opp(buf, op.o_P16),
+                                                      opp(buf, op.o_LP16), cfg, lane, dbg, &sk, &vobj);
             st = po.status;
             nit = po.iters;
+            // slack mode: the slack rows are always satisfiable, phase 1 certifies the box and
+            // Voronoi rows (the ordinary image)
             if (st != ST_OPTIMAL) {
                 const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);
                 if (tstar > op.feas_tol) st = ST_INFEASIBLE;
@@ -236,7 +350,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 yk[j] = sc.y[j];
                 q15[j] = q_s[j];
             }
-            objv = reduced_objective<NZ>(op, buf, q15, yk, kconst);
+            objv = reduced_objective<NZ>(op, buf, q15, yk, kconst) + vobj;
             wave_lds_sync();
             if (lane < NZ) ykeep_s[lane] = sc.y[lane];
             have_curve = true;
@@ -261,7 +375,12 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
     if (a.num_agents <= 0) return hipSuccess;
     if (op.nz != 15 || op.m > dev::WROWS) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(dev::impc_fov_kernel, dim3(a.num_agents), dim3(64), 0, s, op, buf, a);
+    if (op.slack_mode) {
+        if (op.cbf_h > 2) return hipErrorInvalidValue;  // 4 kinds x cbf_h rows per 8-lane segment
+        hipLaunchKernelGGL(dev::impc_fov_kernel<true>, dim3(a.num_agents), dim3(64), 0, s, op, buf, a);
+    } else {
+        hipLaunchKernelGGL(dev::impc_fov_kernel<false>, dim3(a.num_agents), dim3(64), 0, s, op, buf, a);
+    }
     return hipGetLastError();
 }
 

@@ -136,6 +136,73 @@ struct WaveRows {
     double lo[WR], hi[WR], ml[WR];
 };
 
+#ifndef MPCCBF_SLK_INIT  // slack start: 1 = balanced (v = sb = 1/zb), 0 = v = sb = 1
+#define MPCCBF_SLK_INIT 1
+#endif
+// ---- slack mode (FovBezierIMPCCBF slack_mode, FovMPCCBFQPGenerator.cpp:110-207) --------------
+// Neighbour i (< 8) owns a slack variable v_i >= 0 with linear cost w_i that relaxes all of its
+// FoV rows  g_a^T y - v_i <= h_a  (up to 8: 4 kinds x cbf_horizon <= 2). Lane l holds row a = l & 7
+// of neighbour i = l >> 3 (inert when filtered: g = 0, 0 <= 1), so per-neighbour sums are 8-lane
+// DPP reductions and v_i, its bound slack sb_i and dual zb_i are replicated in the 8 lanes.
+// v_i is eliminated from the Newton system per neighbour. With D_a = z_a / s_a, T = sum D_a,
+// S = T + zb/sb and the D-weighted mean row gbar = sum D_a g_a / T, the Schur complement is
+//   sum_a D_a g_a g_a^T - (sum_a D_a g_a)(..)^T / S = sum_a D_a (g_a - gbar)(g_a - gbar)^T
+//                                                   + (T zb / (sb S)) gbar gbar^T,
+// a sum of positive terms: no cancellation when a row is nearly active (D ~ 1e20) while its slack
+// is in use (the textbook downdate would subtract two 1e20-sized terms). The same split applies
+// to every right-hand side: sum_a g_a phi_a + u c / S = sum_a (g_a - gbar) phi_a
+// + gbar (Db sum phi_a + T c) / S. So the matrix cores see the centred rows and one mean row per
+// neighbour as ordinary weighted rows of a second image (Gc).
+constexpr int WSL_NB = 8;                 // neighbours with a slack variable (one 8-lane segment each)
+constexpr int WSL_ROWS = 8 * WSL_NB;      // slack rows (lane = row)
+constexpr int WSL_CROWS = 80;             // centred rows + mean rows, padded to 16
+
+struct WaveSlack {
+    const double* Go;  // WSL_ROWS x 16 original slack rows (LDS; rows >= 8 nnb zero up to the 16-row pad)
+    double* Gc;        // WSL_CROWS x 16: centred rows (8 i + a), mean rows (8 nnb + i), zero pad
+    double* Dvs;       // Gc row weights: Gram, right-hand side (column 15), G^T v
+    double* wvs;
+    double* cvs;
+    double* zvs;       // z of the Go rows (dual residual)
+    double* Tn;        // per neighbour: sum of the live rows' D
+    int nnb;           // neighbours (<= WSL_NB)
+    int nchunk_c;      // chunks of Gc in use (multiple of 4)
+    int nchunk_o;      // chunks of Go in use (multiple of 4)
+    double h, live;    // this lane's row: bound, 1 if live (0: inert)
+    double w;          // slack cost of this lane's neighbour
+};
+
+// sum over the 8-lane segment (row_half_mirror pairs the two quads of each half-row)
+__device__ __forceinline__ double seg8_sum(double v) {
+    v += dpp_mov<DPP_XOR1>(v);
+    v += dpp_mov<DPP_XOR2>(v);
+    return v + dpp_mov<DPP_HALF_MIRROR>(v);
+}
+
+// Rebuild the centred image from the current weights: lane (q, p) handles column p of
+// neighbours q and q + 4.
+__device__ __forceinline__ void wave_slack_center(const WaveSlack& sk, int lane) {
+    const int q = lane >> 4, p = lane & 15;
+#pragma unroll
+    for (int u = 0; u < WSL_NB / 4; u++) {
+        const int i = q + 4 * u;
+        if (i < sk.nnb) {
+            double g[8], acc = 0.0;
+#pragma unroll
+            for (int a = 0; a < 8; a++) {
+                g[a] = sk.Go[(8 * i + a) * WNZ + p];
+                acc = fma(sk.Dvs[8 * i + a], g[a], acc);
+            }
+            const double T = sk.Tn[i];
+            const double gb = T > 0.0 ? acc * rcp(T) : 0.0;
+#pragma unroll
+            for (int a = 0; a < 8; a++) sk.Gc[(8 * i + a) * WNZ + p] = g[a] - gb;
+            sk.Gc[(8 * sk.nnb + i) * WNZ + p] = gb;
+        }
+    }
+    wave_lds_sync();
+}
+
 // a . b over 16 entries, both in LDS (b wave-uniform: broadcast reads)
 __device__ __forceinline__ double dotl(const double* a, const double* b) {
     double s0 = 0.0, s1 = 0.0;
@@ -274,11 +341,16 @@ __device__ __forceinline__ void publish16(double* __restrict__ dst, double v, in
 
 // Main solve. P, LP: 16x16 row-major, padded with the identity (uniform, global). sc.q: linear
 // term; on return sc.y holds the iterate. nchunk: row chunks in use.
+// SLK: slack mode — skp holds the slack rows (see WaveSlack); v_obj gets sum_i w_i v_i.
+template <bool SLK = false>
 __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
                                    WaveScratch& sc, const double* __restrict__ P,
                                    const double* __restrict__ LP, const PdipCfg cfg, int lane,
-                                   long long* dbg = nullptr) {
+                                   long long* dbg = nullptr, const WaveSlack* skp = nullptr,
+                                   double* v_obj = nullptr) {
     (void)dbg;
+    (void)skp;
+    (void)v_obj;
     const int i = lane & 15;
     const double qi = sc.q[i];
     double L[WNZ], inv_i;
@@ -302,6 +374,30 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         pl[s] = rw.ml[s] * rcp(1.0 + fabs(rw.lo[s]));
         pu[s] = rcp(1.0 + fabs(rw.hi[s]));
         nloc += rw.ml[s] + 1.0;
+    }
+    // slack rows: this lane holds row (lane & 7) of neighbour (lane >> 3); lanes of neighbours
+    // >= nnb hold inert rows and no slack variable. Start: zb = max(w, 1) (the dual the bound
+    // carries when no row is active), v = sb = 1 / zb (a centred pair: sb zb = 1 like the rows'
+    // s z; with sb = 1 the pair sat 1e3 off the central path and some crowded QPs broke down
+    // near the optimum), row slacks from the residual.
+    const bool son = SLK && (lane >> 3) < (SLK ? skp->nnb : 0);
+    const bool lead = son && (lane & 7) == 0;  // counts the neighbour's bound once in sums
+    double v = 1.0, sb = 1.0, zb = 1.0, cs = 1.0, cz = 1.0, pc = 1.0, slh = 1.0, sliv = 0.0, slw = 0.0;
+    if constexpr (SLK) {
+        const WaveSlack& sk = *skp;
+        slh = son ? sk.h : 1.0;
+        sliv = son ? sk.live : 0.0;
+        slw = son ? sk.w : 0.0;
+        zb = fmax(slw, 1.0);
+#if MPCCBF_SLK_INIT == 1
+        sb = rcp(zb);  // balanced start: sb zb = 1
+        v = sb;
+#endif
+        const double t = son ? dotl(sk.Go + lane * WNZ, sc.y) : 0.0;
+        cs = fmax(slh - (t - sliv * v), 1.0);
+        cz = rcp(cs);
+        pc = rcp(1.0 + fabs(slh));
+        nloc += lead ? 2.0 : 1.0;
     }
     const double inv_ns = rcp(wave_reduce<Op::Sum>(nloc));
     const double inv_qn = rcp(1.0 + grp_max<16>(fabs(qi)));
@@ -331,9 +427,44 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             mloc = fma(sl[s], zl[s], fma(su[s], zu[s], mloc));
             rp = fmax(rp, fmax(fabs(rl[s]) * pl[s], fabs(ru[s]) * pu[s]));
         }
+        // slack rows: residual cr = h - g y + v - s, D = z / s; per neighbour T = sum D (live),
+        // S = T + Db; weights of the centred rows and of the mean row (predictor right-hand side
+        // phi = D cr, v-equation term -(Db rb + w))
+        double scr = 0.0, sci = 1.0, sD = 0.0, sT = 0.0, siS = 1.0, sDb = 0.0, srb = 0.0;
+        if constexpr (SLK) {
+            const WaveSlack& sk = *skp;
+            const double t = son ? dotl(sk.Go + lane * WNZ, sc.y) : 0.0;
+            scr = slh - t + sliv * v - cs;
+            sci = rcp(cs);
+            sD = cz * sci;
+            const double Dl = sliv * sD;
+            sT = seg8_sum(Dl);
+            const double SR = seg8_sum(Dl * scr);
+            sDb = zb * rcp(sb);
+            srb = v - sb;
+            siS = rcp(sT + sDb);
+            mloc = fma(cs, cz, mloc);
+            if (lead) mloc = fma(sb, zb, mloc);
+            rp = fmax(rp, fabs(scr) * pc);
+            if (son) {
+                rp = fmax(rp, fabs(srb));
+                sk.Dvs[lane] = Dl;
+                sk.wvs[lane] = Dl * scr;
+                sk.zvs[lane] = sliv * cz;
+            }
+            if (lead) {
+                const int nb = lane >> 3;
+                sk.Tn[nb] = sT;
+                sk.Dvs[8 * sk.nnb + nb] = sT * sDb * siS;
+                sk.wvs[8 * sk.nnb + nb] = (sDb * SR - sT * fma(sDb, srb, slw)) * siS;
+            }
+            wave_lds_sync();
+            wave_slack_center(sk, lane);
+        }
         PSTAMP(1);
         wave_lds_sync();
-        const wd4 acc = wave_gram(Gs, sc.Dv, sc.wv, nchunk, lane);
+        wd4 acc = wave_gram(Gs, sc.Dv, sc.wv, nchunk, lane);
+        if constexpr (SLK) acc += wave_gram(skp->Gc, skp->Dvs, skp->wvs, skp->nchunk_c, lane);
         double Mr[WNZ];
         gram_rows(acc, sc.M, lane, Mr);
         const double rhs_i = Mr[WNZ - 1];  // G^T w (column 15)
@@ -343,9 +474,22 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         wave_reduce2<Op::Sum, Op::Max>(mloc, rp);
         const double mu = mloc * inv_ns;
         const double py_i = dotr(Prow, sc.y) + qi;  // (P y + q)_i
+        // exact relative dual residual; slack mode adds the slack rows (original g, weights z) and
+        // the v equations w - sum_a z_a - zb (relative to 1 + w)
+        auto dual_res = [&]() {
+            double gt = wave_gt(Gs, sc.cv, nchunk, lane);
+            if constexpr (SLK) gt += wave_gt(skp->Go, skp->zvs, skp->nchunk_o, lane);
+            double r = grp_max<16>(fabs(py_i + gt)) * inv_qn;
+            if constexpr (SLK) {
+                const double zs = seg8_sum(sliv * cz);
+                const double rv = son ? fabs(slw - zs - zb) * rcp(1.0 + slw) : 0.0;
+                r = fmax(r, wave_reduce<Op::Max>(rv));
+            }
+            return r;
+        };
         bool rd_fresh = false;
         if (rd_exact) {
-            rd_track = grp_max<16>(fabs(py_i + wave_gt(Gs, sc.cv, nchunk, lane))) * inv_qn;
+            rd_track = dual_res();
             rd_exact = false;
             rd_fresh = true;
         }
@@ -353,7 +497,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         const bool finite = isfinite(rp) && isfinite(rd_track) && isfinite(mu) && isfinite(Mr[0]);
         if (finite && rp <= cfg.tol && mu <= cfg.tol * 0.1 && rd_track <= cfg.tol) {
             if (!rd_fresh)  // the tracked dual residual is a prediction: confirm it exactly
-                rd_track = grp_max<16>(fabs(py_i + wave_gt(Gs, sc.cv, nchunk, lane))) * inv_qn;
+                rd_track = dual_res();
             if (rd_track <= cfg.tol) {
                 out.status = ST_OPTIMAL;
                 break;
@@ -362,12 +506,33 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         if (it == 0) mu0 = mu;
         if (it >= cfg.maxit || !finite || mu > 1e8 * fmax(mu0, 1.0)) {
             out.status = ST_UNKNOWN;
+#ifdef MPCCBF_DEBUG_EXIT  // diagnostics build: exit reason in the iteration count
+            out.iters = it + 1000 * (it >= cfg.maxit ? 1 : !finite ? 2 : 3);
+#endif
             break;
         }
         PSTAMP(3);
         // ---- factor
-        if (!chol_rows(Mr, L, inv_i, sc.M, lane)) {
+        bool fok = chol_rows(Mr, L, inv_i, sc.M, lane);
+        if constexpr (SLK) {
+            if (!fok) {
+                // a pivot lost to cancellation (active rows' D ~ 1e20 against P ~ 1e5, more
+                // frequent with the slack rows' coupled pairs): refactor with a diagonal shift of
+                // 1e-12 of the largest diagonal entry (inexact Newton step; residuals stay exact)
+                double dg = 0.0;
+#pragma unroll
+                for (int k = 0; k < WNZ; k++) dg = (k == i) ? Mr[k] : dg;
+                const double tau = 1e-12 * grp_max<16>(fabs(dg));
+#pragma unroll
+                for (int k = 0; k < WNZ; k++) Mr[k] += (k == i) ? tau : 0.0;
+                fok = chol_rows(Mr, L, inv_i, sc.M, lane);
+            }
+        }
+        if (!fok) {
             out.status = ST_UNKNOWN;
+#ifdef MPCCBF_DEBUG_EXIT
+            out.iters = it + 4000;
+#endif
             break;
         }
         PSTAMP(4);
@@ -388,6 +553,25 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             rs = fmax(rs, fmax(-ql, -qu));
             rz = fmax(rz, fmax(rw.ml[s] * (1.0 + ql), 1.0 + qu));
         }
+        // slack rows: dv = (sum_a D_a (g_a dy - cr_a) - Db rb - w) / S, ds = cr - g dy + dv
+        double sds = 0.0, sdz = 0.0, sdv = 0.0, sdsb = 0.0, sdzb = 0.0;
+        if constexpr (SLK) {
+            const double td = son ? dotl(skp->Go + lane * WNZ, sc.d) : 0.0;
+            const double sd = seg8_sum(sliv * sD * (td - scr));
+            sdv = (sd - fma(sDb, srb, slw)) * siS;
+            sds = scr - td + sliv * sdv;
+            const double qs = sds * sci;
+            sdz = -cz * (1.0 + qs);
+            rs = fmax(rs, -qs);
+            rz = fmax(rz, 1.0 + qs);
+            if (son) {
+                sdsb = sdv + srb;
+                const double qb = sdsb * rcp(sb);
+                sdzb = -zb * (1.0 + qb);
+                rs = fmax(rs, -qb);
+                rz = fmax(rz, 1.0 + qb);
+            }
+        }
         wave_reduce2<Op::Max, Op::Max>(rs, rz);
         const double ap = rcp(fmax(1.0, rs)), ad = rcp(fmax(1.0, rz));
         double mua = 0.0;
@@ -395,6 +579,10 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         for (int s = 0; s < WR; s++) {
             mua = fma(sl[s] + ap * dsl[s], zl[s] + ad * dzl[s], mua);
             mua = fma(su[s] + ap * dsu[s], zu[s] + ad * dzu[s], mua);
+        }
+        if constexpr (SLK) {
+            mua = fma(cs + ap * sds, cz + ad * sdz, mua);
+            if (lead) mua = fma(sb + ap * sdsb, zb + ad * sdzb, mua);
         }
         mua = wave_reduce<Op::Sum>(mua) * inv_ns;
         double sig = mu > 0.0 ? mua * rcp(mu) : 0.0;
@@ -409,8 +597,23 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             ku[s] = smu - dsu[s] * dzu[s];
             sc.cv[wave_owner_row(lane, s)] = kl[s] * il[s] - ku[s] * iu[s];
         }
+        // slack rows: row weights om = -kc / s on the centred rows; the mean row takes
+        // (Db sum om + T kb / sb) / S; the v equation keeps vcv = -sum om + kb / sb
+        double skc = 0.0, skb = 0.0, svcv = 0.0;
+        if constexpr (SLK) {
+            const WaveSlack& sk = *skp;
+            skc = smu - sds * sdz;
+            const double om = -skc * sci;
+            const double som = seg8_sum(sliv * om);
+            skb = smu - sdsb * sdzb;
+            const double isb = rcp(sb);
+            svcv = fma(skb, isb, -som);
+            if (son) sk.cvs[lane] = sliv * om;
+            if (lead) sk.cvs[8 * sk.nnb + (lane >> 3)] = fma(sDb, som, sT * skb * isb) * siS;
+        }
         wave_lds_sync();
-        const double vc_i = wave_gt(Gs, sc.cv, nchunk, lane);
+        double vc_i = wave_gt(Gs, sc.cv, nchunk, lane);
+        if constexpr (SLK) vc_i += wave_gt(skp->Gc, skp->cvs, skp->nchunk_c, lane);
         PSTAMP(7);
         const double dy_i = dya_i + solve_rows(L, sc.M, inv_i, vc_i, i);
         publish16(sc.d, dy_i, lane);
@@ -427,6 +630,21 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             rmax = fmax(rmax, fmax(-dsl[s] * il[s], -dsu[s] * iu[s]));
             rmax = fmax(rmax, fmax(-rw.ml[s] * dzl[s] * izl, -dzu[s] * rcp_fast(zu[s])));
         }
+        // slack rows, combined direction: dv adds the corrector's v-equation term vcv
+        if constexpr (SLK) {
+            const double td = son ? dotl(skp->Go + lane * WNZ, sc.d) : 0.0;
+            const double sd = seg8_sum(sliv * sD * (td - scr));
+            sdv = (sd - fma(sDb, srb, slw) + svcv) * siS;
+            sds = scr - td + sliv * sdv;
+            sdz = (skc - cs * cz - cz * sds) * sci;
+            rmax = fmax(rmax, fmax(-sds * sci, -sdz * rcp_fast(cz)));
+            if (son) {
+                sdsb = sdv + srb;
+                const double isb = rcp(sb);
+                sdzb = (skb - sb * zb - zb * sdsb) * isb;
+                rmax = fmax(rmax, fmax(-sdsb * isb, -sdzb * rcp_fast(zb)));
+            }
+        }
         rmax = wave_reduce<Op::Max>(rmax);
         const double alpha = 0.99 * rcp(fmax(0.99, rmax));
         PSTAMP(9);
@@ -439,11 +657,21 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             zl[s] = rw.ml[s] * fmax(fma(alpha, dzl[s], zl[s]), 1e-300);
             zu[s] = fmax(fma(alpha, dzu[s], zu[s]), 1e-300);
         }
+        if constexpr (SLK) {
+            cs = fmax(fma(alpha, sds, cs), 1e-300);
+            cz = fmax(fma(alpha, sdz, cz), 1e-300);
+            if (son) {
+                v = fma(alpha, sdv, v);
+                sb = fmax(fma(alpha, sdsb, sb), 1e-300);
+                zb = fmax(fma(alpha, sdzb, zb), 1e-300);
+            }
+        }
         PSTAMP(10);
         rd_track *= (1.0 - alpha);
         PSTAMP(11);
         if (it % 8 == 7) rd_exact = true;
     }
+    if constexpr (SLK) *v_obj = wave_reduce<Op::Sum>(lead ? slw * v : 0.0);
     return out;
 }
 

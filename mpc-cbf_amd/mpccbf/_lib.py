@@ -75,6 +75,7 @@ class Batch(C.Structure):
         ("next_states", C.c_void_p), ("knn_k", C.c_int32), ("knn_radius", C.c_double),
         ("stamps", C.c_void_p), ("traj_t", C.c_void_p), ("pos_std", C.c_double),
         ("vel_std", C.c_double), ("noise_seed", C.c_uint64), ("step_index", C.c_int64),
+        ("cov", C.c_void_p),
     ]
 
 
@@ -213,7 +214,7 @@ class Context:
     def impc_solve(self, states, nb_row_ptr=None, nb_col=None, targets=None, refs=None,
                    agent_first=0, num_agents=None, x=None, status=None, obj=None, iters=None,
                    next_states=None, knn_k=0, knn_radius=0.0, stream=None, stamps=None,
-                   traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0):
+                   traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0, cov=None):
         """CSR neighbours (nb_row_ptr/nb_col) or, with both None, the knn_k nearest within
         knn_radius found on the device in the same launch sequence. traj_t (float64, one per
         agent, initialised to -1) turns on the closed-loop simulator semantics: x persists the
@@ -226,14 +227,16 @@ class Context:
                   status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters),
                   next_states=_ptr(next_states), knn_k=int(knn_k), knn_radius=float(knn_radius),
                   stamps=_ptr(stamps), traj_t=_ptr(traj_t), pos_std=float(pos_std),
-                  vel_std=float(vel_std), noise_seed=int(noise_seed), step_index=int(step_index))
+                  vel_std=float(vel_std), noise_seed=int(noise_seed), step_index=int(step_index),
+                  cov=_ptr(cov))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
 
     def run_steps(self, states, states_alt, num_steps, targets=None, refs=None, agent_first=0,
                   num_agents=None, knn_k=0, knn_radius=0.0, nb_row_ptr=None, nb_col=None, x=None,
                   status=None, obj=None, iters=None, status_log=None, iters_log=None,
                   timing=False, comm=None, reserve_steps=0, solve_stride=1, step_timing=True,
-                  stream=None, traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0):
+                  stream=None, traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0,
+                  cov=None):
         """Closed-loop control steps on the device (mpccbf_run_steps). Returns a dict with the
         table holding the final states ('final', a tensor) and, with timing=True, per-step
         device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms)."""
@@ -245,7 +248,7 @@ class Context:
                   status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters), next_states=None,
                   knn_k=int(knn_k), knn_radius=float(knn_radius), stamps=None,
                   traj_t=_ptr(traj_t), pos_std=float(pos_std), vel_std=float(vel_std),
-                  noise_seed=int(noise_seed), step_index=int(step_index))
+                  noise_seed=int(noise_seed), step_index=int(step_index), cov=_ptr(cov))
         step_ms = np.zeros(max(num_steps, 1), dtype=np.float32) if timing and step_timing else None
         solve_ms = np.zeros(max(num_steps, 1), dtype=np.float32) if timing else None
         r = Run(num_steps=num_steps, states_alt=_ptr(states_alt), status_log=_ptr(status_log),

@@ -23,24 +23,25 @@ def _torch():
     return torch
 
 
-def run_gpu(ctx, states, targets, row_ptr, col, torch):
+def run_gpu(ctx, states, targets, row_ptr, col, torch, cov=None):
     dev = torch.device("cuda", 0)
     st = torch.tensor(states, dtype=torch.float64, device=dev)
     tg = torch.tensor(targets, dtype=torch.float64, device=dev)
     rp = torch.tensor(row_ptr, dtype=torch.int32, device=dev)
     cl = torch.tensor(col if len(col) else np.zeros(1, np.int32), dtype=torch.int32, device=dev)
     out = ctx.alloc_outputs(len(states))
-    ctx.impc_solve(st, rp, cl, targets=tg, **out)
+    cv = None if cov is None else torch.tensor(cov, dtype=torch.float64, device=dev)
+    ctx.impc_solve(st, rp, cl, targets=tg, cov=cv, **out)
     torch.cuda.synchronize()
     return {k: v.cpu().numpy() for k, v in out.items()}
 
 
-def run_oracle(cfg, states, targets, row_ptr, col, agents):
+def run_oracle(cfg, states, targets, row_ptr, col, agents, cov=None):
     p = O.make_params(cfg)
     refs = swarm.refs_from_targets(targets, cfg["k_hor"])
     res = []
     for a in agents:
-        res.append(O.impc_optimize(p, states, a, col[row_ptr[a]:row_ptr[a + 1]], refs[a]))
+        res.append(O.impc_optimize(p, states, a, col[row_ptr[a]:row_ptr[a + 1]], refs[a], covs=cov))
     return res
 
 
@@ -271,7 +272,7 @@ def test_fov_controller_matches_oracle(mpclib, scale, n_agents):
     states[:, :2] *= scale
     rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
     ctx = mpclib.Context(cfg)
-    assert ctx.kernel_name == "impc_fov_kernel"
+    assert ctx.kernel_name == "impc_fov_kernel<false>"
     g = run_gpu(ctx, states, targets, rp, col, torch)
     agents = list(range(n_agents))
     ref = run_oracle(cfg, states, targets, rp, col, agents)
@@ -360,3 +361,89 @@ def test_very_crowded_swarm_statuses_match_oracle(mpclib):
     ref = run_oracle(cfg, states, targets, rp, col, agents)
     compare(cfg, g, ref, agents)
     assert np.sum(g["status"][:, 0] == O.INFEASIBLE) > 16
+
+
+def _estimate_covs(n, seed):
+    """Per-agent position covariances (cxx, cxy, cyy) of the neighbours' estimates: the FoV
+    example's 0.1 I for a third, random anisotropic ones for the rest, a few unknown (inf)."""
+    rng = np.random.default_rng(seed)
+    cov = np.zeros((n, 3))
+    for j in range(n):
+        if j % 3 == 0:
+            cov[j] = (0.1, 0.0, 0.1)
+        elif j % 11 == 5:
+            cov[j] = (np.inf, 0.0, np.inf)
+        else:
+            L = rng.normal(size=(2, 2)) * 0.4
+            c = L @ L.T + 0.01 * np.eye(2)
+            cov[j] = (c[0, 0], c[0, 1], c[1, 1])
+    return cov
+
+
+@pytest.mark.parametrize("scale,decay", [(1.0, 0.5), (0.6, 0.9)])
+def test_fov_slack_mode_matches_oracle(mpclib, scale, decay):
+    """FovBezierIMPCCBF in slack mode (the FoV example's setting: slack_cost 1000): one slack per
+    observed neighbour relaxes its FoV rows; weights ordered by distanceToEllipse with the
+    reference's idx[i] indexing; the kernel eliminates each slack in its 8-lane segment through
+    the centred-row Schur form (impc_fov_kernel<true>)."""
+    torch = _torch()
+    cfg = swarm.fov_config(20, slack_mode=1, slack_cost=1000.0, slack_decay_rate=decay)
+    n = 100
+    states, targets = swarm.heading_swarm(n, seed=2)
+    states[:, :2] *= scale
+    cov = _estimate_covs(n, 5)
+    rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+    ctx = mpclib.Context(cfg)
+    assert ctx.kernel_name == "impc_fov_kernel<true>"
+    g = run_gpu(ctx, states, targets, rp, col, torch, cov=cov)
+    agents = list(range(n))
+    ref = run_oracle(cfg, states, targets, rp, col, agents, cov=cov)
+    compare(cfg, g, ref, agents)
+    assert np.mean(g["status"][:, 0] == O.OPTIMAL) > 0.9
+
+
+def test_fov_slack_mode_crowded_closed_loop(mpclib):
+    """Slack mode on closed-loop-evolved crowded states (device neighbour query, 30 steps), where
+    the plain FoV QPs are often infeasible: the slack QPs solve, and match the oracle."""
+    torch = _torch()
+    cfg = swarm.fov_config(20, slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.7)
+    n = 100
+    states, targets = swarm.heading_swarm(n, seed=3)
+    states[:, :2] *= 0.6
+    targets[:, :2] *= 0.6
+    cov = _estimate_covs(n, 9)
+    dev = torch.device("cuda", 0)
+    ctx = mpclib.Context(cfg)
+    a, b = torch.tensor(states, device=dev), torch.empty((n, 6), dtype=torch.float64, device=dev)
+    r = ctx.run_steps(a, b, 30, targets=torch.tensor(targets, device=dev), knn_k=8,
+                      knn_radius=cfg["fov_Rs"], cov=torch.tensor(cov, device=dev))
+    torch.cuda.synchronize()
+    evolved = r["final"].cpu().numpy()
+    rp, col = swarm.fov_csr(evolved, 8, cfg["fov_Rs"], cfg["fov_beta"])
+    g = run_gpu(ctx, evolved, targets, rp, col, torch, cov=cov)
+    agents = list(range(n))
+    ref = run_oracle(cfg, evolved, targets, rp, col, agents, cov=cov)
+    compare(cfg, g, ref, agents)
+    plain = run_oracle(swarm.fov_config(20), evolved, targets, rp, col, agents)
+    n_inf_plain = sum(r_["status"][0] == O.INFEASIBLE for r_ in plain)
+    assert np.sum(g["status"][:, 0] == O.OPTIMAL) >= n - n_inf_plain
+
+
+def test_fov_slack_grid_neighbours_match_csr(mpclib):
+    """Slack weights from the device FoV neighbour query equal the CSR path's (same lists)."""
+    torch = _torch()
+    cfg = swarm.fov_config(20, slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.5)
+    states, targets = swarm.heading_swarm(300, seed=6)
+    states[:, :2] *= 0.7
+    cov = _estimate_covs(300, 1)
+    rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+    ctx = mpclib.Context(cfg)
+    g_csr = run_gpu(ctx, states, targets, rp, col, torch, cov=cov)
+    dev = torch.device("cuda", 0)
+    out = ctx.alloc_outputs(len(states))
+    ctx.impc_solve(torch.tensor(states, device=dev), targets=torch.tensor(targets, device=dev),
+                   knn_k=8, knn_radius=cfg["fov_Rs"], cov=torch.tensor(cov, device=dev), **out)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), g_csr["status"])
+    ok = g_csr["status"] == 0
+    np.testing.assert_allclose(out["obj"].cpu().numpy()[ok], g_csr["obj"][ok], rtol=1e-10, atol=1e-9)
