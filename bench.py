@@ -43,6 +43,11 @@ def parse():
     ap.add_argument("--agents-total", type=int, default=0, help="strong scaling: fixed total")
     ap.add_argument("--k-hor", type=int, default=0, help="default 15 (collision), 20 (fov)")
     ap.add_argument("--knn", type=int, default=8)
+    ap.add_argument("--slack", action="store_true",
+                    help="slack_mode (one slack per neighbour on its CBF rows): the FoV example's "
+                         "setting (slack_cost 1000, neighbour covariances 0.1 I, "
+                         "BezierIMPCCBFPFXYYaw_example.cpp:138-142,201-202)")
+    ap.add_argument("--slack-decay", type=float, default=0.9)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--cpu-baseline-agents", type=int, default=-1,
                     help="agents in the CPU-oracle sample (default: sized for ~10 s)")
@@ -103,15 +108,19 @@ def main():
     per = total // world
     assert per * world == total, "agents must divide evenly over ranks"
     first = rank * per
+    slack = dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=args.slack_decay) if args.slack else {}
     if fov:
-        cfg = swarm.fov_config(args.k_hor)
+        cfg = swarm.fov_config(args.k_hor, **slack)
         radius = cfg["fov_Rs"]  # observed neighbours: inside the FoV cone and the sensing range
         states_h, targets_h = swarm.heading_swarm(total)
         # 5 m lattice, sensing range 6 m: 1-3 observed neighbours per agent, steady closed loop
     else:
-        cfg = swarm.config(args.k_hor)
+        cfg = swarm.config(args.k_hor, **slack)
         radius = 3.0 * cfg["d_min"]
         states_h, targets_h = swarm.lattice_swarm(total)
+    # neighbour-estimate covariances (FoV slack weights): the FoV example's 0.1 I for everyone
+    cov_h = np.tile([0.1, 0.0, 0.1], (total, 1)) if (fov and args.slack) else None
+    cov = None if cov_h is None else torch.tensor(cov_h, dtype=torch.float64, device=dev)
     ctx = Context(cfg, device=local)
     ctx.set_variant(args.variant)
 
@@ -145,7 +154,7 @@ def main():
         traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
         common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn,
                       knn_radius=radius, x=out["x"], obj=out["obj"], comm=comm, traj_t=traj_t,
-                      pos_std=0.001, vel_std=0.01, noise_seed=20251015)
+                      pos_std=0.001, vel_std=0.01, noise_seed=20251015, cov=cov)
         r = ctx.run_steps(tables[0], tables[1], args.warmup, status=out["status"],
                           iters=out["iters"], reserve_steps=nsteps, **common)
         if r["final"] is not tables[0]:
@@ -183,7 +192,7 @@ def main():
                 kev_pair[0].record(stream)
             ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
                            x=out["x"], status=st, obj=out["obj"], iters=it,
-                           next_states=shard.next_out, **nb)
+                           next_states=shard.next_out, cov=cov, **nb)
             if kev_pair is not None:
                 kev_pair[1].record(stream)
             shard.publish()
@@ -261,6 +270,7 @@ def main():
                      if fov else
                      f"config3: {total} agents, horizon {cfg['k_hor']}, pairwise collision CBF, "
                      f"knn{args.knn} r={radius:g}m ({args.neighbours})")
+                    + (f", slack_mode (cost 1000, decay {args.slack_decay:g})" if args.slack else "")
                     + ", base_config.json; 2 IMPC QPs/agent/step"
                     + ("" if world == 1 else f"; {per}/GPU, RCCL all-gather of states")),
                 "agents_total": total,
@@ -287,7 +297,7 @@ def main():
             "cpu_baseline": None,
         }
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args, radius)
+            res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -312,7 +322,7 @@ def pmc_traffic(kname: str):
     return None, None
 
 
-def cpu_baseline(cfg, states_h, targets_h, args, radius):
+def cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h=None):
     """The oracle (CPU restatement of the reference assembly + dense QP solve, standing in for
     CPLEX which cannot run here) on a bounded sample of the same workload, 1 thread (CPLEX
     Threads=1, CPLEX.cpp:158)."""
@@ -330,11 +340,11 @@ def cpu_baseline(cfg, states_h, targets_h, args, radius):
     if count is None:
         # calibrate on 32 agents, then size the sample for ~10 s
         t = time.perf_counter()
-        r = O.impc_batch(p, states_h, refs, rp, col, 0, 32, 1)
+        r = O.impc_batch(p, states_h, refs, rp, col, 0, 32, 1, covs=cov_h)
         dt = (time.perf_counter() - t) / 32
         count = int(min(n, max(64, 10.0 / max(dt, 1e-6))))
     t = time.perf_counter()
-    r = O.impc_batch(p, states_h, refs, rp, col, 0, count, 1)
+    r = O.impc_batch(p, states_h, refs, rp, col, 0, count, 1, covs=cov_h)
     dt = time.perf_counter() - t
     return {"value": r["solved"] / dt, "unit": "QP/s", "cores": 1, "kind": "port",
             "sample": f"first {count} agents of the same swarm/step, {r['solved']} QPs, "

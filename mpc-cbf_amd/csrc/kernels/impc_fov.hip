@@ -311,6 +311,10 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             long long* dbg = (args.stamps && it == 0)
                                  ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 16
                                  : nullptr;
+#elif defined(MPCCBF_DEBUG_TRACE)  // per-iteration trace of the last IMPC iteration's solve
+            long long* dbg = (args.stamps && it == op.impc_iter - 1)
+                                 ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 512
+                                 : nullptr;
 #else
             long long* dbg = nullptr;
 #endif

@@ -1458,7 +1458,8 @@ double orc_distance_to_ellipse(const double* robot2, const double* mean2, const 
 
 int64_t orc_impc_batch(const orc_params* p, int32_t N, const double* states, const double* refs,
                        const int32_t* rp, const int32_t* col, int32_t first, int32_t count,
-                       int32_t nthreads, int32_t* status, double* obj, double* x_last) {
+                       int32_t nthreads, int32_t* status, double* obj, double* x_last,
+                       const double* covs) {
     std::atomic<int> next(0);
     std::atomic<int64_t> solved(0);
     const int K = p->k_hor, it_n = p->impc_iter;
@@ -1471,7 +1472,8 @@ int64_t orc_impc_batch(const orc_params* p, int32_t N, const double* states, con
             const int n = orc_num_vars(p, nb);
             std::vector<double> xs((size_t)n * it_n, 0.0);
             int att = orc::impc(p, N, states, a, nb, col + rp[a], refs + (size_t)a * 3 * K,
-                                status + (size_t)i * it_n, obj + (size_t)i * it_n, xs.data(), nullptr);
+                                status + (size_t)i * it_n, obj + (size_t)i * it_n, xs.data(), nullptr,
+                                covs);
             solved += att;
             int last_ok = -1;
             for (int t = 0; t < att; t++)

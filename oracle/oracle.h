@@ -129,7 +129,8 @@ int64_t orc_impc_batch(const orc_params* p, int32_t num_agents, const double* st
                        const double* refs /* N x 3K */, const int32_t* nb_row_ptr,
                        const int32_t* nb_col, int32_t first, int32_t count, int32_t nthreads,
                        int32_t* status /* count x impc_iter */, double* obj /* count x impc_iter */,
-                       double* x_last /* count x n_curve */);
+                       double* x_last /* count x n_curve */,
+                       const double* covs /* N x 3 (FoV slack weights), or NULL */);
 
 /* Curve evaluation of a solution vector (SingleParameterPiecewiseCurve::eval,
  * splines/src/curves/SingleParameterPiecewiseCurve.cpp:94-127): out3 = d-th derivative at t. */

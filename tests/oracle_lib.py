@@ -94,7 +94,7 @@ def lib():
         L.orc_distance_to_ellipse.argtypes = [dp, dp, dp]
         L.orc_impc_batch.restype = C.c_int64
         L.orc_impc_batch.argtypes = [C.POINTER(OrcParams), C.c_int32, dp, dp, ip, ip, C.c_int32,
-                                     C.c_int32, C.c_int32, ip, dp, dp]
+                                     C.c_int32, C.c_int32, ip, dp, dp, dp]
         L.orc_eval_curve.argtypes = [C.POINTER(OrcParams), dp, C.c_double, C.c_int32, dp]
         _lib = L
     return _lib
@@ -216,8 +216,9 @@ def impc_optimize(p: OrcParams, states, self_idx, neighbor_idx, ref, covs=None):
     return dict(attempted=att, status=status, obj=obj, x=x, qp_iters=qi)
 
 
-def impc_batch(p: OrcParams, states, refs, row_ptr, col, first, count, nthreads=1):
+def impc_batch(p: OrcParams, states, refs, row_ptr, col, first, count, nthreads=1, covs=None):
     states = np.ascontiguousarray(states, dtype=np.float64)
+    cv = None if covs is None else np.ascontiguousarray(covs, dtype=np.float64)
     refs = np.ascontiguousarray(refs, dtype=np.float64)
     rp = np.ascontiguousarray(row_ptr, dtype=np.int32)
     cl = np.ascontiguousarray(col if len(col) else np.zeros(1), dtype=np.int32)
@@ -229,7 +230,8 @@ def impc_batch(p: OrcParams, states, refs, row_ptr, col, first, count, nthreads=
     solved = lib().orc_impc_batch(C.byref(p), len(states), _d(states), _d(refs),
                                   rp.ctypes.data_as(C.POINTER(C.c_int32)),
                                   cl.ctypes.data_as(C.POINTER(C.c_int32)), first, count, nthreads,
-                                  status.ctypes.data_as(C.POINTER(C.c_int32)), _d(obj), _d(xl))
+                                  status.ctypes.data_as(C.POINTER(C.c_int32)), _d(obj), _d(xl),
+                                  None if cv is None else _d(cv))
     return dict(solved=int(solved), status=status, obj=obj, x_last=xl)
 
 
