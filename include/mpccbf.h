@@ -228,8 +228,9 @@ int mpccbf_build_neighbors(mpccbf_ctx* ctx, const double* states, int32_t num_st
  * Per agent: min ||u - u_des||^2 over the control input u (3) subject to the 4 FoV HOCBF rows of
  * every observed neighbour (FovQPGenerator.cpp:12-115), the velocity CBF rows
  * u_d <= vmax_d - v_d and -u_d <= v_d - vmin_d (FovCBF.cpp:112-146, linear alpha) and
- * u_min <= u <= u_max. No context needed; all pointers are device pointers, asynchronous on the
- * stream. slack_mode is not supported yet (MPCCBF_ERR_INVALID_ARGUMENT). */
+ * u_min <= u <= u_max. slack_mode: one slack variable >= 0 per observed neighbour relaxes its FoV
+ * rows (FovControl.cpp:25-62). No context needed; all pointers are device pointers, asynchronous
+ * on the stream. */
 typedef struct mpccbf_fov_control_params {
     double fov, Ds, Rs;       /* FovCBF(fov, safety_dist, max_dist, ...) */
     double v_min[3], v_max[3];
@@ -250,10 +251,14 @@ typedef struct mpccbf_fov_control_batch {
     int32_t* status;           /* out, num_agents (qpcpp::SolveStatus), or NULL */
     double* obj;               /* out, ||u - u_des||^2, or NULL */
     int32_t* iters;            /* out, PDIP iterations, or NULL */
+    const double* nb_cov;      /* slack mode: per observed neighbour (cxx, cxy, cyy), the estimate's
+                                  position covariance ordering the slack weights by
+                                  distanceToEllipse (FovControl.cpp:25-46); NULL = unknown */
 } mpccbf_fov_control_batch;
 
-/* Capacity: 4 * neighbours + 9 <= 64 rows per agent (13 observed neighbours); beyond it the
- * agent's status is MPCCBF_ERROR. */
+/* Capacity: 4 * neighbours + 9 <= 64 rows per agent (13 observed neighbours) without slack;
+ * 16 observed neighbours in slack mode (one slack variable each, cost slack_cost *
+ * decay^{idx[i]}, included in obj); beyond it the agent's status is MPCCBF_ERROR. */
 int mpccbf_fov_control_solve(const mpccbf_fov_control_params* p, const mpccbf_fov_control_batch* b,
                              int32_t device, void* hip_stream);
 

@@ -501,9 +501,10 @@ extern "C" {
 int mpccbf_fov_control_solve(const mpccbf_fov_control_params* p, const mpccbf_fov_control_batch* b,
                              int32_t device, void* stream) {
     if (!p || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
-    if (p->slack_mode)
-        return fail(MPCCBF_ERR_INVALID_ARGUMENT,
-                    "FovControl slack_mode is not supported by this build yet (SURVEY.md §8f rank 3)");
+    if (p->slack_mode && !(p->slack_cost > 0.0))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "Slack cost must be positive when slack_mode is enabled");
+    if (p->slack_mode && !(p->slack_decay_rate > 0.0 && p->slack_decay_rate <= 1.0))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "Slack decay rate must be in (0,1] when slack_mode is enabled");
     if (!(p->fov > 0.0) || !(p->Rs > 0.0))
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "fov and Rs must be positive");
     for (int d = 0; d < 3; d++)
@@ -544,6 +545,10 @@ int mpccbf_fov_control_solve(const mpccbf_fov_control_params* p, const mpccbf_fo
         a.P[i] = (i % 4 == 0) ? 2.0 : 0.0;  // ||u - u_des||^2 = 1/2 u^T (2 I) u - 2 u_des^T u + c
         a.LP[i] = (i % 4 == 0) ? std::sqrt(2.0) : 0.0;
     }
+    a.slack_mode = p->slack_mode ? 1 : 0;
+    a.slack_cost = p->slack_cost;
+    a.slack_decay = p->slack_decay_rate;
+    a.nb_cov = b->nb_cov;
     HIP_TRY(launch_fov_control(a, (hipStream_t)stream));
     return MPCCBF_OK;
 }

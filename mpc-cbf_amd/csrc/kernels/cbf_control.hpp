@@ -22,6 +22,10 @@ struct FovControlArgs {
     int32_t maxit;
     double tol, feas_tol;
     double P[9], LP[9];  // 2 I and its Cholesky factor (objective 1/2 u^T P u + q^T u)
+    // slack mode (FovControl.cpp:25-62): one slack per observed neighbour (<= 16)
+    int32_t slack_mode;
+    double slack_cost, slack_decay;
+    const double* nb_cov;  // per observed neighbour (cxx, cxy, cyy), or nullptr (unknown)
 };
 
 constexpr int FOV_CONTROL_ROW_CAP = 4 * 16;  // rows per agent (R = 4 slots x 16 lanes)

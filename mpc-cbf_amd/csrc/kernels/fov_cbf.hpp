@@ -60,5 +60,30 @@ __device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double 
     b = lf2 + 5.0 * gamma * b4 * lf + gamma * p2 * p2 * psi;
 }
 
+// FovBezierIMPCCBF::distanceToEllipse (FovBezierIMPCCBF.cpp:226-280; FovControl.cpp:90-148 is the
+// same function): signed distance from the
+// robot to the point of the target's 90 % confidence ellipse (s = 4.605) at parametric angle
+// slope - theta (negative inside); cov = (cxx, cxy, cyy). The closed-form symmetric 2x2
+// eigen-decomposition replaces Eigen::EigenSolver (the result does not depend on the eigenpair
+// order or the eigenvector signs).
+__device__ inline double distance_to_ellipse(double rx, double ry, double mx, double my, double cxx,
+                                      double cxy, double cyy) {
+    if (isinf(cxx)) return -5.0;
+    const double hm = 0.5 * (cxx + cyy), hd = 0.5 * (cxx - cyy);
+    const double rt = sqrt(hd * hd + cxy * cxy);
+    const double a = sqrt(4.605 * (hm + rt)), b = sqrt(4.605 * (hm - rt));
+    double th = rt > 0.0 ? 0.5 * atan2(2.0 * cxy, cxx - cyy) : 0.0;
+    if (th < 0.0) th += M_PI;
+    const double sl = atan2(ry - my, rx - mx);
+    const double c1 = cos(sl - th), s1 = sin(sl - th), ct = cos(th), st = sin(th);
+    const double xn = mx + a * c1 * ct - b * s1 * st;
+    const double yn = my + a * c1 * st + b * s1 * ct;
+    const double dist = sqrt((xn - rx) * (xn - rx) + (yn - ry) * (yn - ry));
+    if (isnan(dist)) return 5.0;
+    const double d = sqrt((mx - rx) * (mx - rx) + (my - ry) * (my - ry));
+    const double range = sqrt((mx - xn) * (mx - xn) + (my - yn) * (my - yn));
+    return d < range ? -dist : dist;
+}
+
 }  // namespace dev
 }  // namespace mpccbf

@@ -382,7 +382,8 @@ class FovControlParams(C.Structure):
 class FovControlBatch(C.Structure):
     _fields_ = [("num_agents", C.c_int32), ("states", C.c_void_p), ("desired_u", C.c_void_p),
                 ("nb_row_ptr", C.c_void_p), ("nb_xy", C.c_void_p), ("u", C.c_void_p),
-                ("status", C.c_void_p), ("obj", C.c_void_p), ("iters", C.c_void_p)]
+                ("status", C.c_void_p), ("obj", C.c_void_p), ("iters", C.c_void_p),
+                ("nb_cov", C.c_void_p)]
 
 
 def fov_control_params(cfg: dict) -> FovControlParams:
@@ -401,11 +402,13 @@ def fov_control_params(cfg: dict) -> FovControlParams:
 
 
 def fov_control_solve(cfg: dict, states, desired_u, nb_row_ptr, nb_xy, u, status=None, obj=None,
-                      iters=None, device: int = 0, stream=None):
-    """Batched FovControl::optimize (mpccbf_fov_control_solve): device tensors in, u out."""
+                      iters=None, device: int = 0, stream=None, nb_cov=None):
+    """Batched FovControl::optimize (mpccbf_fov_control_solve): device tensors in, u out.
+    Slack mode: cfg["control_slack_mode"] with slack_cost / slack_decay_rate; nb_cov (one
+    (cxx, cxy, cyy) row per observed neighbour) orders the slack weights."""
     b = FovControlBatch(num_agents=states.shape[0], states=_ptr(states), desired_u=_ptr(desired_u),
                         nb_row_ptr=_ptr(nb_row_ptr), nb_xy=_ptr(nb_xy), u=_ptr(u),
-                        status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters))
+                        status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters), nb_cov=_ptr(nb_cov))
     p = fov_control_params(cfg)
     _check(load().mpccbf_fov_control_solve(C.byref(p), C.byref(b), device, _stream(stream)))
 

@@ -1496,23 +1496,41 @@ int64_t orc_impc_batch(const orc_params* p, int32_t N, const double* states, con
     return solved.load();
 }
 
-int orc_fov_control(double fov, double Ds, double Rs, const double* vmin3, const double* vmax3,
-                    const double* umin3, const double* umax3, const double* st,
-                    const double* ud, int32_t nb, const double* nb_xy, double* u_out,
-                    double* obj_out) {
+int orc_fov_control_slack(double fov, double Ds, double Rs, const double* vmin3, const double* vmax3,
+                          const double* umin3, const double* umax3, const double* st,
+                          const double* ud, int32_t nb, const double* nb_xy, int32_t slack_mode,
+                          double slack_cost, double slack_decay, const double* nb_cov,
+                          double* u_out, double* obj_out) {
     try {
         orc::DenseQP q;
-        q.n = 3;
+        // decision variables: u (3), then one slack per neighbour in slack mode
+        // (CBFQPGeneratorBase.cpp:9-27: addVariable(0, max))
+        const int ns = slack_mode ? nb : 0;
+        const int n = 3 + ns;
+        q.n = n;
         // addDesiredControlCost (CBFQPGeneratorBase.cpp:36-57): I, -2 u_des, |u_des|^2
-        q.H.assign(9, 0.0);
-        q.c.assign(3, 0.0);
+        q.H.assign((size_t)n * n, 0.0);
+        q.c.assign(n, 0.0);
         for (int d = 0; d < 3; d++) {
-            q.H[d * 3 + d] = 1.0;
+            q.H[d * n + d] = 1.0;
             q.c[d] = -2.0 * ud[d];
             q.c0 += ud[d] * ud[d];
         }
-        auto add_row = [&](const double* g, double hi) {
-            for (int d = 0; d < 3; d++) q.A.push_back(g[d]);
+        if (slack_mode) {
+            // FovControl.cpp:25-46: sort by distanceToEllipse (:90-148, the same restatement as
+            // FovBezierIMPCCBF's), weight of neighbour i = w * decay^{idx[i]}; addSlackCost ->
+            // linear terms (CBFQPGeneratorBase.cpp:59-74, 136-170)
+            const double inf_cov[3] = {INFINITY, 0.0, INFINITY};
+            std::vector<double> de(nb);
+            for (int i = 0; i < nb; i++)
+                de[i] = orc::distance_to_ellipse(st, nb_xy + 2 * i, nb_cov ? nb_cov + 3 * i : inf_cov);
+            std::vector<size_t> idx(nb);
+            std::iota(idx.begin(), idx.end(), 0);
+            std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return de[a] < de[b]; });
+            for (int i = 0; i < nb; i++) q.c[3 + i] = slack_cost * std::pow(slack_decay, (double)idx[i]);
+        }
+        auto add_row = [&](const double* g, double hi, int slack) {
+            for (int d = 0; d < n; d++) q.A.push_back(d < 3 ? g[d] : (d - 3 == slack ? -1.0 : 0.0));
             q.lo.push_back(-std::numeric_limits<double>::max());
             q.hi.push_back(hi);
             q.m++;
@@ -1523,28 +1541,40 @@ int orc_fov_control(double fov, double Ds, double Rs, const double* vmin3, const
             for (int r = 0; r < 4; r++) {
                 if (!fr[r].present) continue;  // 360-degree FoV: no border rows
                 const double g[3] = {-fr[r].a[0], -fr[r].a[1], -fr[r].a[2]};
-                add_row(g, fr[r].b);
+                add_row(g, fr[r].b, slack_mode ? i : -1);  // FovQPGenerator.cpp:24-36: -1 on slack i
             }
         }
         for (int d = 0; d < 3; d++) {  // addMinVelConstraints: -(+e_d) u <= v_d - vmin_d
             double g[3] = {0, 0, 0};
             g[d] = -1.0;
-            add_row(g, st[3 + d] - vmin3[d]);
+            add_row(g, st[3 + d] - vmin3[d], -1);
         }
         for (int d = 0; d < 3; d++) {  // addMaxVelConstraints: -(-e_d) u <= vmax_d - v_d
             double g[3] = {0, 0, 0};
             g[d] = 1.0;
-            add_row(g, vmax3[d] - st[3 + d]);
+            add_row(g, vmax3[d] - st[3 + d], -1);
         }
-        q.vlo.assign(umin3, umin3 + 3);
-        q.vhi.assign(umax3, umax3 + 3);
+        q.vlo.assign(n, 0.0);
+        q.vhi.assign(n, std::numeric_limits<double>::infinity());
+        for (int d = 0; d < 3; d++) {
+            q.vlo[d] = umin3[d];
+            q.vhi[d] = umax3[d];
+        }
         orc::Solution r = orc::solve(q);
-        for (int d = 0; d < 3; d++) u_out[d] = r.x.size() == 3 ? r.x[d] : 0.0;
+        for (int d = 0; d < 3; d++) u_out[d] = (int)r.x.size() == n ? r.x[d] : 0.0;
         if (obj_out) *obj_out = r.obj;
         return r.status;
     } catch (...) {
         return ORC_ERROR;
     }
+}
+
+int orc_fov_control(double fov, double Ds, double Rs, const double* vmin3, const double* vmax3,
+                    const double* umin3, const double* umax3, const double* st,
+                    const double* ud, int32_t nb, const double* nb_xy, double* u_out,
+                    double* obj_out) {
+    return orc_fov_control_slack(fov, Ds, Rs, vmin3, vmax3, umin3, umax3, st, ud, nb, nb_xy, 0, 0.0,
+                                 1.0, nullptr, u_out, obj_out);
 }
 
 int orc_eval_curve(const orc_params* p, const double* x, double t, int32_t d, double* out3) {

@@ -144,6 +144,15 @@ int orc_fov_control(double fov, double Ds, double Rs, const double* vmin3, const
                     const double* umin3, const double* umax3, const double* state6,
                     const double* desired_u3, int32_t num_neighbors, const double* nb_xy,
                     double* u_out3, double* obj_out);
+/* orc_fov_control with slack_mode (FovControl.cpp:25-46, FovQPGenerator.cpp:12-115): one slack
+ * variable >= 0 per observed neighbour relaxes its 4 FoV rows (-1 coefficient), linear cost
+ * slack_cost * decay^{idx[i]} with idx the neighbours sorted by distanceToEllipse (nb_cov:
+ * nb x 3 = (cxx, cxy, cyy) per neighbour, or NULL = unknown). obj_out includes the slack cost. */
+int orc_fov_control_slack(double fov, double Ds, double Rs, const double* vmin3, const double* vmax3,
+                          const double* umin3, const double* umax3, const double* state6,
+                          const double* desired_u3, int32_t num_neighbors, const double* nb_xy,
+                          int32_t slack_mode, double slack_cost, double slack_decay,
+                          const double* nb_cov, double* u_out3, double* obj_out);
 int orc_eval_curve(const orc_params* p, const double* x, double t, int32_t deriv, double* out3);
 
 #ifdef __cplusplus

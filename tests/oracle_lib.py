@@ -79,6 +79,9 @@ def lib():
         L.orc_apply_input.argtypes = [C.c_double, dp, dp, dp]
         L.orc_fov_cbf.argtypes = [dp, dp, C.c_double, C.c_double, C.c_double, dp, dp, ip]
         L.orc_prediction_matrices.argtypes = [C.c_double, C.c_int32, dp, dp]
+        L.orc_fov_control_slack.argtypes = [C.c_double, C.c_double, C.c_double, dp, dp, dp, dp,
+                                            dp, dp, C.c_int32, dp, C.c_int32, C.c_double,
+                                            C.c_double, dp, dp, dp]
         L.orc_fov_control.argtypes = [C.c_double, C.c_double, C.c_double, dp, dp, dp, dp, dp, dp,
                                       C.c_int32, dp, dp, dp]
         L.orc_num_vars.argtypes = [C.POINTER(OrcParams), C.c_int32]
@@ -246,8 +249,10 @@ def fov_cbf(state, target, fov, Ds, Rs):
     return a.reshape(4, 3), b, pr
 
 
-def fov_control(cfg: dict, state, desired_u, nb_xy):
-    """FovControl::optimize restated (non-slack): (status, u (3,), objective incl. constant)."""
+def fov_control(cfg: dict, state, desired_u, nb_xy, nb_cov=None):
+    """FovControl::optimize restated: (status, u (3,), objective incl. constant and, in slack
+    mode (cfg control_slack_mode / slack_cost / slack_decay_rate), the slack cost). nb_cov: per-neighbour
+    (cxx, cxy, cyy) for the slack weights, None = unknown."""
     f = lambda v: np.ascontiguousarray(v, dtype=np.float64)  # noqa: E731
     umin = cfg.get("u_min", cfg["a_min"])
     umax = cfg.get("u_max", cfg["a_max"])
@@ -256,9 +261,13 @@ def fov_control(cfg: dict, state, desired_u, nb_xy):
     obj = np.zeros(1)
     vmin, vmax, umin, umax, st, ud = (f(cfg["v_min"]), f(cfg["v_max"]), f(umin), f(umax), f(state),
                                       f(desired_u))
-    stt = lib().orc_fov_control(cfg["fov_beta"], cfg["fov_Ds"], cfg["fov_Rs"], _d(vmin), _d(vmax),
-                                _d(umin), _d(umax), _d(st), _d(ud), len(nb),
-                                _d(nb) if len(nb) else None, _d(u), _d(obj))
+    cv = None if nb_cov is None else np.ascontiguousarray(np.reshape(nb_cov, (-1, 3)), dtype=np.float64)
+    stt = lib().orc_fov_control_slack(cfg["fov_beta"], cfg["fov_Ds"], cfg["fov_Rs"], _d(vmin),
+                                      _d(vmax), _d(umin), _d(umax), _d(st), _d(ud), len(nb),
+                                      _d(nb) if len(nb) else None, int(cfg.get("control_slack_mode", 0)),
+                                      float(cfg.get("slack_cost", 0.0)),
+                                      float(cfg.get("slack_decay_rate", 1.0)),
+                                      None if cv is None or not len(cv) else _d(cv), _d(u), _d(obj))
     return stt, u, float(obj[0])
 
 
