@@ -1588,3 +1588,231 @@ int orc_eval_curve(const orc_params* p, const double* x, double t, int32_t d, do
 }
 
 }  // extern "C"
+
+// ================================================================ ConnectivityControl (CBF-only)
+// cbf/src/controller/ConnectivityControl.cpp:22-99 with the rows of
+// cbf/src/detail/ConnectivityCBF.cpp (safety :152-198, CLF :200-243, velocity :250-286,
+// lambda2 :375-414, connectivity gradient :430-456, connectivity CBF :458-512) and
+// cbf/src/optimization/ConnectivityQPGenerator.cpp:13-150.
+namespace orc {
+
+// ConnectivityCBF::getLambda2 (:375-414): weighted Laplacian of the planar positions,
+// A_ij = exp((Rs^2 - d_ij^2)^2 / sigma) - 1 within Rs = dmax, sigma = dmax^4 / ln 2 (getSigma,
+// :368-370); second smallest eigenvalue and its unit eigenvector. Eigen's
+// SelfAdjointEigenSolver is restated by a cyclic Jacobi sweep to machine precision (eigenvalues
+// sorted ascending; the eigenvector's sign is immaterial: it enters squared differences only).
+static void lambda2(int N, const double* pos2, double dmax, double* l2, double* vec) {
+    const double Rs2 = dmax * dmax, sigma = std::pow(dmax, 4) / std::log(2.0);
+    std::vector<double> A((size_t)N * N, 0.0), V((size_t)N * N, 0.0);
+    for (int i = 0; i < N; i++) {
+        double deg = 0.0;
+        for (int j = 0; j < N; j++) {
+            if (i == j) continue;
+            const double dx = pos2[2 * i] - pos2[2 * j], dy = pos2[2 * i + 1] - pos2[2 * j + 1];
+            const double d2 = dx * dx + dy * dy;
+            const double wij = d2 <= Rs2 ? std::exp(std::pow(Rs2 - d2, 2) / sigma) - 1.0 : 0.0;
+            A[(size_t)i * N + j] = -wij;
+            deg += wij;
+        }
+        A[(size_t)i * N + i] = deg;
+        V[(size_t)i * N + i] = 1.0;
+    }
+    for (int sweep = 0; sweep < 100; sweep++) {
+        double off = 0.0, tot = 0.0;
+        for (int i = 0; i < N; i++)
+            for (int j = 0; j < N; j++) {
+                const double a = A[(size_t)i * N + j] * A[(size_t)i * N + j];
+                tot += a;
+                if (i != j) off += a;
+            }
+        if (off <= 1e-32 * tot || off == 0.0) break;
+        for (int p = 0; p < N - 1; p++)
+            for (int q = p + 1; q < N; q++) {
+                const double apq = A[(size_t)p * N + q];
+                if (apq == 0.0) continue;
+                const double app = A[(size_t)p * N + p], aqq = A[(size_t)q * N + q];
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
+                const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < N; k++) {  // A <- J^T A J, V <- V J
+                    const double akp = A[(size_t)k * N + p], akq = A[(size_t)k * N + q];
+                    A[(size_t)k * N + p] = c * akp - s * akq;
+                    A[(size_t)k * N + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < N; k++) {
+                    const double apk = A[(size_t)p * N + k], aqk = A[(size_t)q * N + k];
+                    A[(size_t)p * N + k] = c * apk - s * aqk;
+                    A[(size_t)q * N + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < N; k++) {
+                    const double vkp = V[(size_t)k * N + p], vkq = V[(size_t)k * N + q];
+                    V[(size_t)k * N + p] = c * vkp - s * vkq;
+                    V[(size_t)k * N + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    std::vector<int> ord(N);
+    std::iota(ord.begin(), ord.end(), 0);
+    std::stable_sort(ord.begin(), ord.end(),
+                     [&](int a, int b) { return A[(size_t)a * N + a] < A[(size_t)b * N + b]; });
+    const int k = N > 1 ? ord[1] : ord[0];
+    *l2 = A[(size_t)k * N + k];
+    double nrm = 0.0;
+    for (int i = 0; i < N; i++) nrm += V[(size_t)i * N + k] * V[(size_t)i * N + k];
+    nrm = std::sqrt(nrm);
+    for (int i = 0; i < N; i++) vec[i] = V[(size_t)i * N + k] / nrm;  // eigenvec.normalize()
+}
+
+// ConnectivityCBF::initConnCBF / getConnConstraints / getConnBound (:430-512) for robot `self`:
+// h = lambda2 - 0.1; grad h over the self position (compute_full_grad_h, :430-456: every other
+// robot j, in range or not), its Hessian over the self position (eigenvector entries held
+// fixed, as the symbols are substituted after differentiation), Lf h = grad . v,
+// Lf^2 h = v^T Hess v, and with the linear alpha (setAlpha(defaultAlpha), gamma = 5)
+// Bc = Lf^2 h + alpha(Lf h) + alpha(Lf h + alpha(h)). Ac = (dh/dx, dh/dy, 0).
+static void conn_row(int N, const double* states, int self, const double* ev, double l2,
+                     double dmax, double* a3, double* b, double* dbg /* gx gy Hxx Hxy Hyy Lfh Lf2h */) {
+    const double Rs2 = dmax * dmax, sigma = std::pow(dmax, 4) / std::log(2.0);
+    const double* si = states + 6 * self;
+    double gx = 0, gy = 0, hxx = 0, hxy = 0, hyy = 0;
+    for (int j = 0; j < N; j++) {
+        if (j == self) continue;
+        const double* sj = states + 6 * j;
+        const double dx = si[0] - sj[0], dy = si[1] - sj[1];
+        const double diff = Rs2 - (dx * dx + dy * dy);
+        const double E = std::exp(diff * diff / sigma);  // A_ij + 1
+        const double c = std::pow(ev[self] - ev[j], 2);
+        const double k = -4.0 * c / sigma;  // dA/dx = -4 (A + 1) diff / sigma dx
+        gx += k * E * diff * dx;
+        gy += k * E * diff * dy;
+        // d/dx (E diff dx) = -4 E diff^2 dx^2 / sigma - 2 E dx^2 + E diff, etc.
+        hxx += k * (-4.0 * E * diff * diff * dx * dx / sigma - 2.0 * E * dx * dx + E * diff);
+        hxy += k * (-4.0 * E * diff * diff * dx * dy / sigma - 2.0 * E * dx * dy);
+        hyy += k * (-4.0 * E * diff * diff * dy * dy / sigma - 2.0 * E * dy * dy + E * diff);
+    }
+    const double vx = si[3], vy = si[4];
+    const double lfh = gx * vx + gy * vy;
+    const double lf2h = vx * (hxx * vx + hxy * vy) + vy * (hxy * vx + hyy * vy);
+    const double gamma = 5.0, h = l2 - 0.1;
+    *b = lf2h + gamma * lfh + gamma * (lfh + gamma * h);
+    a3[0] = gx;
+    a3[1] = gy;
+    a3[2] = 0.0;
+    if (dbg) {
+        const double d[7] = {gx, gy, hxx, hxy, hyy, lfh, lf2h};
+        std::memcpy(dbg, d, sizeof d);
+    }
+}
+
+// ConnectivityCBF::initCLFCBF (:200-243) at (state, neighbour): V = (|p - p_n| - 2)^2, ego
+// velocity only; Ac = grad V (x, y), Bc = Lf^2 V + 5 Lf V + 2 V.
+static void clf_row(const double* st, const double* nb, double* a3, double* b) {
+    const double dx = st[0] - nb[0], dy = st[1] - nb[1];
+    const double dist = std::sqrt(dx * dx + dy * dy), e = dist - 2.0;
+    const double gx = 2.0 * e * dx / dist, gy = 2.0 * e * dy / dist;
+    const double vx = st[3], vy = st[4];
+    const double lfv = gx * vx + gy * vy;
+    const double dv = (dx * vx + dy * vy) / dist;  // v . grad dist
+    const double vv = vx * vx + vy * vy;
+    const double lf2v = 2.0 * dv * dv + 2.0 * e * (vv - dv * dv) / dist;  // v^T Hess V v
+    *b = lf2v + 5.0 * lfv + 2.0 * e * e;
+    a3[0] = gx;
+    a3[1] = gy;
+    a3[2] = 0.0;
+}
+
+}  // namespace orc
+
+extern "C" {
+
+void orc_lambda2(int32_t N, const double* pos2, double dmax, double* l2, double* vec) {
+    orc::lambda2(N, pos2, dmax, l2, vec);
+}
+
+void orc_conn_cbf(int32_t N, const double* states, int32_t self, const double* ev, double l2,
+                  double dmax, double* a3, double* b, double* dbg7) {
+    orc::conn_row(N, states, self, ev, l2, dmax, a3, b, dbg7);
+}
+
+void orc_clf_cbf(const double* st, const double* nb, double* a3, double* b) { orc::clf_row(st, nb, a3, b); }
+
+int orc_connectivity_control(double dmin, double dmax, const double* vmin3, const double* vmax3,
+                             int32_t slack_mode, double slack_cost, double slack_decay, int32_t N,
+                             const double* states, int32_t self, const double* ud, double* u_out,
+                             double* obj_out, double* l2_out) {
+    try {
+        orc::DenseQP q;
+        const int ns = slack_mode ? N : 0;  // CBFQPGeneratorBase(num_robots, slack): N slacks
+        const int n = 3 + ns;
+        q.n = n;
+        q.H.assign((size_t)n * n, 0.0);
+        q.c.assign(n, 0.0);
+        for (int d = 0; d < 3; d++) {  // addDesiredControlCost
+            q.H[d * n + d] = 1.0;
+            q.c[d] = -2.0 * ud[d];
+            q.c0 += ud[d] * ud[d];
+        }
+        for (int i = 0; i < ns; i++) q.c[3 + i] = slack_cost * std::pow(slack_decay, (double)i);  // :31-38
+        auto add_row = [&](const double* g, double hi, int slack) {
+            for (int d = 0; d < n; d++) q.A.push_back(d < 3 ? g[d] : (d - 3 == slack ? -1.0 : 0.0));
+            q.lo.push_back(-std::numeric_limits<double>::max());
+            q.hi.push_back(hi);
+            q.m++;
+        };
+        const double* st = states + 6 * self;
+        // safety rows vs every other robot (:49-55), slack i
+        for (int i = 0; i < N - 1; i++) {
+            const double* nb = states + 6 * (i + (i >= self ? 1 : 0));
+            double a[3], b;
+            orc_safety_cbf(st, nb, dmin, a, &b);
+            const double g[3] = {-a[0], -a[1], -a[2]};
+            add_row(g, b, slack_mode ? i : -1);
+        }
+        // velocity CBFs (:58-59): -u_d <= v_d - vmin_d, u_d <= vmax_d - v_d; no control bounds
+        // (addControlBoundConstraint is commented out, :60)
+        for (int d = 0; d < 3; d++) {
+            double g[3] = {0, 0, 0};
+            g[d] = -1.0;
+            add_row(g, st[3 + d] - vmin3[d], -1);
+        }
+        for (int d = 0; d < 3; d++) {
+            double g[3] = {0, 0, 0};
+            g[d] = 1.0;
+            add_row(g, vmax3[d] - st[3 + d], -1);
+        }
+        std::vector<double> pos(2 * N), ev(N);
+        for (int i = 0; i < N; i++) {
+            pos[2 * i] = states[6 * i];
+            pos[2 * i + 1] = states[6 * i + 1];
+        }
+        double l2 = 0.0;
+        orc::lambda2(N, pos.data(), dmax, &l2, ev.data());
+        if (l2_out) *l2_out = l2;
+        if (l2 > 0.1) {  // addConnConstraint (:70-71; ConnectivityQPGenerator.cpp:13-44): last slack
+            double a[3], b;
+            orc::conn_row(N, states, self, ev.data(), l2, dmax, a, &b, nullptr);
+            const double g[3] = {-a[0], -a[1], -a[2]};
+            add_row(g, b, slack_mode ? N - 1 : -1);
+        } else {  // CLF rows (:72-82; :47-69): +Ac u <= -Bc, slack i
+            for (int i = 0; i < N - 1; i++) {
+                const double* nb = states + 6 * (i + (i >= self ? 1 : 0));
+                double a[3], b;
+                orc::clf_row(st, nb, a, &b);
+                add_row(a, -b, slack_mode ? i : -1);
+            }
+        }
+        q.vlo.assign(n, 0.0);  // slack variables [0, max)
+        q.vhi.assign(n, std::numeric_limits<double>::infinity());
+        for (int d = 0; d < 3; d++) {  // control inputs: free (addVariable() defaults)
+            q.vlo[d] = -std::numeric_limits<double>::infinity();
+            q.vhi[d] = std::numeric_limits<double>::infinity();
+        }
+        orc::Solution r = orc::solve(q);
+        for (int d = 0; d < 3; d++) u_out[d] = (int)r.x.size() == n ? r.x[d] : 0.0;
+        if (obj_out) *obj_out = r.obj;
+        return r.status;
+    } catch (...) {
+        return ORC_ERROR;
+    }
+}
+
+}  // extern "C"

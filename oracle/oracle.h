@@ -153,6 +153,22 @@ int orc_fov_control_slack(double fov, double Ds, double Rs, const double* vmin3,
                           const double* desired_u3, int32_t num_neighbors, const double* nb_xy,
                           int32_t slack_mode, double slack_cost, double slack_decay,
                           const double* nb_cov, double* u_out3, double* obj_out);
+/* ---- ConnectivityControl (cbf/src/controller/ConnectivityControl.cpp:22-99) ----
+ * orc_lambda2: ConnectivityCBF::getLambda2 (:375-414): lambda2 and the unit Fiedler vector of
+ * the weighted Laplacian of N planar positions (pos2: N x 2). orc_conn_cbf: the connectivity
+ * HOCBF row of robot self (Ac over (ux, uy, uw) and Bc, :430-512; dbg7 = grad x, grad y, Hxx,
+ * Hxy, Hyy, Lf h, Lf^2 h, or NULL). orc_clf_cbf: the connectivity CLF row (:200-243).
+ * orc_connectivity_control: the whole CBF-only QP of robot self (states: N x 6), solved densely;
+ * u free (the control bounds are commented out in the reference), N slack variables in slack
+ * mode with weights slack_cost * decay^i. Returns the status; l2_out gets lambda2. */
+void orc_lambda2(int32_t N, const double* pos2, double dmax, double* l2, double* vec);
+void orc_conn_cbf(int32_t N, const double* states, int32_t self, const double* eigvec,
+                  double lambda2, double dmax, double* a3, double* b, double* dbg7);
+void orc_clf_cbf(const double* state6, const double* neighbor6, double* a3, double* b);
+int orc_connectivity_control(double dmin, double dmax, const double* vmin3, const double* vmax3,
+                             int32_t slack_mode, double slack_cost, double slack_decay, int32_t N,
+                             const double* states, int32_t self, const double* desired_u3,
+                             double* u_out3, double* obj_out, double* l2_out);
 int orc_eval_curve(const orc_params* p, const double* x, double t, int32_t deriv, double* out3);
 
 #ifdef __cplusplus

@@ -6,12 +6,34 @@ Sources (paths under workspace/lib of ywang760/mpc-cbf @ 2025-08-29):
   qpcpp/tests/CPLEXTest.cpp:28-56          min x^2 + y^2 s.t. x + y >= 1 -> x = y = 0.5
   model/tests/DoubleIntegratorXYYawTest.cpp:19-47  applyInput with ts = 0.1
   math/tests/CombinatoricsTest.cpp:17-63   fac / comb / perm
+  cbf/tests/TestInitConnectivity.cpp:103-153  connectivity (lambda2) CBF Ac/Bc, d_max 3.0;
+      the intermediate values (lambda2, grad h, Hessian, Lf h, Lf^2 h) are the ones the same
+      test run printed, cbf/tests/results.log:7-128 (a data file the reference's tests hold)
 Run:  python tests/golden/make_reference_kats.py
 """
 import json
 import os
 
 KATS = {
+    "connectivity_cbf": {
+        "source": "cbf/tests/TestInitConnectivity.cpp:103-153, cbf/tests/results.log:7-128",
+        "d_min": 0.8, "d_max": 3.0, "lambda2_min": 0.1,
+        "tolerance_Ac": 1e-6, "Bc_check": "EXPECT_DOUBLE_EQ (4 ulp)",
+        "cases": [
+            {"name": "Misc", "self": 0,
+             "robot_states": [[1.0, 2.0, 0, 0, 0, 0], [1.0, 4.0, 0, 0, 0, 0], [1.0, 6.0, 0, 0, 0, 0]],
+             "Ac": [0.0, -2.703392, 0.0], "Bc": 3.4635324630258153,
+             "log_lambda2": 0.23854129852103262, "log_grad_h": [0.0, -2.703392],
+             "log_hessian": [[0.622855, 0.0], [0.0, 6.990999]], "log_Lfh": 0.0, "log_Lf2h": 0.0},
+            {"name": "Misc2", "self": 0,
+             "robot_states": [[0.212, 1.592, 0, -0.293, -0.21, 0.0], [1.01, 4.20, 0, -1.2, 0.12, 0],
+                              [-1.0, -0.02, 0, -0.2, 0.16, 0]],
+             "Ac": [0.061292, 0.201971, 0.0], "Bc": -2.2784138163109593,
+             "log_lambda2": 0.030874640699123754, "log_grad_h": [0.061292, 0.201971],
+             "log_hessian": [[-0.011820, 0.217050], [0.217050, 0.629234]],
+             "log_Lfh": -0.0603724539485257, "log_Lf2h": 0.05344470569620386},
+        ],
+    },
     "safety_cbf": {
         "source": "cbf/tests/TestInitSafetyCBF.cpp:50-143",
         "d_min": 0.8,

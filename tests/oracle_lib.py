@@ -82,6 +82,14 @@ def lib():
         L.orc_fov_control_slack.argtypes = [C.c_double, C.c_double, C.c_double, dp, dp, dp, dp,
                                             dp, dp, C.c_int32, dp, C.c_int32, C.c_double,
                                             C.c_double, dp, dp, dp]
+        L.orc_lambda2.argtypes = [C.c_int32, dp, C.c_double, dp, dp]
+        L.orc_lambda2.restype = None
+        L.orc_conn_cbf.argtypes = [C.c_int32, dp, C.c_int32, dp, C.c_double, C.c_double, dp, dp, dp]
+        L.orc_conn_cbf.restype = None
+        L.orc_clf_cbf.argtypes = [dp, dp, dp, dp]
+        L.orc_clf_cbf.restype = None
+        L.orc_connectivity_control.argtypes = [C.c_double, C.c_double, dp, dp, C.c_int32, C.c_double,
+                                               C.c_double, C.c_int32, dp, C.c_int32, dp, dp, dp, dp]
         L.orc_fov_control.argtypes = [C.c_double, C.c_double, C.c_double, dp, dp, dp, dp, dp, dp,
                                       C.c_int32, dp, dp, dp]
         L.orc_num_vars.argtypes = [C.POINTER(OrcParams), C.c_int32]
@@ -278,3 +286,46 @@ def eval_curve(p: OrcParams, x, t, d):
     if rc != 0:
         raise ValueError("eval out of range")
     return out
+
+
+def lambda2(pos2, dmax):
+    """ConnectivityCBF::getLambda2: (lambda2, unit Fiedler vector)."""
+    pos = np.ascontiguousarray(np.reshape(pos2, (-1, 2)), dtype=np.float64)
+    l2 = np.zeros(1)
+    v = np.zeros(len(pos))
+    lib().orc_lambda2(len(pos), _d(pos), float(dmax), _d(l2), _d(v))
+    return float(l2[0]), v
+
+
+def conn_cbf(states, self_idx, eigvec, l2, dmax):
+    """Connectivity CBF row of robot self_idx: (Ac (3,), Bc, [gx, gy, Hxx, Hxy, Hyy, Lfh, Lf2h])."""
+    st = np.ascontiguousarray(states, dtype=np.float64)
+    a = np.zeros(3)
+    b = np.zeros(1)
+    dbg = np.zeros(7)
+    lib().orc_conn_cbf(len(st), _d(st), int(self_idx), _d(eigvec), float(l2), float(dmax), _d(a),
+                       _d(b), _d(dbg))
+    return a, float(b[0]), dbg
+
+
+def clf_cbf(state, neighbor):
+    a = np.zeros(3)
+    b = np.zeros(1)
+    lib().orc_clf_cbf(_d(state), _d(neighbor), _d(a), _d(b))
+    return a, float(b[0])
+
+
+def connectivity_control(cfg: dict, states, self_idx, desired_u):
+    """ConnectivityControl::optimize restated: (status, u (3,), objective, lambda2). cfg keys:
+    d_min, d_max, v_min, v_max, control_slack_mode, slack_cost, slack_decay_rate."""
+    st = np.ascontiguousarray(states, dtype=np.float64)
+    u = np.zeros(3)
+    obj = np.zeros(1)
+    l2 = np.zeros(1)
+    f = lambda v: np.ascontiguousarray(v, dtype=np.float64)  # noqa: E731
+    stt = lib().orc_connectivity_control(
+        float(cfg["d_min"]), float(cfg["d_max"]), _d(f(cfg["v_min"])), _d(f(cfg["v_max"])),
+        int(cfg.get("control_slack_mode", 0)), float(cfg.get("slack_cost", 0.0)),
+        float(cfg.get("slack_decay_rate", 1.0)), len(st), _d(st), int(self_idx), _d(f(desired_u)),
+        _d(u), _d(obj), _d(l2))
+    return stt, u, float(obj[0]), float(l2[0])
