@@ -262,6 +262,42 @@ typedef struct mpccbf_fov_control_batch {
 int mpccbf_fov_control_solve(const mpccbf_fov_control_params* p, const mpccbf_fov_control_batch* b,
                              int32_t device, void* hip_stream);
 
+/* ---- Batched CBF-only connectivity controller (ConnectivityControl::optimize,
+ * cbf/src/controller/ConnectivityControl.cpp:22-99) for teams of robots ----------------------
+ * Per robot of a team (<= 16 robots; robots of team t are rows team_ptr[t] .. team_ptr[t+1]-1):
+ * min ||u - u_des||^2 over u (3) subject to the safety CBF rows against every other team member
+ * (ConnectivityCBF.cpp:152-198, d_min, cubic alpha), the velocity CBF rows (:250-286) and, when the
+ * team's algebraic connectivity lambda2 (weighted Laplacian, :375-414, d_max) exceeds 0.1, the
+ * connectivity CBF row (:430-512), else one CLF row per other member (:200-243). u is unbounded
+ * (the reference's addControlBoundConstraint is commented out, :60). slack_mode: num_robots slack
+ * variables, weights slack_cost * decay^i (:31-38); neighbour i's safety / CLF rows take slack i,
+ * the connectivity row the last one. All pointers are device pointers; asynchronous. */
+typedef struct mpccbf_connectivity_control_params {
+    double d_min, d_max;
+    double v_min[3], v_max[3];
+    int32_t slack_mode;
+    double slack_cost, slack_decay_rate;
+    int32_t max_pdip_iters;   /* default 60 */
+    double tolerance;         /* default 1e-9 */
+} mpccbf_connectivity_control_params;
+
+typedef struct mpccbf_connectivity_control_batch {
+    int32_t num_teams;
+    const int32_t* team_ptr;   /* num_teams + 1 offsets into the robot rows */
+    const double* states;      /* robots x 6 (x, y, yaw, vx, vy, w) */
+    const double* desired_u;   /* robots x 3 */
+    double* u;                 /* out, robots x 3 (NaN when not OPTIMAL) */
+    int32_t* status;           /* out, robots (qpcpp::SolveStatus), or NULL */
+    double* obj;               /* out, ||u - u_des||^2 (+ slack cost), or NULL */
+    int32_t* iters;            /* out, PDIP iterations, or NULL */
+    double* lambda2;           /* out, num_teams, or NULL */
+} mpccbf_connectivity_control_batch;
+
+/* A team with more than 16 robots gets status MPCCBF_ERROR for all its robots. */
+int mpccbf_connectivity_control_solve(const mpccbf_connectivity_control_params* p,
+                                      const mpccbf_connectivity_control_batch* b, int32_t device,
+                                      void* hip_stream);
+
 /* Generic dense QP in the flattened CPLEX form (host pointers; synchronous):
  *   minimise  x^T H x + c^T x + c0        (H symmetric: sum_{i<=j} q_ij x_i x_j, CPLEX.cpp:122-147)
  *   s.t.      lo_r <= A_r x <= hi_r       (rows; lo == hi is an equality)

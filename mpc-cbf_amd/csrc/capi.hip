@@ -498,6 +498,53 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
 
 extern "C" {
 
+int mpccbf_connectivity_control_solve(const mpccbf_connectivity_control_params* p,
+                                      const mpccbf_connectivity_control_batch* b, int32_t device,
+                                      void* stream) {
+    if (!p || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    if (!(p->d_min > 0.0) || !(p->d_max > 0.0))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "d_min and d_max must be positive");
+    for (int d = 0; d < 3; d++)
+        if (!(p->v_min[d] <= p->v_max[d])) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "v_min must not exceed v_max");
+    if (p->slack_mode && !(p->slack_cost > 0.0))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "Slack cost must be positive when slack_mode is enabled");
+    if (p->slack_mode && !(p->slack_decay_rate > 0.0 && p->slack_decay_rate <= 1.0))
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "Slack decay rate must be in (0,1] when slack_mode is enabled");
+    if (b->num_teams < 0) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "num_teams < 0");
+    if (b->num_teams == 0) return MPCCBF_OK;
+    if (!b->team_ptr || !b->states || !b->desired_u || !b->u)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "team_ptr, states, desired_u and u are required");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
+    HIP_TRY(hipSetDevice(device));
+    ConnControlArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.num_teams = b->num_teams;
+    a.team_ptr = b->team_ptr;
+    a.states = b->states;
+    a.desired_u = b->desired_u;
+    a.u = b->u;
+    a.status = b->status;
+    a.obj = b->obj;
+    a.iters = b->iters;
+    a.lambda2 = b->lambda2;
+    a.dmin = p->d_min;
+    a.dmax = p->d_max;
+    for (int d = 0; d < 3; d++) {
+        a.vmin[d] = p->v_min[d];
+        a.vmax[d] = p->v_max[d];
+    }
+    a.maxit = p->max_pdip_iters > 0 ? p->max_pdip_iters : 60;
+    a.tol = p->tolerance > 0.0 ? p->tolerance : 1e-9;
+    a.feas_tol = 1e-6;
+    a.slack_mode = p->slack_mode ? 1 : 0;
+    a.slack_cost = p->slack_cost;
+    a.slack_decay = p->slack_decay_rate;
+    HIP_TRY(launch_connectivity_control(a, (hipStream_t)stream));
+    return MPCCBF_OK;
+}
+
 int mpccbf_fov_control_solve(const mpccbf_fov_control_params* p, const mpccbf_fov_control_batch* b,
                              int32_t device, void* stream) {
     if (!p || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");

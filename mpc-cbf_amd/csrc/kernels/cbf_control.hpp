@@ -28,6 +28,27 @@ struct FovControlArgs {
     const double* nb_cov;  // per observed neighbour (cxx, cxy, cyy), or nullptr (unknown)
 };
 
+// ConnectivityControl::optimize for a batch of teams (connectivity_control.hip)
+struct ConnControlArgs {
+    int32_t num_teams;
+    const int32_t* team_ptr;    // num_teams + 1
+    const double* states;       // robots x 6
+    const double* desired_u;    // robots x 3
+    double* u;                  // robots x 3 (NaN rows: not OPTIMAL)
+    int32_t* status;
+    double* obj;
+    int32_t* iters;
+    double* lambda2;            // num_teams, or nullptr
+    double dmin, dmax;
+    double vmin[3], vmax[3];
+    int32_t maxit;
+    double tol, feas_tol;
+    int32_t slack_mode;
+    double slack_cost, slack_decay;
+};
+
+hipError_t launch_connectivity_control(const ConnControlArgs& a, hipStream_t s);
+
 constexpr int FOV_CONTROL_ROW_CAP = 4 * 16;  // rows per agent (R = 4 slots x 16 lanes)
 
 hipError_t launch_fov_control(const FovControlArgs& a, hipStream_t s);

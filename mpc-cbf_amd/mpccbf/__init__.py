@@ -8,5 +8,6 @@ from ._lib import (  # noqa: F401
     LIB_PATH, MpccbfError, Params, Options, Context, status_name, build_library, load,
     dense_qp_solve, dense_qp_solve_batch, STATUS_NAMES, OPTIMAL, FEASIBLE, UNBOUNDED, INFEASIBLE, ERROR, UNKNOWN,
     INFEASIBLEORUNBOUNDED, Comm, comm_unique_id, fov_control_solve, fov_control_params,
+    connectivity_control_solve,
 )
 from . import swarm  # noqa: F401

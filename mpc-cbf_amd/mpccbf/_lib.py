@@ -20,7 +20,8 @@ EXPORTED = [
     "mpccbf_num_shared_rows", "mpccbf_impc_solve", "mpccbf_set_variant", "mpccbf_build_neighbors",
     "mpccbf_qp_solve_dense", "mpccbf_qp_solve_dense_batch", "mpccbf_last_error",
     "mpccbf_status_string", "mpccbf_abi_version", "mpccbf_run_steps", "mpccbf_comm_unique_id",
-    "mpccbf_comm_create", "mpccbf_comm_destroy", "mpccbf_kernel_name",
+    "mpccbf_comm_create", "mpccbf_comm_destroy", "mpccbf_kernel_name", "mpccbf_fov_control_solve",
+    "mpccbf_connectivity_control_solve", "mpccbf_host_operators", "mpccbf_host_last_error",
 ]
 
 
@@ -411,6 +412,38 @@ def fov_control_solve(cfg: dict, states, desired_u, nb_row_ptr, nb_xy, u, status
                         status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters), nb_cov=_ptr(nb_cov))
     p = fov_control_params(cfg)
     _check(load().mpccbf_fov_control_solve(C.byref(p), C.byref(b), device, _stream(stream)))
+
+
+class ConnControlParams(C.Structure):
+    _fields_ = [("d_min", C.c_double), ("d_max", C.c_double), ("v_min", C.c_double * 3),
+                ("v_max", C.c_double * 3), ("slack_mode", C.c_int32), ("slack_cost", C.c_double),
+                ("slack_decay_rate", C.c_double), ("max_pdip_iters", C.c_int32),
+                ("tolerance", C.c_double)]
+
+
+class ConnControlBatch(C.Structure):
+    _fields_ = [("num_teams", C.c_int32), ("team_ptr", C.c_void_p), ("states", C.c_void_p),
+                ("desired_u", C.c_void_p), ("u", C.c_void_p), ("status", C.c_void_p),
+                ("obj", C.c_void_p), ("iters", C.c_void_p), ("lambda2", C.c_void_p)]
+
+
+def connectivity_control_solve(cfg: dict, team_ptr, states, desired_u, u, status=None, obj=None,
+                               iters=None, lambda2=None, device: int = 0, stream=None):
+    """Batched ConnectivityControl::optimize (mpccbf_connectivity_control_solve) for teams of
+    robots (team t = rows team_ptr[t] .. team_ptr[t+1]-1 of states / desired_u). cfg keys: d_min,
+    d_max, v_min, v_max, control_slack_mode, slack_cost, slack_decay_rate."""
+    p = ConnControlParams()
+    p.d_min, p.d_max = cfg["d_min"], cfg["d_max"]
+    for d in range(3):
+        p.v_min[d], p.v_max[d] = cfg["v_min"][d], cfg["v_max"][d]
+    p.slack_mode = int(cfg.get("control_slack_mode", 0))
+    p.slack_cost = cfg.get("slack_cost", 0.0)
+    p.slack_decay_rate = cfg.get("slack_decay_rate", 1.0)
+    b = ConnControlBatch(num_teams=team_ptr.shape[0] - 1, team_ptr=_ptr(team_ptr),
+                         states=_ptr(states), desired_u=_ptr(desired_u), u=_ptr(u),
+                         status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters),
+                         lambda2=_ptr(lambda2))
+    _check(load().mpccbf_connectivity_control_solve(C.byref(p), C.byref(b), device, _stream(stream)))
 
 
 def comm_unique_id() -> bytes:

@@ -1808,7 +1808,24 @@ int orc_connectivity_control(double dmin, double dmax, const double* vmin3, cons
         }
         orc::Solution r = orc::solve(q);
         for (int d = 0; d < 3; d++) u_out[d] = (int)r.x.size() == n ? r.x[d] : 0.0;
-        if (obj_out) *obj_out = r.obj;
+        double obj = r.obj;
+        if (ns > 0 && r.status == ORC_OPTIMAL) {
+            // slack polish: at the optimum v_i = max(0, max over its rows of g u - h) exactly.
+            // The dense solve's v carries its tolerance relative to the rows' bounds, which reach
+            // 1e6 here (safety Bc); with weights up to 1e5 that is visible in the objective.
+            std::vector<double> v(ns, 0.0);
+            for (int row = 0; row < q.m; row++)
+                for (int i = 0; i < ns; i++)
+                    if (q.A[(size_t)row * n + 3 + i] == -1.0) {
+                        double gu = 0.0;
+                        for (int d = 0; d < 3; d++) gu += q.A[(size_t)row * n + d] * u_out[d];
+                        v[i] = std::max(v[i], gu - q.hi[row]);
+                    }
+            obj = q.c0;
+            for (int d = 0; d < 3; d++) obj += u_out[d] * u_out[d] + q.c[d] * u_out[d];
+            for (int i = 0; i < ns; i++) obj += q.c[3 + i] * v[i];
+        }
+        if (obj_out) *obj_out = obj;
         return r.status;
     } catch (...) {
         return ORC_ERROR;

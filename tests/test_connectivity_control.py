@@ -122,3 +122,71 @@ def test_oracle_connectivity_control_branches(oracle):
             if st == O.OPTIMAL:
                 assert obj2 <= obj + 1e-6 * max(1.0, abs(obj))
     assert seen == {True, False}
+
+
+def _teams(sizes, seed):
+    """Teams of the given sizes, alternating tight (lambda2 row) and spread-out (CLF rows)."""
+    S_all, U_all, ptr = [], [], [0]
+    for t, n in enumerate(sizes):
+        S, ud = _team(n, seed + t, 1.0 if t % 2 == 0 else 5.0)
+        S_all.append(S)
+        U_all.append(ud)
+        ptr.append(ptr[-1] + n)
+    return np.vstack(S_all), np.vstack(U_all), np.array(ptr, dtype=np.int32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("slack", [False, True])
+def test_gpu_connectivity_control_matches_oracle(mpclib, slack):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a visible MI355X")
+    sizes = [2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 6, 6, 6, 3, 16]
+    S, ud, ptr = _teams(sizes, 11)
+    cfg = _cfg(slack)
+    dev = torch.device("cuda", 0)
+    t = lambda v, dt=torch.float64: torch.tensor(v, dtype=dt, device=dev)  # noqa: E731
+    R = len(S)
+    u = torch.empty((R, 3), dtype=torch.float64, device=dev)
+    status = torch.empty(R, dtype=torch.int32, device=dev)
+    obj = torch.empty(R, dtype=torch.float64, device=dev)
+    l2 = torch.empty(len(sizes), dtype=torch.float64, device=dev)
+    mpclib.connectivity_control_solve(cfg, t(ptr, torch.int32), t(S), t(ud), u, status=status, obj=obj,
+                                      lambda2=l2)
+    torch.cuda.synchronize()
+    u, status, obj, l2 = u.cpu().numpy(), status.cpu().numpy(), obj.cpu().numpy(), l2.cpu().numpy()
+    branches = set()
+    n_opt = 0
+    for k in range(len(sizes)):
+        Sk = S[ptr[k]:ptr[k + 1]]
+        lref, _ = O.lambda2(Sk[:, :2], cfg["d_max"])
+        assert abs(l2[k] - lref) <= 1e-10 * max(1.0, abs(lref)), (k, l2[k], lref)
+        branches.add(lref > 0.1)
+        for i in range(len(Sk)):
+            r = ptr[k] + i
+            st, ur, objr, _ = O.connectivity_control(cfg, Sk, i, ud[r])
+            assert status[r] == st, (k, i, status[r], st)
+            if st == O.OPTIMAL:
+                n_opt += 1
+                np.testing.assert_allclose(u[r], ur, atol=1e-5, rtol=1e-5)
+                assert abs(obj[r] - objr) <= 1e-4 * max(1.0, abs(objr)), (k, i, obj[r], objr)
+    assert branches == {True, False}
+    assert n_opt >= 20  # the rest: safety rows against close, fast neighbours are infeasible
+    if slack:
+        assert np.all(status == O.OPTIMAL)
+
+
+@pytest.mark.gpu
+def test_gpu_connectivity_control_team_too_large(mpclib):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a visible MI355X")
+    S, ud, ptr = _teams([17, 3], 2)
+    dev = torch.device("cuda", 0)
+    t = lambda v, dt=torch.float64: torch.tensor(v, dtype=dt, device=dev)  # noqa: E731
+    u = torch.empty((len(S), 3), dtype=torch.float64, device=dev)
+    status = torch.empty(len(S), dtype=torch.int32, device=dev)
+    mpclib.connectivity_control_solve(_cfg(), t(ptr, torch.int32), t(S), t(ud), u, status=status)
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()
+    assert np.all(st[:17] == O.ERROR) and np.all(st[17:] != O.ERROR)
