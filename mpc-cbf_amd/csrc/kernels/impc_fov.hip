@@ -26,8 +26,7 @@ constexpr int FOV_NB_CAP = 16;  // observed neighbours per agent
 // LDS of the slack rows (slack mode only)
 struct FovSlackLds {
     double Go[WSL_ROWS * WNZ];
-    double Gc[WSL_CROWS * WNZ];
-    double Dvs[WSL_CROWS], wvs[WSL_CROWS], cvs[WSL_CROWS], zvs[WSL_ROWS];
+    double zvs[WSL_ROWS];
     double h[WSL_ROWS], live[WSL_ROWS];
     double Tn[WSL_NB], w[WSL_NB], dist[WSL_NB];
     int32_t order[WSL_NB];
@@ -181,12 +180,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             // slack mode: neighbour i's rows go to lanes 8 i .. 8 i + 7 of the slack images
             // (WaveSlack), uncompacted; every row starts inert, pads stay zero
             for (int e = lane; e < WSL_ROWS * WNZ; e += 64) slk->Go[e] = 0.0;
-            for (int e = lane; e < WSL_CROWS * WNZ; e += 64) slk->Gc[e] = 0.0;
-            for (int e = lane; e < WSL_CROWS; e += 64) {
-                slk->Dvs[e] = 0.0;
-                slk->wvs[e] = 0.0;
-                slk->cvs[e] = 0.0;
-            }
             slk->zvs[lane] = 0.0;
             slk->h[lane] = 1.0;
             slk->live[lane] = 0.0;
@@ -258,17 +251,25 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         row_infeasible = __ballot(row_infeasible) != 0ull;
         const int mtot = base + count;
         const int nchunk = ((mtot + 15) / 16) * 4;  // whole groups of 4 chunks (WCH = 48 is one)
-        // zero the image rows that complete the last chunk
-        for (int r = mtot + lane; r < 4 * nchunk && r < WROWS; r += 64)
+        // zero the image rows that complete the last chunk; slack mode: also the slack image
+        // (centred + mean rows, WSL_CROWS from row 4 nchunk) and its weights
+        const int zend = SLACK ? 4 * nchunk + WSL_CROWS : 4 * nchunk;
+        for (int r = mtot + lane; r < zend && r < WROWS; r += 64) {
 #pragma unroll
             for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = 0.0;
+            if (SLACK && r >= 4 * nchunk) {
+                sc.Dv[r] = 0.0;
+                sc.wv[r] = 0.0;
+                sc.cv[r] = 0.0;
+            }
+        }
         if (lane < WNZ) sc.q[lane] = q_s[lane];
         wave_lds_sync();
         if (it < 2) stamp(args, ai, lane, 3 + 2 * it);
         int st;
         int nit = 0;
         double vobj = 0.0;  // slack mode: sum_i w_i v_i (addSlackCost, MPCCBFQPGeneratorBase.cpp:121-130)
-        if (mtot > WROWS || nb_overflow) {
+        if (mtot > WROWS || nb_overflow || (SLACK && 4 * nchunk + WSL_CROWS > WROWS)) {
             st = ST_ERROR;  // capacity (rows per agent / observed neighbours)
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
@@ -298,10 +299,11 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             if constexpr (SLACK) {
                 wave_lds_sync();  // the slack rows written above
                 sk.Go = slk->Go;
-                sk.Gc = slk->Gc;
-                sk.Dvs = slk->Dvs;
-                sk.wvs = slk->wvs;
-                sk.cvs = slk->cvs;
+                sk.coff = 4 * nchunk;
+                sk.Gc = Gimg + (size_t)sk.coff * WNZ;
+                sk.Dvs = sc.Dv + sk.coff;
+                sk.wvs = sc.wv + sk.coff;
+                sk.cvs = sc.cv + sk.coff;
                 sk.zvs = slk->zvs;
                 sk.Tn = slk->Tn;
                 sk.nnb = nnb;

@@ -162,8 +162,12 @@ constexpr int WSL_CROWS = 80;             // centred rows + mean rows, padded to
 
 struct WaveSlack {
     const double* Go;  // WSL_ROWS x 16 original slack rows (LDS; rows >= 8 nnb zero up to the 16-row pad)
-    double* Gc;        // WSL_CROWS x 16: centred rows (8 i + a), mean rows (8 nnb + i), zero pad
-    double* Dvs;       // Gc row weights: Gram, right-hand side (column 15), G^T v
+    // The centred rows (8 i + a) and mean rows (8 nnb + i) sit in the main row image right after
+    // the ordinary rows, at image row coff (a multiple of 16), so one MFMA Gram chain and one
+    // G^T v cover both; Dvs / wvs / cvs alias the WaveScratch weight arrays at coff.
+    int coff;
+    double* Gc;
+    double* Dvs;
     double* wvs;
     double* cvs;
     double* zvs;       // z of the Go rows (dual residual)
@@ -424,9 +428,11 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             iu[s] = rcp(su[s]);
             const double Dl = zl[s] * il[s], Du = zu[s] * iu[s];
             const int r = wave_owner_row(lane, s);
-            sc.Dv[r] = Dl + Du;
-            sc.wv[r] = Du * ru[s] - Dl * rl[s];
-            sc.cv[r] = zu[s] - zl[s];
+            if (!SLK || r < skp->coff) {  // (slack mode: rows past coff are the slack image's)
+                sc.Dv[r] = Dl + Du;
+                sc.wv[r] = Du * ru[s] - Dl * rl[s];
+                sc.cv[r] = zu[s] - zl[s];
+            }
             mloc = fma(sl[s], zl[s], fma(su[s], zu[s], mloc));
             rp = fmax(rp, fmax(fabs(rl[s]) * pl[s], fabs(ru[s]) * pu[s]));
         }
@@ -466,8 +472,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         }
         PSTAMP(1);
         wave_lds_sync();
-        wd4 acc = wave_gram(Gs, sc.Dv, sc.wv, nchunk, lane);
-        if constexpr (SLK) acc += wave_gram(skp->Gc, skp->Dvs, skp->wvs, skp->nchunk_c, lane);
+        const wd4 acc = wave_gram(Gs, sc.Dv, sc.wv, nchunk + (SLK ? skp->nchunk_c : 0), lane);
         double Mr[WNZ];
         gram_rows(acc, sc.M, lane, Mr);
         const double rhs_i = Mr[WNZ - 1];  // G^T w (column 15)
@@ -606,7 +611,8 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         for (int s = 0; s < WR; s++) {
             kl[s] = rw.ml[s] * (smu - dsl[s] * dzl[s]);
             ku[s] = smu - dsu[s] * dzu[s];
-            sc.cv[wave_owner_row(lane, s)] = kl[s] * il[s] - ku[s] * iu[s];
+            const int r = wave_owner_row(lane, s);
+            if (!SLK || r < skp->coff) sc.cv[r] = kl[s] * il[s] - ku[s] * iu[s];
         }
         // slack rows: row weights om = -kc / s on the centred rows; the mean row takes
         // (Db sum om + T kb / sb) / S; the v equation keeps vcv = -sum om + kb / sb
@@ -623,8 +629,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             if (lead) sk.cvs[8 * sk.nnb + (lane >> 3)] = fma(sDb, som, sT * skb * isb) * siS;
         }
         wave_lds_sync();
-        double vc_i = wave_gt(Gs, sc.cv, nchunk, lane);
-        if constexpr (SLK) vc_i += wave_gt(skp->Gc, skp->cvs, skp->nchunk_c, lane);
+        const double vc_i = wave_gt(Gs, sc.cv, nchunk + (SLK ? skp->nchunk_c : 0), lane);
         PSTAMP(7);
         const double dy_i = dya_i + solve_rows(L, sc.M, inv_i, vc_i, i);
         publish16(sc.d, dy_i, lane);

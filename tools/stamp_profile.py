@@ -20,8 +20,10 @@ WARM = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 VARIANTS = [int(v) for v in sys.argv[3:]] or [0, 3]
 PH = ["setup", "neighbours", "cbf_rows0", "solve0", "cbf_rows1", "solve1", "outputs"]
 FOV = os.environ.get("WORKLOAD", "") == "fov"
+SLACK = os.environ.get("SLACK", "") == "1"
+COV = None
 if FOV:
-    cfg = swarm.fov_config(20)
+    cfg = swarm.fov_config(20, **(dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.9) if SLACK else {}))
     states_h, targets_h = swarm.heading_swarm(N)
     states_h[:, :2] *= float(os.environ.get("SCALE", "1.0"))
 else:
@@ -33,8 +35,10 @@ tg = torch.tensor(targets_h, device=dev)
 radius = cfg["fov_Rs"] if FOV else 3.0 * cfg["d_min"]
 ctx = Context(cfg)
 out = ctx.alloc_outputs(N)
+if FOV and SLACK:
+    COV = torch.tensor(np.tile([0.1, 0.0, 0.1], (N, 1)), device=dev)
 for _ in range(WARM):
-    ctx.impc_solve(st, targets=tg, knn_k=8, knn_radius=radius, **out)
+    ctx.impc_solve(st, targets=tg, knn_k=8, knn_radius=radius, cov=COV, **out)
     st.copy_(out["next_states"])
 torch.cuda.synchronize()
 snap = st.clone()
@@ -47,7 +51,7 @@ for v in VARIANTS:
     ctx.set_variant(v)
     stamps = torch.zeros(N * 8 + (N * 16 if PDIP else 0), dtype=torch.int64, device=dev)
     for rep in range(3):  # last rep measured (warm caches)
-        ctx.impc_solve(snap, targets=tg, knn_k=8, knn_radius=radius, stamps=stamps, **out)
+        ctx.impc_solve(snap, targets=tg, knn_k=8, knn_radius=radius, stamps=stamps, cov=COV, **out)
     torch.cuda.synchronize()
     allst = stamps.cpu().numpy()
     s = allst[:N * 8].reshape(N, 8).astype(np.float64) * 0.01  # 10 ns ticks -> us
