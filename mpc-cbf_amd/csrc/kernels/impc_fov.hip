@@ -27,6 +27,7 @@ constexpr int FOV_NB_CAP = 16;  // observed neighbours per agent
 struct FovSlackLds {
     double Go[WSL_ROWS * WNZ];
     double zvs[WSL_ROWS];
+    double st[WSL_NST * 64];  // per-lane slack solver state (WaveSlack::st)
     double h[WSL_ROWS], live[WSL_ROWS];
     double Tn[WSL_NB], w[WSL_NB], dist[WSL_NB];
     int32_t order[WSL_NB];
@@ -306,6 +307,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 sk.cvs = sc.cv + sk.coff;
                 sk.zvs = slk->zvs;
                 sk.Tn = slk->Tn;
+                sk.st = slk->st;
                 sk.nnb = nnb;
                 sk.nchunk_c = ((9 * nnb + 15) / 16) * 4;
                 sk.nchunk_o = ((8 * nnb + 15) / 16) * 4;

@@ -177,7 +177,11 @@ struct WaveSlack {
     int nchunk_o;      // chunks of Go in use (multiple of 4)
     double h, live;    // this lane's row: bound, 1 if live (0: inert)
     double w;          // slack cost of this lane's neighbour
+    double* st;        // WSL_NST x 64 per-lane solver state in LDS (keeps the registers for the
+                       // Newton matrix, factor and solves; the slack state is touched a few times
+                       // per step)
 };
+constexpr int WSL_NST = 24;
 
 // sum over the 8-lane segment (row_half_mirror pairs the two quads of each half-row)
 __device__ __forceinline__ double seg8_sum(double v) {
@@ -389,7 +393,12 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
     // near the optimum), row slacks from the residual.
     const bool son = SLK && (lane >> 3) < (SLK ? skp->nnb : 0);
     const bool lead = son && (lane & 7) == 0;  // counts the neighbour's bound once in sums
-    double v = 1.0, sb = 1.0, zb = 1.0, cs = 1.0, cz = 1.0, pc = 1.0, slh = 1.0, sliv = 0.0, slw = 0.0;
+    double lst_dummy[WSL_NST];  // (non-slack instantiation: never touched)
+    double* const lst = SLK ? skp->st + lane : lst_dummy;
+    constexpr int lsd = SLK ? 64 : 1;
+    double &v = lst[0 * lsd], &sb = lst[1 * lsd], &zb = lst[2 * lsd], &cs = lst[3 * lsd],
+           &cz = lst[4 * lsd], &pc = lst[5 * lsd], &slh = lst[6 * lsd], &sliv = lst[7 * lsd],
+           &slw = lst[8 * lsd];
     if constexpr (SLK) {
         const WaveSlack& sk = *skp;
         slh = son ? sk.h : 1.0;
@@ -439,7 +448,8 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         // slack rows: residual cr = h - g y + v - s, D = z / s; per neighbour T = sum D (live),
         // S = T + Db; weights of the centred rows and of the mean row (predictor right-hand side
         // phi = D cr, v-equation term -(Db rb + w))
-        double scr = 0.0, sci = 1.0, sD = 0.0, sT = 0.0, siS = 1.0, sDb = 0.0, srb = 0.0;
+        double &scr = lst[9 * lsd], &sci = lst[10 * lsd], &sD = lst[11 * lsd], &sT = lst[12 * lsd],
+               &siS = lst[13 * lsd], &sDb = lst[14 * lsd], &srb = lst[15 * lsd];
         if constexpr (SLK) {
             const WaveSlack& sk = *skp;
             const double t = son ? dotl(sk.Go + lane * WNZ, sc.y) : 0.0;
@@ -570,7 +580,9 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             rz = fmax(rz, fmax(rw.ml[s] * (1.0 + ql), 1.0 + qu));
         }
         // slack rows: dv = (sum_a D_a (g_a dy - cr_a) - Db rb - w) / S, ds = cr - g dy + dv
-        double sds = 0.0, sdz = 0.0, sdv = 0.0, sdsb = 0.0, sdzb = 0.0;
+        double &sds = lst[16 * lsd], &sdz = lst[17 * lsd], &sdv = lst[18 * lsd], &sdsb = lst[19 * lsd],
+               &sdzb = lst[20 * lsd];
+        if constexpr (SLK) sdsb = sdzb = 0.0;
         if constexpr (SLK) {
             const double td = son ? dotl(skp->Go + lane * WNZ, sc.d) : 0.0;
             const double sd = seg8_sum(sliv * sD * (td - scr));
@@ -616,7 +628,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         }
         // slack rows: row weights om = -kc / s on the centred rows; the mean row takes
         // (Db sum om + T kb / sb) / S; the v equation keeps vcv = -sum om + kb / sb
-        double skc = 0.0, skb = 0.0, svcv = 0.0;
+        double &skc = lst[21 * lsd], &skb = lst[22 * lsd], &svcv = lst[23 * lsd];
         if constexpr (SLK) {
             const WaveSlack& sk = *skp;
             skc = smu - sds * sdz;
