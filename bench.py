@@ -324,8 +324,8 @@ def pmc_traffic(kname: str):
 
 def cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h=None):
     """The oracle (CPU restatement of the reference assembly + dense QP solve, standing in for
-    CPLEX which cannot run here) on a bounded sample of the same workload, 1 thread (CPLEX
-    Threads=1, CPLEX.cpp:158)."""
+    CPLEX which cannot run here) on a bounded sample of the same workload: on the host cores
+    (thread pool, `cores`) and on 1 thread (CPLEX Threads=1, CPLEX.cpp:158)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
     from mpccbf import swarm
@@ -346,9 +346,24 @@ def cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h=None):
     t = time.perf_counter()
     r = O.impc_batch(p, states_h, refs, rp, col, 0, count, 1, covs=cov_h)
     dt = time.perf_counter() - t
-    return {"value": r["solved"] / dt, "unit": "QP/s", "cores": 1, "kind": "port",
-            "sample": f"first {count} agents of the same swarm/step, {r['solved']} QPs, "
-                      f"{dt:.1f} s single-threaded (oracle/ CPU restatement; CPLEX unavailable)"}
+    # the same sample on a thread pool, one agent per task (CPLEX Threads=1 per solve), over the
+    # host cores this job may use (16 on the GPU box: OMP_NUM_THREADS; os.cpu_count() shows the
+    # whole machine there)
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16, os.cpu_count() or 1))
+    t = time.perf_counter()
+    rm = O.impc_batch(p, states_h, refs, rp, col, 0, count, threads, covs=cov_h)
+    dtm = time.perf_counter() - t
+    model = ""
+    try:
+        model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
+    return {"value": rm["solved"] / dtm, "unit": "QP/s", "cores": threads, "kind": "port",
+            "single_core_value": r["solved"] / dt,
+            "cpu": model,
+            "sample": f"first {count} agents of the same swarm/step, {r['solved']} QPs: {dtm:.2f} s on "
+                      f"{threads} threads (one agent per task), {dt:.1f} s on 1 thread "
+                      f"(oracle/ CPU restatement; CPLEX unavailable)"}
 
 
 if __name__ == "__main__":
