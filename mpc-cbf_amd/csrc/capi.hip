@@ -29,7 +29,7 @@ int launch_neighbors(const double* states, int num_states, int first, int num_ag
 size_t neighbors_scratch_bytes(int num_states, int num_agents, int k);
 size_t grid_scratch_bytes(int num_states);
 uint32_t launch_grid_build(const double* states, int n, double radius, void* scratch,
-                           uint32_t** start, uint32_t** sorted, hipStream_t s);
+                           uint32_t** start, uint32_t** sorted, hipStream_t s, bool clear_counts);
 
 static thread_local std::string g_err;
 
@@ -61,6 +61,7 @@ struct mpccbf_ctx {
     size_t scratch_bytes = 0;
     void* grid_scratch = nullptr;
     size_t grid_bytes = 0;
+    int grid_n = -1;  // state count of the last grid build with grid_scratch (-1: none)
     int variant = 0;
 };
 
@@ -107,10 +108,12 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
             c->grid_bytes = 0;
             HIP_TRY(hipMalloc(&c->grid_scratch, need));
             c->grid_bytes = need;
+            c->grid_n = -1;
         }
         uint32_t *start = nullptr, *sorted = nullptr;
         const uint32_t T = launch_grid_build(b->states, b->num_states, b->knn_radius, c->grid_scratch,
-                                             &start, &sorted, stream);
+                                             &start, &sorted, stream, c->grid_n != b->num_states);
+        c->grid_n = b->num_states;
         if (T == 0) return fail(MPCCBF_ERR_CAPACITY, "grid neighbours: num_states > 32768 or launch failure");
         a.grid.start = start;
         a.grid.sorted = sorted;

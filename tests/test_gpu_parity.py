@@ -447,3 +447,40 @@ def test_fov_slack_grid_neighbours_match_csr(mpclib):
     np.testing.assert_array_equal(out["status"].cpu().numpy(), g_csr["status"])
     ok = g_csr["status"] == 0
     np.testing.assert_allclose(out["obj"].cpu().numpy()[ok], g_csr["obj"][ok], rtol=1e-10, atol=1e-9)
+
+
+def test_grid_neighbours_large_table(mpclib):
+    """State tables above 8192 agents (the multi-GPU bench gathers 8 x 4096) use the three-kernel
+    spatial-hash build (count / scan / scatter); a window of agents solved against the whole table
+    matches the CSR path with the CPU k-nearest lists."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    n, first, count = 12000, 5000, 512
+    states, targets = swarm.lattice_swarm(n, seed=17)
+    states[:, :2] *= 0.6
+    p = states[:, :2]
+    rows = []
+    for i in range(first, first + count):
+        d2 = np.sum((p - p[i]) ** 2, axis=1)
+        d2[i] = np.inf
+        cand = np.nonzero(d2 <= 36.0)[0]
+        rows.append(np.sort(cand[np.lexsort((cand, d2[cand]))[:8]]))
+    rp = np.zeros(count + 1, dtype=np.int32)
+    rp[1:] = np.cumsum([len(r) for r in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    st = torch.tensor(states, device=dev)
+    tg = torch.tensor(targets[first:first + count], device=dev)
+    ctx = mpclib.Context(cfg)
+    o_csr = ctx.alloc_outputs(count)
+    ctx.impc_solve(st, torch.tensor(rp, device=dev), torch.tensor(col, device=dev), targets=tg,
+                   agent_first=first, num_agents=count, **o_csr)
+    o_grid = ctx.alloc_outputs(count)
+    ctx.impc_solve(st, targets=tg, agent_first=first, num_agents=count, knn_k=8, knn_radius=6.0, **o_grid)
+    torch.cuda.synchronize()
+    s_csr, s_grid = o_csr["status"].cpu().numpy(), o_grid["status"].cpu().numpy()
+    np.testing.assert_array_equal(s_grid, s_csr)
+    ok = s_csr == 0
+    assert ok.sum() > count // 2
+    np.testing.assert_allclose(o_grid["obj"].cpu().numpy()[ok], o_csr["obj"].cpu().numpy()[ok],
+                               rtol=1e-10, atol=1e-9)
