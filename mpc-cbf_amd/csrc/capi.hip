@@ -27,9 +27,10 @@ int launch_neighbors(const double* states, int num_states, int first, int num_ag
                      double radius, int32_t* row_ptr, int32_t* col, void* scratch,
                      size_t scratch_bytes, hipStream_t s);
 size_t neighbors_scratch_bytes(int num_states, int num_agents, int k);
-size_t grid_scratch_bytes(int num_states);
-uint32_t launch_grid_build(const double* states, int n, double radius, void* scratch,
-                           uint32_t** start, uint32_t** sorted, hipStream_t s, bool clear_counts);
+size_t grid_table_bytes(int num_states);
+void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots);
+hipError_t launch_grid_insert(const double* states, int n, int skip0, int skip1, double radius,
+                              uint32_t* cnt, uint32_t* slots, hipStream_t s);
 
 static thread_local std::string g_err;
 
@@ -59,9 +60,8 @@ struct mpccbf_ctx {
     size_t dbuf_elems = 0;
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
-    void* grid_scratch = nullptr;
+    void* grid_scratch = nullptr;  // three neighbour tables (see GridArgs)
     size_t grid_bytes = 0;
-    int grid_n = -1;  // state count of the last grid build with grid_scratch (-1: none)
     int variant = 0;
 };
 
@@ -80,9 +80,26 @@ static void pack(std::vector<double>& v, int32_t& off, const std::vector<Mat>& m
     for (const Mat& m : ms) v.insert(v.end(), m.a.begin(), m.a.end());
 }
 
-// One IMPC step for a batch: grid build (grid mode) + the fused kernel, enqueued on `stream`;
-// ev0 / ev1 (optional) are recorded around the IMPC kernel alone.
-int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1) {
+// The three neighbour tables of grid mode in ctx scratch (grown on demand).
+static int grid_tables(mpccbf_ctx* c, int num_states, uint32_t* (&cnt)[3], uint32_t* (&slots)[3]) {
+    const size_t tb = grid_table_bytes(num_states);
+    if (3 * tb > c->grid_bytes) {
+        if (c->grid_scratch) (void)hipFree(c->grid_scratch);
+        c->grid_scratch = nullptr;
+        c->grid_bytes = 0;
+        HIP_TRY(hipMalloc(&c->grid_scratch, 3 * tb));
+        c->grid_bytes = 3 * tb;
+    }
+    for (int t = 0; t < 3; t++) grid_table_carve((char*)c->grid_scratch + t * tb, num_states, &cnt[t], &slots[t]);
+    return MPCCBF_OK;
+}
+
+// One IMPC step for a batch, enqueued on `stream`; ev0 / ev1 (optional) are recorded around the
+// IMPC kernel alone. Grid mode: gstep < 0 builds table 0 from b->states first (memset + insert
+// kernel); gstep >= 0 (mpccbf_run_steps) reads table gstep % 3, which the previous step filled,
+// has the kernel insert its next states into table (gstep + 1) % 3 and zero table (gstep + 2) % 3.
+int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1,
+                 int gstep = -1) {
     if (!c || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
     if (b->num_agents < 0 || b->agent_first < 0 || b->agent_first + b->num_agents > b->num_states)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
@@ -101,22 +118,22 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     std::memset(&a, 0, sizeof(a));
     HIP_TRY(hipSetDevice(c->device));
     if (grid) {
-        const size_t need = grid_scratch_bytes(b->num_states);
-        if (need > c->grid_bytes) {
-            if (c->grid_scratch) (void)hipFree(c->grid_scratch);
-            c->grid_scratch = nullptr;
-            c->grid_bytes = 0;
-            HIP_TRY(hipMalloc(&c->grid_scratch, need));
-            c->grid_bytes = need;
-            c->grid_n = -1;
+        uint32_t *cnt[3], *slots[3];
+        const int rc = grid_tables(c, b->num_states, cnt, slots);
+        if (rc != MPCCBF_OK) return rc;
+        const uint32_t T = grid_table_size(b->num_states);
+        int rd = 0;
+        if (gstep < 0) {
+            HIP_TRY(hipMemsetAsync(cnt[0], 0, (size_t)T * 4, stream));
+            HIP_TRY(launch_grid_insert(b->states, b->num_states, 0, 0, b->knn_radius, cnt[0], slots[0], stream));
+        } else {
+            rd = gstep % 3;
+            a.grid.ins_cnt = cnt[(gstep + 1) % 3];
+            a.grid.ins_slots = slots[(gstep + 1) % 3];
+            a.grid.clr_cnt = cnt[(gstep + 2) % 3];
         }
-        uint32_t *start = nullptr, *sorted = nullptr;
-        const uint32_t T = launch_grid_build(b->states, b->num_states, b->knn_radius, c->grid_scratch,
-                                             &start, &sorted, stream, c->grid_n != b->num_states);
-        c->grid_n = b->num_states;
-        if (T == 0) return fail(MPCCBF_ERR_CAPACITY, "grid neighbours: num_states > 32768 or launch failure");
-        a.grid.start = start;
-        a.grid.sorted = sorted;
+        a.grid.cnt = cnt[rd];
+        a.grid.slots = slots[rd];
         a.grid.mask = T - 1;
         a.grid.inv_cell = 1.0 / b->knn_radius;
         a.grid.radius = b->knn_radius;
@@ -449,6 +466,20 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
     mpccbf_batch sb = *b;
     hipEvent_t* ev = c->events.data();
     if (timing) HIP_TRY(hipEventRecord(ev[0], stream));
+    // grid mode: neighbour table 0 from the initial states, table 1 zeroed for step 0's inserts
+    // (each IMPC launch zeroes the table two steps ahead, see impc_enqueue)
+    const bool gtab = b->nb_row_ptr == nullptr && count > 0 && r->num_steps > 0;
+    uint32_t *gcnt[3] = {}, *gslots[3] = {};
+    if (gtab) {
+        if (b->knn_k < 1 || !(b->knn_radius > 0))
+            return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
+        const int rc = grid_tables(c, ns, gcnt, gslots);
+        if (rc != MPCCBF_OK) return rc;
+        const size_t cb = (size_t)grid_table_size(ns) * 4;
+        HIP_TRY(hipMemsetAsync(gcnt[0], 0, cb, stream));
+        HIP_TRY(hipMemsetAsync(gcnt[1], 0, cb, stream));
+        HIP_TRY(launch_grid_insert(b->states, ns, 0, 0, b->knn_radius, gcnt[0], gslots[0], stream));
+    }
     for (int s = 0; s < r->num_steps; s++) {
         double* cur = tables[s & 1];
         double* nxt = tables[(s & 1) ^ 1];
@@ -466,13 +497,19 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
                                        (size_t)tail * 6 * sizeof(double), hipMemcpyDeviceToDevice, stream));
         }
         const bool tk = r->solve_ms && (r->solve_stride <= 1 || s % r->solve_stride == 0);
-        const int rc = impc_enqueue(c, &sb, stream, tk ? ev[3 * s + 1] : nullptr, tk ? ev[3 * s + 2] : nullptr);
+        const int rc = impc_enqueue(c, &sb, stream, tk ? ev[3 * s + 1] : nullptr, tk ? ev[3 * s + 2] : nullptr,
+                                    gtab ? s : -1);
         if (rc != MPCCBF_OK) return rc;
         if (r->comm && r->comm->nranks > 1) {
             const ncclResult_t nr = ncclAllGather(nxt + (size_t)first * 6, nxt, (size_t)count * 6, ncclDouble,
                                                   r->comm->nccl, stream);
             if (nr != ncclSuccess) return fail(MPCCBF_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(nr));
         }
+        // the rows the kernel did not insert (static rows / the other ranks' rows) join the table
+        // of the next step
+        if (gtab && count < ns)
+            HIP_TRY(launch_grid_insert(nxt, ns, first, first + count, b->knn_radius, gcnt[(s + 1) % 3],
+                                       gslots[(s + 1) % 3], stream));
         if (r->step_ms || (timing && s == r->num_steps - 1)) HIP_TRY(hipEventRecord(ev[3 * s + 3], stream));
     }
     r->final_table = r->num_steps & 1;

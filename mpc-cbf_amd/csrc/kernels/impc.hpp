@@ -45,11 +45,20 @@ constexpr int WBOX_ROW = 16 + 6 + 2;
 constexpr int SEP_ROW = 10;
 constexpr int SEP_NZD_HOST = 2;  // reduced variables per channel the separable kernel handles
 
-// Spatial hash of agent positions (uniform cells of edge `radius`), built by grid_build_kernel:
-// bucket h holds sorted[start[h] .. start[h+1]).
+// Spatial hash of agent positions (uniform cells of edge `radius`) with fixed-capacity buckets:
+// bucket h holds the state rows slots[h*GRID_CAP .. h*GRID_CAP + cnt[h]) in insertion order
+// (cnt[h] > GRID_CAP: overflow, an agent reading that bucket scans the whole state table
+// instead, so the neighbour sets never depend on the capacity). Filled by atomics, so no
+// scan: mpccbf_run_steps rotates three tables (read this step | filled with this step's next
+// states by the IMPC kernel itself | zeroed by the IMPC kernel for the step after next).
+constexpr int GRID_CAP = 64;
+
 struct GridArgs {
-    const uint32_t* start;
-    const uint32_t* sorted;
+    const uint32_t* cnt;   // T bucket counts of the table read this step
+    const uint32_t* slots; // T x GRID_CAP state rows
+    uint32_t* ins_cnt;     // table of the next step (NULL: none): next_states rows are inserted
+    uint32_t* ins_slots;
+    uint32_t* clr_cnt;     // bucket counts zeroed by this launch (NULL: none)
     uint32_t mask;
     double inv_cell;
     double radius;
@@ -63,6 +72,13 @@ constexpr int NB_CAP = 64;  // grid-mode candidate capacity per agent (LDS)
 __host__ __device__ inline uint32_t cell_hash(long long cx, long long cy, uint32_t mask) {
     const uint64_t h = (uint64_t)(cx * 73856093LL) ^ (uint64_t)(cy * 19349663LL);
     return (uint32_t)(h ^ (h >> 29)) & mask;
+}
+
+// insert state row `row` at planar position (x, y) into the table (ins_cnt, ins_slots)
+__device__ inline void grid_insert(const GridArgs& g, double x, double y, uint32_t row) {
+    const uint32_t h = cell_hash((long long)floor(x * g.inv_cell), (long long)floor(y * g.inv_cell), g.mask);
+    const uint32_t j = atomicAdd(&g.ins_cnt[h], 1u);
+    if (j < (uint32_t)GRID_CAP) g.ins_slots[(size_t)h * GRID_CAP + j] = row;
 }
 
 // hash table size for n agents: power of two >= n (>= 1024)

@@ -58,13 +58,15 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
     // the 9 cells' buckets (a bucket reached from two cells is scanned once), concatenated: lane
     // gl takes candidates gl, gl + G, ... of the whole list, so the dependent loads (bucket entry,
     // then the agent's position) of all cells are in flight together
-    uint32_t hs[9], b0[9], nc[9];
+    uint32_t hs[9], nc[9];
+    bool full = false;
 #pragma unroll
     for (int c = 0; c < 9; c++) {
         hs[c] = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
-        b0[c] = gr.start[hs[c]];
-        nc[c] = gr.start[hs[c] + 1] - b0[c];
+        nc[c] = gr.cnt[hs[c]];
+        full = full || nc[c] > (uint32_t)GRID_CAP;
     }
+    // a bucket that overflowed its slots: scan the whole state table instead (same result)
     uint32_t off[9], total = 0;
 #pragma unroll
     for (int c = 0; c < 9; c++) {
@@ -75,6 +77,7 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         off[c] = total;
         total += nc[c];
     }
+    if (full) total = (uint32_t)args.num_states;
     int cnt = 0;
     for (uint32_t t0 = 0; t0 < total; t0 += G) {
         const uint32_t t = t0 + gl;
@@ -82,11 +85,15 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         int j = -1;
         double d2 = 0.0;
         if (t < total) {
-            uint32_t e = 0;
+            if (full) {
+                j = (int)t;
+            } else {
+                uint32_t e = 0;
 #pragma unroll
-            for (int c = 0; c < 9; c++)  // last cell whose range starts at or before t
-                if (off[c] <= t && t - off[c] < nc[c]) e = b0[c] + (t - off[c]);
-            j = (int)gr.sorted[e];
+                for (int c = 0; c < 9; c++)  // the cell whose range holds t
+                    if (off[c] <= t && t - off[c] < nc[c]) e = hs[c] * (uint32_t)GRID_CAP + (t - off[c]);
+                j = (int)gr.slots[e];
+            }
             const double ex = args.states[(size_t)j * 6] - px;
             const double ey = args.states[(size_t)j * 6 + 1] - py;
             d2 = ex * ex + ey * ey;
@@ -431,6 +438,20 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
     const double sd = gl < 3 ? args.pos_std : args.vel_std;
     if (sd > 0.0) v = fma(sd, normal_sample(args.noise_seed, args.step_index, args.agent_first + ai, gl), v);
     if (args.next_states) args.next_states[(size_t)ai * 6 + gl] = v;
+    if (args.grid.ins_cnt) {  // the next step's neighbour table gets this row (lane 0: x, lane 1: y)
+        const int base = (int)(threadIdx.x & 63u) & ~(G - 1);
+        const double y = __shfl(v, base + 1, 64);
+        if (gl == 0) grid_insert(args.grid, v, y, (uint32_t)(args.agent_first + ai));
+    }
+}
+
+// the bucket counts of the table two steps ahead are zeroed by the launch's threads (called by
+// every thread before any early exit)
+__device__ __forceinline__ void grid_clear(const ImpcArgs& args) {
+    if (!args.grid.clr_cnt) return;
+    const uint32_t T = args.grid.mask + 1u;
+    const uint32_t nthr = gridDim.x * blockDim.x;
+    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < T; e += nthr) args.grid.clr_cnt[e] = 0u;
 }
 
 // diagnostics: wall-clock stamp (s_memrealtime, 100 MHz, chip-wide) of phase `k` of agent ai

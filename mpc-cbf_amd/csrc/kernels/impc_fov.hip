@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     constexpr int NZ = 15;
     const int lane = threadIdx.x;
     const int ai = blockIdx.x;
+    grid_clear(args);
     if (ai >= args.num_agents) return;
     stamp(args, ai, lane, 0);
     const double* zero_row = nullptr;

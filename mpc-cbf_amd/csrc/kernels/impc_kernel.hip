@@ -41,6 +41,7 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
     const int gl = threadIdx.x & (G - 1);
     const int gib = threadIdx.x / G;
     const int ai = blockIdx.x * GPB + gib;  // agent index within the batch
+    grid_clear(args);
     if (ai >= args.num_agents) return;      // whole group leaves together
     stamp(args, ai, gl, 0);
 
@@ -247,6 +248,7 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
     const int gl = threadIdx.x & (G - 1);
     const int gib = threadIdx.x / G;
     const int ai = blockIdx.x * GPB + gib;
+    grid_clear(args);
     if (ai >= args.num_agents) return;
     stamp(args, ai, gl, 0);
 

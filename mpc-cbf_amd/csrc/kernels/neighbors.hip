@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 
 #include "impc.hpp"
 
@@ -243,194 +244,48 @@ int launch_neighbors(const double* states, int num_states, int first, int num_ag
 namespace mpccbf {
 namespace dev {
 
-// Spatial hash of all agents in ONE workgroup (n <= 32768): LDS histogram -> block scan ->
-// scatter. One launch instead of count/scan/scatter; bucket order inside a cell follows LDS
-// atomic order (the consumer orders neighbours by index, so results do not depend on it).
-// Each thread keeps the bucket and in-bucket offset of its (up to GB_PER) agents in registers
-// between the passes; the bucket scan is a per-thread serial sum, a wave-level DPP/shuffle scan
-// and one scan of the 16 wave totals (3 barriers instead of a 1024-wide Hillis-Steele).
-constexpr int GB_THREADS = 1024;
-constexpr int GB_PER = 32;  // agents per thread: n <= 32768
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u = __shfl_up(v, o, 64);
-        if (lane >= o) v += u;
-    }
-    return v;
-}
-
-__global__ void __launch_bounds__(GB_THREADS) grid_build_kernel(const double* __restrict__ st, int n,
-                                                                double inv, uint32_t T, uint32_t* start,
-                                                                uint32_t* sorted) {
-    extern __shared__ uint32_t cnt[];  // T buckets
-    __shared__ uint32_t wsum[GB_THREADS / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (uint32_t i = tid; i < T; i += GB_THREADS) cnt[i] = 0u;
-    __syncthreads();
-    uint32_t h[GB_PER], off[GB_PER];
-#pragma unroll
-    for (int k = 0; k < GB_PER; k++) {
-        const int i = tid + k * GB_THREADS;
-        if (i < n) {
-            const long long cx = (long long)floor(st[(size_t)i * 6] * inv);
-            const long long cy = (long long)floor(st[(size_t)i * 6 + 1] * inv);
-            h[k] = cell_hash(cx, cy, T - 1);
-            off[k] = atomicAdd(&cnt[h[k]], 1u);
-        }
-    }
-    __syncthreads();
-    // exclusive scan of cnt: thread t owns buckets [t*per, (t+1)*per)
-    const uint32_t per = T / GB_THREADS, b = tid * per;
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < per; i++) s += cnt[b + i];
-    const uint32_t incl = wave_incl_scan(s, lane);
-    if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
-    if (wid == 0) {
-        const uint32_t w = lane < GB_THREADS / 64 ? wsum[lane] : 0u;
-        const uint32_t wi = wave_incl_scan(w, lane);
-        if (lane < GB_THREADS / 64) wsum[lane] = wi - w;  // exclusive wave offsets
-        if (lane == GB_THREADS / 64 - 1) start[T] = wi;
-    }
-    __syncthreads();
-    uint32_t run = wsum[wid] + incl - s;
-    for (uint32_t i = 0; i < per; i++) {
-        const uint32_t c = cnt[b + i];
-        cnt[b + i] = run;
-        start[b + i] = run;
-        run += c;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < GB_PER; k++) {
-        const int i = tid + k * GB_THREADS;
-        if (i < n) sorted[cnt[h[k]] + off[k]] = (uint32_t)i;
-    }
-}
-
-// Large tables (the multi-GPU bench gathers 8 x 4096 = 32768 states per rank: the single
-// workgroup above needs ~68 us there): count (global atomics, one thread per agent, the bucket
-// and in-bucket offset kept in scratch) -> one-workgroup scan of the T bucket counts -> scatter.
-constexpr int GB_MULTI_MIN = 8192;  // n above which the three-kernel build is used
-
-__global__ void __launch_bounds__(256) grid_count_kernel(const double* __restrict__ st, int n, double inv,
-                                                         uint32_t T, uint32_t* __restrict__ gcnt,
-                                                         uint32_t* __restrict__ hb, uint32_t* __restrict__ ob) {
+// Insert state rows [0, n) except [skip0, skip1) into a zeroed fixed-capacity bucket table, one
+// thread per row (global atomics on the bucket counts; slot order inside a bucket follows atomic
+// order, and the consumer orders neighbours by (distance, index), so results do not depend on it).
+// Used for a whole table (standalone solve) and, in mpccbf_run_steps, for the rows the IMPC
+// kernel did not write itself (static rows, or the other ranks' rows after the all-gather).
+__global__ void __launch_bounds__(256) grid_insert_kernel(const double* __restrict__ st, int n, int skip0,
+                                                          int skip1, GridArgs g) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const long long cx = (long long)floor(st[(size_t)i * 6] * inv);
-    const long long cy = (long long)floor(st[(size_t)i * 6 + 1] * inv);
-    const uint32_t h = cell_hash(cx, cy, T - 1);
-    hb[i] = h;
-    ob[i] = atomicAdd(&gcnt[h], 1u);
-}
-
-// Exclusive scan of the T bucket counts in one workgroup: a coalesced copy into LDS (padded by
-// one word per 32 so that thread t's contiguous run of T/1024 buckets is bank-conflict free), a
-// per-thread serial sum, wave / block scans of the 1024 partial sums, a per-thread serial
-// rewrite in LDS and a coalesced copy out.
-__device__ __forceinline__ uint32_t pad32(uint32_t j) { return j + (j >> 5); }
-
-__global__ void __launch_bounds__(GB_THREADS) grid_scan_kernel(uint32_t* __restrict__ gcnt, uint32_t T,
-                                                                uint32_t* __restrict__ start) {
-    extern __shared__ uint32_t lc[];  // pad32(T) words
-    __shared__ uint32_t wsum[GB_THREADS / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    for (uint32_t j = tid; j < T; j += GB_THREADS) {
-        lc[pad32(j)] = gcnt[j];
-        gcnt[j] = 0u;  // ready for the next build with the same layout (no memset then)
-    }
-    __syncthreads();
-    const uint32_t per = T / GB_THREADS, b = tid * per;  // T: power of two >= 1024
-    uint32_t s = 0;
-    for (uint32_t i = 0; i < per; i++) s += lc[pad32(b + i)];
-    const uint32_t incl = wave_incl_scan(s, lane);
-    if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
-    if (wid == 0) {
-        const uint32_t w = lane < GB_THREADS / 64 ? wsum[lane] : 0u;
-        const uint32_t wi = wave_incl_scan(w, lane);
-        if (lane < GB_THREADS / 64) wsum[lane] = wi - w;
-        if (lane == GB_THREADS / 64 - 1) start[T] = wi;
-    }
-    __syncthreads();
-    uint32_t run = wsum[wid] + incl - s;
-    for (uint32_t i = 0; i < per; i++) {
-        const uint32_t c = lc[pad32(b + i)];
-        lc[pad32(b + i)] = run;
-        run += c;
-    }
-    __syncthreads();
-    for (uint32_t j = tid; j < T; j += GB_THREADS) start[j] = lc[pad32(j)];
-}
-
-__global__ void __launch_bounds__(256) grid_scatter_kernel(int n, const uint32_t* __restrict__ start,
-                                                           const uint32_t* __restrict__ hb,
-                                                           const uint32_t* __restrict__ ob,
-                                                           uint32_t* __restrict__ sorted) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    sorted[start[hb[i]] + ob[i]] = (uint32_t)i;
+    const int gap = skip1 - skip0;
+    if (i >= n - gap) return;
+    const int r = i < skip0 ? i : i + gap;
+    grid_insert(g, st[(size_t)r * 6], st[(size_t)r * 6 + 1], (uint32_t)r);
 }
 
 }  // namespace dev
 
 static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
-size_t grid_scratch_bytes(int num_states) {
+// one table: bucket counts (T) | slots (T x GRID_CAP)
+size_t grid_table_bytes(int num_states) {
     const uint32_t T = grid_table_size(num_states);
-    // start (T+1) | sorted (n) [| counts (T) | bucket (n) | offset (n) for the multi-kernel build]
-    size_t b = al256((size_t)(T + 1) * 4) + al256((size_t)num_states * 4);
-    if (num_states > dev::GB_MULTI_MIN) b += al256((size_t)T * 4) + 2 * al256((size_t)num_states * 4);
-    return b;
+    return al256((size_t)T * 4) + (size_t)T * GRID_CAP * 4;
 }
 
-// start (T+1) | sorted (n) | slot_off (n) carved from scratch; returns T or 0 on error
-uint32_t launch_grid_build(const double* states, int n, double radius, void* scratch,
-                           uint32_t** start, uint32_t** sorted, hipStream_t s, bool clear_counts) {
-    const uint32_t T = grid_table_size(n);
-    if (T > 32768 || n > dev::GB_THREADS * dev::GB_PER) return 0;  // single-workgroup limits
-    char* p = (char*)scratch;
-    *start = (uint32_t*)p;
-    p += al256((size_t)(T + 1) * 4);
-    *sorted = (uint32_t*)p;
-    p += al256((size_t)n * 4);
-    if (n > dev::GB_MULTI_MIN) {
-        uint32_t* gcnt = (uint32_t*)p;
-        p += al256((size_t)T * 4);
-        uint32_t* hb = (uint32_t*)p;
-        p += al256((size_t)n * 4);
-        uint32_t* ob = (uint32_t*)p;
-        // the scan kernel leaves the counts zeroed: the caller asks for a clear only when this
-        // scratch was not used with the same n by the previous build
-        if (clear_counts && hipMemsetAsync(gcnt, 0, (size_t)T * 4, s) != hipSuccess) return 0;
-        const int blocks = (n + 255) / 256;
-        hipLaunchKernelGGL(dev::grid_count_kernel, dim3(blocks), dim3(256), 0, s, states, n, 1.0 / radius, T,
-                           gcnt, hb, ob);
-        static bool scan_attr = false;  // > 64 KiB of dynamic LDS needs an opt-in
-        if (!scan_attr) {
-            if (hipFuncSetAttribute((const void*)dev::grid_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (32768 + 1024) * 4) != hipSuccess)
-                return 0;
-            scan_attr = true;
-        }
-        hipLaunchKernelGGL(dev::grid_scan_kernel, dim3(1), dim3(dev::GB_THREADS), (size_t)(T + T / 32) * 4, s,
-                           gcnt, T, *start);
-        hipLaunchKernelGGL(dev::grid_scatter_kernel, dim3(blocks), dim3(256), 0, s, n, *start, hb, ob, *sorted);
-        return hipGetLastError() == hipSuccess ? T : 0;
-    }
-    static bool attr_set = false;  // > 64 KiB of dynamic LDS needs an opt-in (gfx950: 160 KiB/CU)
-    if (!attr_set) {
-        if (hipFuncSetAttribute((const void*)dev::grid_build_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4) != hipSuccess)
-            return 0;
-        attr_set = true;
-    }
-    hipLaunchKernelGGL(dev::grid_build_kernel, dim3(1), dim3(dev::GB_THREADS), (size_t)T * 4, s, states,
-                       n, 1.0 / radius, T, *start, *sorted);
-    return hipGetLastError() == hipSuccess ? T : 0;
+void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots) {
+    const uint32_t T = grid_table_size(num_states);
+    *cnt = (uint32_t*)base;
+    *slots = (uint32_t*)((char*)base + al256((size_t)T * 4));
+}
+
+hipError_t launch_grid_insert(const double* states, int n, int skip0, int skip1, double radius,
+                              uint32_t* cnt, uint32_t* slots, hipStream_t s) {
+    const int m = n - (skip1 - skip0);
+    if (m <= 0) return hipSuccess;
+    GridArgs g;
+    memset(&g, 0, sizeof(g));
+    g.ins_cnt = cnt;
+    g.ins_slots = slots;
+    g.mask = grid_table_size(n) - 1u;
+    g.inv_cell = 1.0 / radius;
+    hipLaunchKernelGGL(dev::grid_insert_kernel, dim3((m + 255) / 256), dim3(256), 0, s, states, n, skip0, skip1, g);
+    return hipGetLastError();
 }
 
 }  // namespace mpccbf

@@ -450,9 +450,9 @@ def test_fov_slack_grid_neighbours_match_csr(mpclib):
 
 
 def test_grid_neighbours_large_table(mpclib):
-    """State tables above 8192 agents (the multi-GPU bench gathers 8 x 4096) use the three-kernel
-    spatial-hash build (count / scan / scatter); a window of agents solved against the whole table
-    matches the CSR path with the CPU k-nearest lists."""
+    """A state table of 12000 agents (the multi-GPU bench gathers 8 x 4096) in the fixed-capacity
+    bucket table: a window of agents solved against the whole table matches the CSR path with the
+    CPU k-nearest lists."""
     torch = _torch()
     cfg = swarm.config(15)
     n, first, count = 12000, 5000, 512
@@ -484,3 +484,44 @@ def test_grid_neighbours_large_table(mpclib):
     assert ok.sum() > count // 2
     np.testing.assert_allclose(o_grid["obj"].cpu().numpy()[ok], o_csr["obj"].cpu().numpy()[ok],
                                rtol=1e-10, atol=1e-9)
+
+
+def test_grid_bucket_overflow_falls_back_to_full_scan(mpclib):
+    """70 agents in one hash cell (two tight clusters at opposite corners, each agent with 34
+    others in range) overflow the 64-slot bucket: the agents that read it scan the whole table,
+    so the grid path still equals the CSR path with the CPU k-nearest lists, in the standalone
+    solve and after native closed-loop steps."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    n = 300
+    states = np.zeros((n, 6))
+    g = np.arange(35)
+    states[:35, 0], states[:35, 1] = 0.05 + 0.1 * (g % 6), 0.05 + 0.1 * (g // 6)  # cell (0, 0)
+    states[35:70, 0], states[35:70, 1] = 5.95 - 0.1 * (g % 6), 5.95 - 0.1 * (g // 6)  # > 6 apart
+    m = np.arange(n - 70)
+    states[70:, 0], states[70:, 1] = 40.0 + 7.0 * (m % 20), 40.0 + 7.0 * (m // 20)
+    targets = states[:, :3].copy()
+    targets[:, 0] += 1.0
+    dev = torch.device("cuda", 0)
+    tg = torch.tensor(targets, device=dev)
+    ctx = mpclib.Context(cfg)
+    for it in range(2):
+        rp, col = swarm.knn_csr(states, 8, 6.0)
+        st = torch.tensor(states, device=dev)
+        o_csr, o_grid = ctx.alloc_outputs(n), ctx.alloc_outputs(n)
+        ctx.impc_solve(st, torch.tensor(rp, device=dev), torch.tensor(col, device=dev), targets=tg, **o_csr)
+        ctx.impc_solve(st, targets=tg, knn_k=8, knn_radius=6.0, **o_grid)
+        torch.cuda.synchronize()
+        s_csr, s_grid = o_csr["status"].cpu().numpy(), o_grid["status"].cpu().numpy()
+        np.testing.assert_array_equal(s_grid, s_csr)
+        assert np.all(s_csr[70:, 0] == O.OPTIMAL)
+        ok = s_csr == 0
+        np.testing.assert_allclose(o_grid["obj"].cpu().numpy()[ok], o_csr["obj"].cpu().numpy()[ok],
+                                   rtol=1e-10, atol=1e-9)
+        if it == 0:  # evolve with the native loop (grid tables rotated by the kernel), then recheck
+            a, b = st.clone(), torch.empty_like(st)
+            r = ctx.run_steps(a, b, 4, targets=tg, knn_k=8, knn_radius=6.0)
+            torch.cuda.synchronize()
+            states = r["final"].cpu().numpy()
+            ref, _ = _manual_loop(ctx, st, tg, 4, 0, n, torch)
+            np.testing.assert_array_equal(states, ref)
