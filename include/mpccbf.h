@@ -121,8 +121,9 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *   nb_col      neighbour indices into `states` (the reference uses all N-1 others, :59-67)
  *   knn_k, knn_radius   used when nb_row_ptr is NULL: the neighbours of each agent are its
  *               knn_k nearest others (planar) within knn_radius, found on the device in the same
- *               launch sequence (spatial hash of `states` + in-kernel 3x3-cell query);
- *               requires num_states <= 32768 and at most 64 agents within the radius
+ *               launch sequence (spatial hash of `states` + in-kernel 3x3-cell query; in
+ *               mpccbf_run_steps the IMPC kernel itself fills the next step's hash table);
+ *               at most 64 agents within the radius (more: that agent's QP reports ERROR)
  * Outputs (device, any may be NULL):
  *   x           num_agents x n: control points of the last OPTIMAL iteration (the curve the
  *               driver keeps, example :160-164); NaN if no iteration was OPTIMAL
