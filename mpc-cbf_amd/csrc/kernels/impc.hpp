@@ -46,7 +46,8 @@ constexpr int SEP_ROW = 10;
 constexpr int SEP_NZD_HOST = 2;  // reduced variables per channel the separable kernel handles
 
 // Spatial hash of agent positions (uniform cells of edge `radius`) with fixed-capacity buckets:
-// bucket h holds the state rows slots[h*GRID_CAP .. h*GRID_CAP + cnt[h]) in insertion order
+// bucket h holds the state rows slots[j*T + h], j < cnt[h], in insertion order (slot-major: the
+// first slots of all buckets are one dense T-word plane, so the table's touched lines stay few)
 // (cnt[h] > GRID_CAP: overflow, an agent reading that bucket scans the whole state table
 // instead, so the neighbour sets never depend on the capacity). Filled by atomics, so no
 // scan: mpccbf_run_steps rotates three tables (read this step | filled with this step's next
@@ -55,7 +56,7 @@ constexpr int GRID_CAP = 64;
 
 struct GridArgs {
     const uint32_t* cnt;   // T bucket counts of the table read this step
-    const uint32_t* slots; // T x GRID_CAP state rows
+    const uint32_t* slots; // GRID_CAP x T state rows (slot-major)
     uint32_t* ins_cnt;     // table of the next step (NULL: none): next_states rows are inserted
     uint32_t* ins_slots;
     uint32_t* clr_cnt;     // bucket counts zeroed by this launch (NULL: none)
@@ -78,7 +79,7 @@ __host__ __device__ inline uint32_t cell_hash(long long cx, long long cy, uint32
 __device__ inline void grid_insert(const GridArgs& g, double x, double y, uint32_t row) {
     const uint32_t h = cell_hash((long long)floor(x * g.inv_cell), (long long)floor(y * g.inv_cell), g.mask);
     const uint32_t j = atomicAdd(&g.ins_cnt[h], 1u);
-    if (j < (uint32_t)GRID_CAP) g.ins_slots[(size_t)h * GRID_CAP + j] = row;
+    if (j < (uint32_t)GRID_CAP) g.ins_slots[(size_t)j * (g.mask + 1u) + h] = row;
 }
 
 // hash table size for n agents: power of two >= n (>= 1024)

@@ -91,7 +91,7 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
                 uint32_t e = 0;
 #pragma unroll
                 for (int c = 0; c < 9; c++)  // the cell whose range holds t
-                    if (off[c] <= t && t - off[c] < nc[c]) e = hs[c] * (uint32_t)GRID_CAP + (t - off[c]);
+                    if (off[c] <= t && t - off[c] < nc[c]) e = (t - off[c]) * (gr.mask + 1u) + hs[c];
                 j = (int)gr.slots[e];
             }
             const double ex = args.states[(size_t)j * 6] - px;

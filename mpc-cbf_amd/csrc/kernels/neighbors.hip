@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(256) grid_insert_kernel(const double* __restri
 
 static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
-// one table: bucket counts (T) | slots (T x GRID_CAP)
+// one table: bucket counts (T) | slots (GRID_CAP x T, slot-major)
 size_t grid_table_bytes(int num_states) {
     const uint32_t T = grid_table_size(num_states);
     return al256((size_t)T * 4) + (size_t)T * GRID_CAP * 4;

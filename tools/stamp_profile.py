@@ -87,5 +87,10 @@ for v in VARIANTS:
     crit = int(np.argmax(end))
     print(f"   critical agent {crit}: status {status[crit]}, start {start[crit]:.1f}, "
           f"phases {np.round(np.diff(s[crit]), 2)}")
-    # how many agents end late
+    print(f"   critical agent iters {its[crit]}")
+    # how many agents end late, and the latest end per iteration-0 status
     print(f"   agents ending after 0.8*span: {(end > 0.8 * end.max()).sum()}")
+    for stv in np.unique(status[:, 0]):
+        m = status[:, 0] == stv
+        print(f"   status0 {stv}: {m.sum()} agents, wall max {np.max(end[m] - start[m]):.1f} "
+              f"p99 {np.percentile(end[m] - start[m], 99):.1f} us, solve0 iters max {its[m, 0].max()}")
