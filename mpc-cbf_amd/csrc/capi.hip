@@ -326,6 +326,10 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     d.cbf_filter = c->opt.no_cbf_filter ? 0 : 1;
     d.maxit = c->opt.max_pdip_iters > 0 ? c->opt.max_pdip_iters : 60;
     d.tol = c->opt.tolerance > 0 ? c->opt.tolerance : 1e-9;
+    {
+        const char* w = getenv("MPCCBF_WARM_DELTA");  // tuning override of the IMPC warm start
+        d.warm_delta = w ? atof(w) : 0.3;
+    }
     d.feas_tol = 1e-6;  // CPLEX default feasibility tolerance
     c->variant = 0;
     hipError_t e = hipSetDevice(c->device);

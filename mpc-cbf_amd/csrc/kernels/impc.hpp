@@ -38,6 +38,9 @@ struct DevOps {
     // distanceToEllipse with the reference's idx[i] indexing (FovBezierIMPCCBF.cpp:58-81)
     int32_t slack_mode;
     double slack_cost, slack_decay;
+    // IMPC iteration 1 warm start (impc_sep_kernel, no slack mode): the PDIP starts from
+    // iteration 0's solution with slacks and duals floored at warm_delta (0: cold start)
+    double warm_delta;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;

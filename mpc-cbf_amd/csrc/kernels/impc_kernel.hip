@@ -305,6 +305,8 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
     for (int i = 0; i < NZ; i++) y[i] = ykeep[i] = 0.0;
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
+    SepWarm<SB> warm;  // box duals of the previous OPTIMAL solve (iteration 1 warm start)
+    const double warm_delta = SLACK ? 0.0 : op.warm_delta;
 
     for (int it = 0; it < op.impc_iter; it++) {
         const size_t oi = (size_t)ai * op.impc_iter + it;
@@ -348,8 +350,18 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
 #else
             long long* dbg = nullptr;
 #endif
-            const PdipOut po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr),
-                                                                q, y, cfg, dbg, wslack, &vslack, red_all[gib]);
+            const bool warm_try = it > 0 && warm_delta > 0.0;
+            PdipOut po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr),
+                                                          q, y, cfg, dbg, wslack, &vslack, red_all[gib],
+                                                          &warm, warm_try ? warm_delta : 0.0);
+            if (warm_try && po.status != ST_OPTIMAL) {
+                // a warm start that does not converge is retried cold, so the statuses never
+                // depend on it (group-uniform)
+                const int wit = po.iters;
+                po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y,
+                                                      cfg, dbg, wslack, &vslack, red_all[gib], &warm, 0.0);
+                po.iters += wit;
+            }
             st = po.status;
             nit = po.iters;
             if (st != ST_OPTIMAL) {

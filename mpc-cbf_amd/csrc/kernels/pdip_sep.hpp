@@ -52,6 +52,13 @@ __device__ __forceinline__ void acc_blk2(double* a, double D, double g0, double 
     a[2] = fma(D * g1, g1, a[2]);
 }
 
+// Box-row duals of the last OPTIMAL solve: IMPC iteration 1 has the same box rows and cost as
+// iteration 0 and differs only in its CBF rows, so it starts from iteration 0's primal-dual point.
+template <int SB>
+struct SepWarm {
+    double zl[SEP_D][SB], zu[SEP_D][SB];
+};
+
 // Solve with the separable Newton matrix: 4x4 packed (x, y) factor + 2x2 packed yaw factor.
 __device__ __forceinline__ void sep_solve(const double (&Mxy)[10], const double (&dxy)[4],
                                           const double (&Mw)[3], const double (&dw)[2],
@@ -80,21 +87,28 @@ template <int G, int SB, int CB, bool SLACK = false>
 __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                                   const double* __restrict__ LP, const double (&q)[SEP_NZ],
                                   double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg = nullptr,
-                                  double wv_cost = 0.0, double* v_out = nullptr, double* red = nullptr) {
+                                  double wv_cost = 0.0, double* v_out = nullptr, double* red = nullptr,
+                                  SepWarm<SB>* warm = nullptr, double warm_delta = 0.0) {
     (void)dbg;
     const bool slk = SLACK && has_cbf;  // group-uniform
     // slack variable, its bound's slack and dual; the dual starts at the linear cost it carries at
     // the optimum (w = sum_rows z + z_bound with inactive rows)
     double v = 1.0, sb = 1.0, zb = SLACK ? fmax(wv_cost, 1.0) : 1.0;
+    // warm start (group-uniform): y holds the previous solution; slacks from it and the stored
+    // duals, both floored at delta (complementarity >= delta^2), CBF rows centred at delta^2
+    const bool use_warm = warm != nullptr && warm_delta > 0.0;
+    const double wd = warm_delta, wd2 = warm_delta * warm_delta;
     // ---- start: unconstrained minimiser (block-diagonal P: per-channel 2x2 solves)
+    if (!use_warm) {
 #pragma unroll
-    for (int d = 0; d < SEP_D; d++) {
-        const int o = 2 * d;
-        const double l00 = LP[o * 6 + o], l10 = LP[(o + 1) * 6 + o], l11 = LP[(o + 1) * 6 + o + 1];
-        const double w0 = -q[o] * rcp(l00);
-        const double w1 = (-q[o + 1] - l10 * w0) * rcp(l11);
-        y[o + 1] = w1 * rcp(l11);
-        y[o] = (w0 - l10 * y[o + 1]) * rcp(l00);
+        for (int d = 0; d < SEP_D; d++) {
+            const int o = 2 * d;
+            const double l00 = LP[o * 6 + o], l10 = LP[(o + 1) * 6 + o], l11 = LP[(o + 1) * 6 + o + 1];
+            const double w0 = -q[o] * rcp(l00);
+            const double w1 = (-q[o + 1] - l10 * w0) * rcp(l11);
+            y[o + 1] = w1 * rcp(l11);
+            y[o] = (w0 - l10 * y[o + 1]) * rcp(l00);
+        }
     }
     // slacks (s) and duals (z): box lower / upper sides, CBF upper side
     double sl[SEP_D][SB], su[SEP_D][SB], zl[SEP_D][SB], zu[SEP_D][SB], cs[CB], cz[CB];
@@ -104,10 +118,17 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #pragma unroll
         for (int k = 0; k < SB; k++) {
             const double t = rw.bg[d][k][0] * y[2 * d] + rw.bg[d][k][1] * y[2 * d + 1];
-            sl[d][k] = fmax(t - rw.blo[d][k], 1.0);
-            su[d][k] = fmax(rw.bhi[d][k] - t, 1.0);
-            zl[d][k] = rcp(sl[d][k]);
-            zu[d][k] = rcp(su[d][k]);
+            if (use_warm) {
+                sl[d][k] = fmax(t - rw.blo[d][k], wd);
+                su[d][k] = fmax(rw.bhi[d][k] - t, wd);
+                zl[d][k] = fmax(warm->zl[d][k], wd);
+                zu[d][k] = fmax(warm->zu[d][k], wd);
+            } else {
+                sl[d][k] = fmax(t - rw.blo[d][k], 1.0);
+                su[d][k] = fmax(rw.bhi[d][k] - t, 1.0);
+                zl[d][k] = rcp(sl[d][k]);
+                zu[d][k] = rcp(su[d][k]);
+            }
             pl[d][k] = rcp(1.0 + fabs(rw.blo[d][k]));
             pu[d][k] = rcp(1.0 + fabs(rw.bhi[d][k]));
         }
@@ -117,8 +138,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #pragma unroll
         for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
         if (slk) t -= rw.ccv[c] * v;
-        cs[c] = fmax(rw.chi[c] - t, 1.0);
-        cz[c] = rcp(cs[c]);
+        cs[c] = fmax(rw.chi[c] - t, use_warm ? wd : 1.0);
+        cz[c] = use_warm ? wd2 * rcp(cs[c]) : rcp(cs[c]);
         pc[c] = rcp(1.0 + fabs(rw.chi[c]));
     }
     const double nsides = (double)(G * (2 * SEP_D * SB + (has_cbf ? CB : 0) + (slk ? 1 : 0)));
@@ -642,6 +663,15 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #endif
     }
     if (v_out) *v_out = slk ? v : 0.0;
+    if (warm != nullptr && out.status == ST_OPTIMAL) {
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                warm->zl[d][k] = zl[d][k];
+                warm->zu[d][k] = zu[d][k];
+            }
+    }
 #ifdef MPCCBF_DEBUG_EXIT
     if (dbg) {  // per-lane exit iteration (all lanes of a group must agree)
         const int gl = threadIdx.x & (G - 1);

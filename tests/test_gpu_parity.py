@@ -525,3 +525,27 @@ def test_grid_bucket_overflow_falls_back_to_full_scan(mpclib):
             states = r["final"].cpu().numpy()
             ref, _ = _manual_loop(ctx, st, tg, 4, 0, n, torch)
             np.testing.assert_array_equal(states, ref)
+
+
+@pytest.mark.parametrize("scale", [0.55, 0.42])
+def test_iteration1_warm_start_matches_cold_start(mpclib, monkeypatch, scale):
+    """IMPC iteration 1 warm-started from iteration 0's primal-dual point (the default,
+    MPCCBF_WARM_DELTA = 0.3) and cold-started (0) reach the same optima: statuses equal,
+    objectives within solver tolerance; the warm start saves Newton steps on iteration 1."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(1024, seed=5)
+    states[:, :2] *= scale
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    res = {}
+    for delta in ("0", "0.3"):
+        monkeypatch.setenv("MPCCBF_WARM_DELTA", delta)  # read when the context is created
+        res[delta] = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    cold, warm = res["0"], res["0.3"]
+    np.testing.assert_array_equal(cold["status"], warm["status"])
+    ok = cold["status"] == 0
+    assert ok[:, 1].sum() > 200
+    err = np.abs(cold["obj"][ok] - warm["obj"][ok]) / np.maximum(1.0, np.abs(cold["obj"][ok]))
+    assert err.max() <= 1e-7, err.max()
+    assert np.nanmax(np.abs(cold["x"] - warm["x"])) <= 1e-5
+    assert warm["iters"][ok[:, 1], 1].mean() < cold["iters"][ok[:, 1], 1].mean()
