@@ -95,6 +95,9 @@ typedef struct mpccbf_options {
     int32_t no_cbf_filter;     /* 1: keep every CBF row (no exact in-kernel redundancy filter) */
     int32_t max_pdip_iters;    /* default 60 */
     double tolerance;          /* PDIP relative tolerance, default 1e-9 */
+    /* IMPC iteration 1 starts from iteration 0's primal-dual point (same box rows and cost) with
+     * a cold retry if that start does not converge; env MPCCBF_WARM_DELTA (read here, default
+     * 0.3, 0 = cold) sets its slack / dual floor. Statuses and optima do not depend on it. */
 } mpccbf_options;
 
 /* Validates p like parsing.hpp:37-135,182-214, builds the parameter-only operators on the host
