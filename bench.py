@@ -9,8 +9,13 @@ Default workload (N=1): BASELINE config 3 — 4096 agents, horizon 15, pairwise 
 8 nearest neighbours within 3 d_min, base_config.json parameters. Multi-GPU: weak scaling,
 4096 agents per GPU (config 4's 8192 agents at --gpus 2; --agents-total 8192 pins config 4).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]      (N > 1: relaunches itself as N ranks)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Timing: the timed pass runs warm-up + K steps with nothing else on the stream (barrier +
+synchronize on both sides, max over ranks); an identical replay of the same steps (same initial
+swarm and counter-based noise) records HIP events around every step and every IMPC kernel for the
+p99 step latency and the kernel's average duration (roofline).
 """
 from __future__ import annotations
 
@@ -79,8 +84,42 @@ def flops_per_qp_sep(iters: np.ndarray, rows: int) -> float:
     return float(np.sum(iters * (rows * 60 + 100)))
 
 
+STATUS_NAMES = {0: "OPTIMAL", 3: "INFEASIBLE", 4: "ERROR", 5: "UNKNOWN"}
+
+
+def spawn_ranks(args) -> None:
+    """`--gpus N` outside torch.distributed.run: relaunch this command as N ranks (one process per
+    GPU, torch.distributed.run on 127.0.0.1) before anything touches the GPU, and exit with the
+    launcher's code. A torchrun environment whose WORLD_SIZE differs from --gpus is an error."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
+def algorithmic_bytes_per_agent(n: int, knn: int, impc_iter: int, cov: bool) -> int:
+    """HBM bytes one agent-step must move: state 48 + target 24 + knn neighbour
+    states (px, py, vx, vy: 32 each) + the kept curve x (8 n) + per-iteration status, iterations
+    and objective (16 each) + next state 48 + trajectory time read / write 16 (+ 24 per neighbour
+    covariance in FoV slack mode)."""
+    return 48 + 24 + 32 * knn + 8 * n + 16 * impc_iter + 48 + 16 + (24 * knn if cov else 0)
+
+
 def main():
     args = parse()
+    spawn_ranks(args)
     import torch
     import torch.distributed as dist
     from mpccbf import swarm, Context, Comm, comm_unique_id
@@ -90,10 +129,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE",
-                  file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -128,8 +163,9 @@ def main():
     out = ctx.alloc_outputs(per, device=dev)
     out.pop("next_states")  # written straight into the next state table
     nsteps = args.steps
-    status_log = torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev)
-    iters_log = torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev)
+    logs = [(torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev),
+             torch.empty((nsteps, per, cfg["impc_iter"]), dtype=torch.int32, device=dev))
+            for _ in range(2)]
     full0 = torch.tensor(states_h, dtype=torch.float64, device=dev)
 
     def barrier_sync():
@@ -138,9 +174,11 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    replay_same = None
     if args.loop == "native" and args.neighbours == "grid":
-        # the whole closed loop in libmpccbf (mpccbf_run_steps): per step the grid build, the
-        # fused IMPC kernel and, across ranks, one in-place RCCL all-gather of agent states
+        # the whole closed loop in libmpccbf (mpccbf_run_steps): per step the fused IMPC kernel
+        # (neighbour query, both IMPC QPs, next-step neighbour table) and, across ranks, one
+        # in-place RCCL all-gather of agent states
         comm = None
         if world > 1:
             uid = torch.zeros(COMM_ID_BYTES, dtype=torch.uint8, device=dev)
@@ -148,26 +186,37 @@ def main():
                 uid.copy_(torch.tensor(list(comm_unique_id()), dtype=torch.uint8))
             dist.broadcast(uid, 0)
             comm = Comm(bytes(uid.cpu().tolist()), world, rank, local)
-        tables = [full0, torch.empty_like(full0)]
-        # the example's closed loop: fallback to the last successful trajectory, state noise
-        # pos_std / vel_std of base_config.json physical_limits (example :150-221)
-        traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
-        common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn,
-                      knn_radius=radius, x=out["x"], obj=out["obj"], comm=comm, traj_t=traj_t,
-                      pos_std=0.001, vel_std=0.01, noise_seed=20251015, cov=cov)
-        r = ctx.run_steps(tables[0], tables[1], args.warmup, status=out["status"],
-                          iters=out["iters"], reserve_steps=nsteps, **common)
-        if r["final"] is not tables[0]:
-            tables.reverse()
-        barrier_sync()
-        t0 = time.perf_counter()
-        # one event per step (p99 step latency); the IMPC kernel is bracketed by its own events on
-        # every 16th step only (each event pair adds ~10 us of barrier packets to a step)
-        r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=status_log, iters_log=iters_log,
-                          timing=True, solve_stride=16, step_index=args.warmup, **common)
-        barrier_sync()
-        t1 = time.perf_counter()
-        step_ms, kern_ms = r["step_ms"].astype(np.float64), r["solve_ms"].astype(np.float64)
+
+        def closed_loop(log, timing):
+            """warm-up + nsteps control steps from the initial swarm; returns (seconds, run dict).
+            timing=False: nothing but the steps on the stream (the throughput pass);
+            timing=True: HIP events around every step and every IMPC kernel (the replay)."""
+            tables = [full0.clone(), torch.empty_like(full0)]
+            # the example's closed loop: fallback to the last successful trajectory, state noise
+            # pos_std / vel_std of base_config.json physical_limits (example :150-221)
+            traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
+            out["x"].fill_(float("nan"))
+            common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn,
+                          knn_radius=radius, x=out["x"], obj=out["obj"], comm=comm, traj_t=traj_t,
+                          pos_std=0.001, vel_std=0.01, noise_seed=20251015, cov=cov)
+            r = ctx.run_steps(tables[0], tables[1], args.warmup, status=out["status"],
+                              iters=out["iters"], reserve_steps=nsteps, **common)
+            if r["final"] is not tables[0]:
+                tables.reverse()
+            barrier_sync()
+            t0 = time.perf_counter()
+            r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=log[0], iters_log=log[1],
+                              timing=timing, solve_stride=1, step_index=args.warmup, **common)
+            barrier_sync()
+            return time.perf_counter() - t0, r
+
+        elapsed, _ = closed_loop(logs[0], timing=False)
+        # replay of the identical steps (same initial swarm, counter-based noise keyed by the step
+        # index) with HIP events on the launch stream: per-step device time (p99) and the IMPC
+        # kernel's duration on every step (roofline), without perturbing the throughput pass
+        _, rr = closed_loop(logs[1], timing=True)
+        step_ms, kern_ms = rr["step_ms"].astype(np.float64), rr["solve_ms"].astype(np.float64)
+        replay_same = bool(torch.equal(logs[0][0], logs[1][0]) and torch.equal(logs[0][1], logs[1][1]))
         if comm is not None:
             comm.close()
     else:
@@ -186,8 +235,8 @@ def main():
         def step(slot, kev_pair=None):
             states = shard.full
             nb = neighbours(states)
-            st = status_log[slot] if slot is not None else out["status"]
-            it = iters_log[slot] if slot is not None else out["iters"]
+            st = logs[0][0][slot] if slot is not None else out["status"]
+            it = logs[0][1][slot] if slot is not None else out["iters"]
             if kev_pair is not None:
                 kev_pair[0].record(stream)
             ctx.impc_solve(states, targets=targets, agent_first=first, num_agents=per,
@@ -209,43 +258,57 @@ def main():
             step(i, kev[i])
             ev[i + 1].record(stream)
         barrier_sync()
-        t1 = time.perf_counter()
+        elapsed = time.perf_counter() - t0
         step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(nsteps)])
         kern_ms = np.array([a.elapsed_time(b) for a, b in kev])
-    elapsed = t1 - t0
 
-    status = status_log.cpu().numpy()
-    iters = iters_log.cpu().numpy()
-    attempted = int(np.sum(~((status == 5) & (iters == 0))))
-    optimal = int(np.sum(status == 0))
+    status = logs[0][0].cpu().numpy()
+    iters = logs[0][1].cpu().numpy()
+    attempted = ~((status == 5) & (iters == 0))  # UNKNOWN with 0 steps: iteration not attempted
+    hist = {name: int(np.sum((status == code) & attempted)) for code, name in STATUS_NAMES.items()}
+    hist["not_attempted"] = int(np.sum(~attempted))
     rows = ctx.shared_rows  # CBF rows are few (filtered); counted as shared rows only
     kname = ctx.kernel_name
     if kname.startswith("impc_sep_kernel"):
         flops = flops_per_qp_sep(iters.reshape(-1), rows)
     else:
         flops = flops_per_qp(iters.reshape(-1), np.full(iters.size, rows), ctx.nz)
+    # Newton steps per QP over the step index (the first steps from the lattice are the transient)
+    att_it = np.where(attempted, iters, 0)
+    newton_mean = att_it.sum(axis=(1, 2)) / np.maximum(attempted.sum(axis=(1, 2)), 1)
+    newton_max = att_it.max(axis=(1, 2))
 
-    t = torch.tensor([elapsed, float(attempted), float(optimal), flops, float(np.mean(kern_ms)),
-                      float(np.percentile(step_ms, 99))], dtype=torch.float64, device=dev)
+    vals = [elapsed, float(hist["OPTIMAL"]), float(hist["INFEASIBLE"]), float(hist["UNKNOWN"]),
+            float(hist["ERROR"]), float(hist["not_attempted"]), flops, float(np.mean(kern_ms)),
+            float(np.percentile(step_ms, 99)), float(np.max(kern_ms)), float(bool(replay_same) or replay_same is None)]
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
     if world > 1:
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, kern_avg, p99 = float(mx[0]), float(mx[4]), float(mx[5])
-        attempted, optimal, flops = float(sm[1]), float(sm[2]), float(sm[3])
-        flops_rank0 = float(t[3])
+        mn = t.clone()
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        elapsed, kern_avg, p99, kern_max = float(mx[0]), float(mx[7]), float(mx[8]), float(mx[9])
+        for i, k in enumerate(("OPTIMAL", "INFEASIBLE", "UNKNOWN", "ERROR", "not_attempted")):
+            hist[k] = int(sm[1 + i])
+        flops_rank0 = float(t[6])
+        replay_same = bool(mn[10] > 0.5) if replay_same is not None else None
     else:
-        elapsed, attempted, optimal, flops, kern_avg, p99 = [float(v) for v in t.tolist()]
+        kern_avg, p99, kern_max = vals[7], vals[8], vals[9]
         flops_rank0 = flops
 
     if rank == 0:
-        qps = attempted / elapsed
+        solved = hist["OPTIMAL"] + hist["INFEASIBLE"]
+        attempted_n = solved + hist["UNKNOWN"] + hist["ERROR"]
+        qps = solved / elapsed
         # roofline of the dominant kernel on rank 0: executed algorithmic flops per launch /
-        # average launch time (FP64-compute bound; bytes per launch are tiny)
+        # average launch time (HIP events on the launch stream, every step of the replay)
         flops_per_launch = flops_rank0 / nsteps
         achieved_tf = flops_per_launch / (kern_avg * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic(kname)
+        abytes = algorithmic_bytes_per_agent(ctx.n, args.knn, cfg["impc_iter"], cov is not None) * per
+        bound = "mfma" if kname.startswith("impc_fov") else "valu"
         res = {
             "metric": "QP solves/sec (whole node) + p99 step latency, N-agent horizon-15 MPC-CBF",
             "value": qps,
@@ -279,23 +342,44 @@ def main():
                 "qp": {"n": ctx.n, "nz": ctx.nz, "shared_rows": ctx.shared_rows},
                 "parallelism": f"dp{world}",
             },
-            "qps_attempted": attempted,
-            "qps_optimal_frac": optimal / max(attempted, 1),
+            # value counts OPTIMAL and INFEASIBLE QPs (the latter certified by phase 1 and
+            # oracle-confirmed on this workload, tests/test_gpu_status_parity.py); UNKNOWN / ERROR
+            # are attempted but not counted
+            "qps_solved": solved,
+            "qps_attempted": attempted_n,
+            "qps_optimal_frac": hist["OPTIMAL"] / max(attempted_n, 1),
+            "status_hist": hist,
+            "newton_steps_per_qp": ({"mean_by_step": [round(float(v), 3) for v in newton_mean],
+                                     "max_by_step": [int(v) for v in newton_max]}
+                                    if nsteps <= 64 else
+                                    {"mean": float(np.mean(newton_mean)), "max": int(np.max(newton_max))}),
             "roofline": {
-                "bound": "mfma",
+                "bound": bound,
                 "achieved": achieved_tf,
                 "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_tf / FP64_PEAK_TFLOPS,
                 "traffic": traffic,
-                "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE + WRITE_SIZE, gfx950-corrected)",
                 "traffic_source": traffic_src,
                 "kernel": kname,
                 "kernel_avg_us": kern_avg * 1e3,
+                "kernel_max_us": kern_max * 1e3,
+                "kernel_timing": "HIP events around the IMPC kernel on its stream, every step of "
+                                 "an identical replay of the timed steps" + (
+                                     " (statuses bit-identical to the timed pass)" if replay_same else ""),
                 "flops_per_launch": flops_per_launch,
+                "flops_model": "executed Newton steps x per-step FP64 flops of the condensed PDIP "
+                               "(bench.py flops_per_qp_sep); QPs solved by the fast start count 0",
+                "hbm": {"algorithmic_bytes_per_launch": abytes,
+                        "achieved_gbs": abytes / (kern_avg * 1e-3) / 1e9,
+                        "peak_gbs": HBM_PEAK_GBS,
+                        "frac": abytes / (kern_avg * 1e-3) / 1e9 / HBM_PEAK_GBS},
             },
             "cpu_baseline": None,
         }
+        if replay_same is False:
+            res["roofline"]["kernel_timing"] += " (WARNING: replay statuses differ)"
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h)
         print(json.dumps(res), flush=True)

@@ -41,6 +41,9 @@ struct DevOps {
     // IMPC iteration 1 warm start (impc_sep_kernel, no slack mode): the PDIP starts from
     // iteration 0's solution with slacks and duals floored at warm_delta (0: cold start)
     double warm_delta;
+    // divergence test of the first solve (PdipCfg::early_it; 0 = off)
+    int32_t early_it;
+    int32_t fast_start;  // PdipCfg::fast_start
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;

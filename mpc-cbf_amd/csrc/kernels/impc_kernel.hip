@@ -347,39 +347,68 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
             long long* dbg = (args.stamps && it == 0)
                                  ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 16
                                  : nullptr;
+#elif defined(MPCCBF_SOLVE_TRACE)  // per-step (rp, mu, alpha, rd) of the first solve + phase 1
+            long long* dbg = args.stamps ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP +
+                                               ((size_t)ai * 2 + it) * 256
+                                         : nullptr;
 #else
             long long* dbg = nullptr;
 #endif
+            // Attempts (group-uniform; one call site): 0 = warm start (IMPC iteration 1) or cold,
+            // with the divergence test; 1 = cold to the iteration limit; 2 = cold with the shifted
+            // Newton matrix. Before any retry, phase 1 certifies feasibility (minimal uniform row
+            // violation above the tolerance, from the failed solve's last iterate), so an
+            // infeasible QP needs no retry and statuses never depend on the first attempt's
+            // warm start or divergence test.
             const bool warm_try = it > 0 && warm_delta > 0.0;
-            PdipOut po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr),
-                                                          q, y, cfg, dbg, wslack, &vslack, red_all[gib],
-                                                          &warm, warm_try ? warm_delta : 0.0);
-            if (warm_try && po.status != ST_OPTIMAL) {
-                // a warm start that does not converge is retried cold, so the statuses never
-                // depend on it (group-uniform)
-                const int wit = po.iters;
+            int tr_warm = 0, tr_cold = 0, tr_p1 = 0;  // diagnostics (MPCCBF_SOLVE_TRACE)
+            int attempt = 0, total = 0;
+            bool certified = false, infeas = false;
+            PdipOut po{ST_UNKNOWN, 0};
+            for (;;) {
+                PdipCfg ca = cfg;
+                ca.early_it = attempt == 0 ? op.early_it : 0;
+                ca.fast_start = op.fast_start != 0;
+                ca.robust = attempt == 2;
                 po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y,
-                                                      cfg, dbg, wslack, &vslack, red_all[gib], &warm, 0.0);
-                po.iters += wit;
+                                                      ca, dbg, wslack, &vslack, red_all[gib], &warm,
+                                                      (attempt == 0 && warm_try) ? warm_delta : 0.0);
+                total += po.iters;
+                ((attempt == 0 && warm_try) ? tr_warm : tr_cold) += po.iters;
+                if (po.status == ST_OPTIMAL) break;
+                if (!certified) {
+                    SepRows<SB, CB> rp1 = rw;
+                    if constexpr (SLACK) {  // slack rows are always satisfiable: certify the box rows
+#pragma unroll
+                        for (int c = 0; c < CB; c++) {
+#pragma unroll
+                            for (int j = 0; j < 4; j++) rp1.cg[c][j] = 0.0;
+                            rp1.chi[c] = 1.0;
+                        }
+                    }
+                    const double tstar =
+                        pdip_phase1_sep<G, SB, CB>(rp1, cfg, op.feas_tol, y, red_all[gib], &tr_p1, dbg);
+                    infeas = tstar > op.feas_tol && tstar < 1e300;  // 1e300: phase 1 failed
+                    certified = true;
+#ifdef MPCCBF_DEBUG_EXIT
+                    total += tstar >= 1e300 ? 10000 : 0;
+#endif
+                }
+                if (infeas) {
+                    po.status = ST_INFEASIBLE;
+                    break;
+                }
+                if (attempt == 0 && (warm_try || po.early)) attempt = 1;
+                else if (attempt < 2) attempt = 2;
+                else break;
             }
             st = po.status;
-            nit = po.iters;
-            if (st != ST_OPTIMAL) {
-                SepRows<SB, CB> rp1 = rw;
-                if constexpr (SLACK) {  // slack rows are always satisfiable: certify the box rows
-#pragma unroll
-                    for (int c = 0; c < CB; c++) {
-#pragma unroll
-                        for (int j = 0; j < 4; j++) rp1.cg[c][j] = 0.0;
-                        rp1.chi[c] = 1.0;
-                    }
-                }
-                const double tstar = pdip_phase1_sep<G, SB, CB>(rp1, cfg);
-                if (tstar > op.feas_tol && tstar < 1e300) st = ST_INFEASIBLE;  // 1e300: phase 1 failed
-#ifdef MPCCBF_DEBUG_EXIT
-                nit += tstar >= 1e300 ? 10000 : 0;
+            nit = total;
+#ifdef MPCCBF_SOLVE_TRACE  // diagnostics build: warm + 100 cold + 10000 phase-1 iterations
+            nit = tr_warm + 100 * tr_cold + 10000 * tr_p1;
+#else
+            (void)tr_warm, (void)tr_cold, (void)tr_p1;
 #endif
-            }
         }
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {

@@ -109,11 +109,27 @@ struct PdipCfg {
     int maxit;
     double tol;
     double reg = 0.0;  // added to the Newton matrix diagonal (direction only; residuals exact)
+    // divergence test of pdip_solve_sep: from Newton step early_it on, complementarity above
+    // early_mu x its starting value stops the solve (0: off). A QP with no feasible point drives
+    // mu up while the iterate stalls; phase 1 then decides, and a feasible QP is re-solved
+    // without the test, so statuses never depend on it.
+    int early_it = 0;
+    double early_mu = 1.5;
+    // pdip_solve_sep: Newton matrix shifted by 1e-12 of its largest diagonal entry at every step
+    // (inexact Newton, exact residuals and convergence test): the last attempt after a
+    // factorisation breakdown at a degenerate point (active rows' D = z/s ~1e20 against P ~1e5)
+    bool robust = false;
+    // pdip_solve_sep: return the unconstrained minimiser when it satisfies every row
+    bool fast_start = true;
+    // pdip_solve_sep: relative dual residual accepted once primal feasibility and mu are three
+    // orders past their targets (SURVEY.md §8c parity rule; CPLEX's default optimality tolerance)
+    double rd_relax = 1e-6;
 };
 
 struct PdipOut {
     int status;
     int iters;
+    bool early = false;  // stopped by the divergence test (phase 1 decides; pdip_solve_sep)
 };
 
 // step-to-boundary of s + a ds >= 0 (or z): returns the limiting a, or `big` if ds >= 0
@@ -355,7 +371,7 @@ __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ 
 // the decision a 1e-6 row-violation tolerance (CPLEX's default) makes, and the rule the oracle
 // applies (oracle/oracle.cpp phase1). Only run for QPs whose main solve did not converge.
 template <int NZ, int G, int R>
-__device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
+__device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg, int* iters_out = nullptr) {
     constexpr int NV = NZ + 1;
     using S = Sym<NV>;
     constexpr double eps = 1e-10;
@@ -380,7 +396,8 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
     }
     double zt = rcp(t);
     const double inv_ns = rcp(grp_sum<G>(nloc) + 1.0);
-    for (int it = 0; it < 2 * cfg.maxit; it++) {
+    int it = 0;
+    for (; it < 2 * cfg.maxit; it++) {
         constexpr int NA = S::P + NV + 1;
         double acc[NA];
 #pragma unroll
@@ -416,7 +433,10 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
         grp_sum_vec<G, NA>(acc);
         rp = grp_max<G>(rp);
         const double mu = (acc[NA - 1] + t * zt) * inv_ns;
-        if (!isfinite(mu) || !isfinite(rp)) return 1e300;
+        if (!isfinite(mu) || !isfinite(rp)) {
+            if (iters_out) *iters_out = it;
+            return 1e300;
+        }
         if (rp <= cfg.tol && mu <= cfg.tol * 0.1) break;
         double M[S::P], dinv[NV], rhs[NV], dv[NV];
         const double Dt = zt * rcp(t);
@@ -509,6 +529,7 @@ __device__ double pdip_phase1(const Rows<NZ, R>& rw, const PdipCfg cfg) {
             zu[r] = rw.mu[r] * fmax(fma(alpha, dzu[r], zu[r]), 1e-300);
         }
     }
+    if (iters_out) *iters_out = it;
     // t* from the iterate: the largest actual row violation at y (>= 0)
     double worst = 0.0;
 #pragma unroll

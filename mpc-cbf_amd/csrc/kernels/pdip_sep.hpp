@@ -98,16 +98,52 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
     // duals, both floored at delta (complementarity >= delta^2), CBF rows centred at delta^2
     const bool use_warm = warm != nullptr && warm_delta > 0.0;
     const double wd = warm_delta, wd2 = warm_delta * warm_delta;
-    // ---- start: unconstrained minimiser (block-diagonal P: per-channel 2x2 solves)
-    if (!use_warm) {
+    // ---- start: unconstrained minimiser (block-diagonal P: per-channel 2x2 solves). When it
+    // satisfies every row it is the optimum (convex QP, all multipliers zero; slack mode: v = 0
+    // since its cost is positive): no Newton step needed.
+    {
+        double yu[SEP_NZ];
 #pragma unroll
         for (int d = 0; d < SEP_D; d++) {
             const int o = 2 * d;
             const double l00 = LP[o * 6 + o], l10 = LP[(o + 1) * 6 + o], l11 = LP[(o + 1) * 6 + o + 1];
             const double w0 = -q[o] * rcp(l00);
             const double w1 = (-q[o + 1] - l10 * w0) * rcp(l11);
-            y[o + 1] = w1 * rcp(l11);
-            y[o] = (w0 - l10 * y[o + 1]) * rcp(l00);
+            yu[o + 1] = w1 * rcp(l11);
+            yu[o] = (w0 - l10 * yu[o + 1]) * rcp(l00);
+        }
+        bool bad = false;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                const double t = rw.bg[d][k][0] * yu[2 * d] + rw.bg[d][k][1] * yu[2 * d + 1];
+                bad = bad || !(t >= rw.blo[d][k] && t <= rw.bhi[d][k]);  // NaN-safe
+            }
+        if (has_cbf) {
+#pragma unroll
+            for (int c = 0; c < CB; c++) {
+                double t = 0.0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], yu[j], t);
+                bad = bad || !(t <= rw.chi[c]);
+            }
+        }
+        if (cfg.fast_start && grp_ballot<G>(bad) == 0ull) {
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
+            if (v_out) *v_out = 0.0;
+            if (warm != nullptr) {
+#pragma unroll
+                for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+                    for (int k = 0; k < SB; k++) warm->zl[d][k] = warm->zu[d][k] = 0.0;
+            }
+            return PdipOut{ST_OPTIMAL, 0};
+        }
+        if (!use_warm) {
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
         }
     }
     // slacks (s) and duals (z): box lower / upper sides, CBF upper side
@@ -358,15 +394,24 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             return rdn * inv_qn;
         };
         if (finite && rp <= cfg.tol && mu <= cfg.tol * 0.1) {
-            if (rd_track <= cfg.tol) {
+            // a degenerate optimum (active rows' D = z/s ~1e20) can stall the dual residual above
+            // the tolerance while mu keeps falling; three orders below the mu target it is
+            // accepted at the dual tolerance of the parity rule / CPLEX (PdipCfg::rd_relax)
+            const bool stalled = mu <= cfg.tol * 1e-4;
+            if (rd_track <= cfg.tol || stalled) {
                 rd_track = exact_rd();
-                if (rd_track <= cfg.tol) {
+                if (rd_track <= cfg.tol || (stalled && rd_track <= cfg.rd_relax)) {
                     out.status = ST_OPTIMAL;
                     break;
                 }
             }
         }
         if (it == 0) mu0 = mu;
+        if (cfg.early_it > 0 && it >= cfg.early_it && mu > cfg.early_mu * mu0) {
+            out.status = ST_UNKNOWN;  // diverging: phase 1 decides (see PdipCfg::early_it)
+            out.early = true;
+            break;
+        }
         if (it >= cfg.maxit || !finite || mu > 1e8 * fmax(mu0, 1.0)) {
             // out of iterations at a degenerate point the normal matrix can no longer resolve:
             // the same relaxed KKT acceptance as at a factorisation breakdown (below)
@@ -400,7 +445,12 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             Mw[1] = acc[A_MW + 1] + P[4 * 6 + 5];
             Mw[2] = acc[A_MW + 2] + P[5 * 6 + 5] + tau;
         };
-        form(0.0);
+        double tau0 = 0.0;
+        if (cfg.robust)
+            tau0 = 1e-12 * fmax(fmax(fmax(acc[A_MX + 0] + P[0], acc[A_MX + 2] + P[7]),
+                                     fmax(acc[A_MY + 0] + P[14], acc[A_MY + 2] + P[21])),
+                                fmax(acc[A_MW + 0] + P[28], acc[A_MW + 2] + P[35]));
+        form(tau0);
         bool ok4 = chol_packed<4>(Mxy, dxy);
         bool ok2 = chol_packed<2>(Mw, dw);
         if (MPCCBF_SHIFT_RETRY && !(ok4 && ok2)) {
@@ -648,6 +698,15 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         rd_track *= (1.0 - alpha);
         if (it % 8 == 7) rd_exact = true;
         PSTAMP(11);
+#ifdef MPCCBF_SOLVE_TRACE
+        if (dbg && it < 32 && (threadIdx.x & (G - 1)) == 0) {
+            double* dd = (double*)dbg;
+            dd[it * 4 + 0] = rp;
+            dd[it * 4 + 1] = mu;
+            dd[it * 4 + 2] = alpha;
+            dd[it * 4 + 3] = rd_track;
+        }
+#endif
 #ifdef MPCCBF_DEBUG_EXIT
         if (dbg) {  // lane divergence of the iterate (must stay 0: y is group-uniform)
             double dvg = 0.0;
@@ -681,37 +740,352 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
     return out;
 }
 
-// Phase 1 on the separable rows: expand to the dense row form and reuse pdip_phase1 (only runs
-// for QPs whose main solve did not converge).
+// Phase 1 on the separable rows (only runs for QPs whose main solve did not converge):
+//     t* = min t   s.t.  lo - t <= g y <= hi + t  (box rows),  cg y - t <= chi  (CBF rows),  t >= 0
+// with the ridge eps/2 |y|^2 of pdip_phase1. The Newton matrix keeps the separable structure,
+// M = [[A, b], [b^T, c]] with A the (x, y) 4x4 + yaw 2x2 blocks of pdip_solve_sep and (b, c) the
+// t column; it is solved through the Schur complement on t (u = A^-1 b once per step, then
+// dt = (r_t - b^T A^-1 r_y) / (c - b^T u), dy = A^-1 r_y - u dt), so a step costs about one main
+// Newton step instead of a dense 7x7 one. Returns the largest row violation at the final y (an
+// upper bound of t*, equal to it at convergence; the QP is INFEASIBLE iff it exceeds feas_tol).
+// It stops as soon as that decision is settled:
+//   * the row violation at the iterate is <= feas_tol (a point feasible within the tolerance);
+//   * the iterate is primal feasible for the phase-1 LP (relative residual <= tol), t >= 1e-4
+//     and the duality gap is <= 1e-3 t, so t* >= t - gap > 0.999e-4 >> feas_tol;
+// otherwise it converges fully (residual and mu at the main tolerance), as pdip_phase1 does.
 template <int G, int SB, int CB>
-__device__ double pdip_phase1_sep(const SepRows<SB, CB>& rw, const PdipCfg cfg) {
-    constexpr int R = SEP_D * SB + CB;
-    Rows<SEP_NZ, R> dr;
+__device__ double pdip_phase1_sep(const SepRows<SB, CB>& rw, const PdipCfg cfg, double feas_tol,
+                                  const double (&ystart)[SEP_NZ], double* red = nullptr,
+                                  int* iters_out = nullptr, long long* dbg = nullptr) {
+    (void)dbg;
+    constexpr double eps = 1e-10;
+    constexpr int P_MX = 0, P_MY = 3, P_MW = 6, P_MC = 9, P_B = 13, P_C = 19, P_R = 20, P_RT = 26,
+                  P_MU = 27, P_N = 28;
+    // start at ystart (the main solve's last iterate: close to the least violating point; the
+    // origin if it is not finite), t = its largest violation + 1, so every slack is >= 1
+    double y[SEP_NZ];
+    bool fin = true;
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) fin = fin && isfinite(ystart[j]);
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) y[j] = fin ? ystart[j] : 0.0;
+    double viol = 0.0;
 #pragma unroll
     for (int d = 0; d < SEP_D; d++)
 #pragma unroll
         for (int k = 0; k < SB; k++) {
-            const int r = d * SB + k;
-#pragma unroll
-            for (int j = 0; j < SEP_NZ; j++) dr.g[r][j] = 0.0;
-            dr.g[r][2 * d] = rw.bg[d][k][0];
-            dr.g[r][2 * d + 1] = rw.bg[d][k][1];
-            dr.lo[r] = rw.blo[d][k];
-            dr.hi[r] = rw.bhi[d][k];
-            dr.ml[r] = 1.0;
-            dr.mu[r] = 1.0;
+            const double ty = rw.bg[d][k][0] * y[2 * d] + rw.bg[d][k][1] * y[2 * d + 1];
+            viol = fmax(viol, fmax(rw.blo[d][k] - ty, ty - rw.bhi[d][k]));
         }
 #pragma unroll
     for (int c = 0; c < CB; c++) {
-        const int r = SEP_D * SB + c;
+        double tc = 0.0;
 #pragma unroll
-        for (int j = 0; j < SEP_NZ; j++) dr.g[r][j] = j < 4 ? rw.cg[c][j] : 0.0;
-        dr.lo[r] = 0.0;
-        dr.ml[r] = 0.0;
-        dr.hi[r] = rw.chi[c];
-        dr.mu[r] = 1.0;
+        for (int j = 0; j < 4; j++) tc = fma(rw.cg[c][j], y[j], tc);
+        viol = fmax(viol, tc - rw.chi[c]);
     }
-    return pdip_phase1<SEP_NZ, G, R>(dr, cfg);
+    double t = grp_max<G>(viol) + 1.0;
+    double sl[SEP_D][SB], su[SEP_D][SB], zl[SEP_D][SB], zu[SEP_D][SB], pl[SEP_D][SB], pu[SEP_D][SB];
+    double cs[CB], cz[CB], pc[CB];
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+        for (int k = 0; k < SB; k++) {
+            const double ty = rw.bg[d][k][0] * y[2 * d] + rw.bg[d][k][1] * y[2 * d + 1];
+            sl[d][k] = ty + t - rw.blo[d][k];
+            su[d][k] = rw.bhi[d][k] - ty + t;
+            zl[d][k] = rcp(sl[d][k]);
+            zu[d][k] = rcp(su[d][k]);
+            pl[d][k] = rcp(1.0 + fabs(rw.blo[d][k]));
+            pu[d][k] = rcp(1.0 + fabs(rw.bhi[d][k]));
+        }
+#pragma unroll
+    for (int c = 0; c < CB; c++) {
+        double tc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) tc = fma(rw.cg[c][j], y[j], tc);
+        cs[c] = rw.chi[c] - tc + t;
+        cz[c] = rcp(cs[c]);
+        pc[c] = rcp(1.0 + fabs(rw.chi[c]));
+    }
+    double zt = rcp(t);
+    const double inv_ns = 1.0 / (double)(G * (2 * SEP_D * SB + CB) + 1);
+    const int gl = threadIdx.x & (G - 1);
+    int it = 0;
+    for (; it < 2 * cfg.maxit; it++) {
+        double acc[P_N];
+#pragma unroll
+        for (int k = 0; k < P_N; k++) acc[k] = 0.0;
+        double rl[SEP_D][SB], ru[SEP_D][SB], il[SEP_D][SB], iu[SEP_D][SB], cr[CB], ci[CB], Dc[CB];
+        double rp = 0.0, worst = 0.0;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                const double g0 = rw.bg[d][k][0], g1 = rw.bg[d][k][1];
+                const double ty = g0 * y[2 * d] + g1 * y[2 * d + 1];
+                rl[d][k] = ty + t - rw.blo[d][k] - sl[d][k];
+                ru[d][k] = rw.bhi[d][k] - ty + t - su[d][k];
+                il[d][k] = rcp(sl[d][k]);
+                iu[d][k] = rcp(su[d][k]);
+                const double Dl = zl[d][k] * il[d][k], Du = zu[d][k] * iu[d][k];
+                const double wl = -Dl * rl[d][k], wu = -Du * ru[d][k];
+                acc_blk2(acc + P_MX + 3 * d, Dl + Du, g0, g1);
+                acc[P_B + 2 * d] = fma(Dl - Du, g0, acc[P_B + 2 * d]);
+                acc[P_B + 2 * d + 1] = fma(Dl - Du, g1, acc[P_B + 2 * d + 1]);
+                acc[P_C] += Dl + Du;
+                acc[P_R + 2 * d] = fma(g0, wl - wu, acc[P_R + 2 * d]);
+                acc[P_R + 2 * d + 1] = fma(g1, wl - wu, acc[P_R + 2 * d + 1]);
+                acc[P_RT] += wl + wu;
+                acc[P_MU] = fma(sl[d][k], zl[d][k], fma(su[d][k], zu[d][k], acc[P_MU]));
+                rp = fmax(rp, fmax(fabs(rl[d][k]) * pl[d][k], fabs(ru[d][k]) * pu[d][k]));
+                worst = fmax(worst, fmax(rw.blo[d][k] - ty, ty - rw.bhi[d][k]));
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            const double* g = rw.cg[c];
+            double tc = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) tc = fma(g[j], y[j], tc);
+            cr[c] = rw.chi[c] - tc + t - cs[c];
+            ci[c] = rcp(cs[c]);
+            Dc[c] = cz[c] * ci[c];
+            const double D = Dc[c], w = -D * cr[c];
+            acc_blk2(acc + P_MX, D, g[0], g[1]);
+            acc_blk2(acc + P_MY, D, g[2], g[3]);
+            acc[P_MC + 0] = fma(D * g[0], g[2], acc[P_MC + 0]);
+            acc[P_MC + 1] = fma(D * g[0], g[3], acc[P_MC + 1]);
+            acc[P_MC + 2] = fma(D * g[1], g[2], acc[P_MC + 2]);
+            acc[P_MC + 3] = fma(D * g[1], g[3], acc[P_MC + 3]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                acc[P_B + j] = fma(-D, g[j], acc[P_B + j]);
+                acc[P_R + j] = fma(-g[j], w, acc[P_R + j]);
+            }
+            acc[P_C] += D;
+            acc[P_RT] += w;
+            acc[P_MU] = fma(cs[c], cz[c], acc[P_MU]);
+            rp = fmax(rp, fabs(cr[c]) * pc[c]);
+            worst = fmax(worst, tc - rw.chi[c]);
+        }
+        if (red) {  // two LDS passes through the 16 x 21 table of the main solver
+            double h0[14], h1[14];
+#pragma unroll
+            for (int k = 0; k < 14; k++) {
+                h0[k] = acc[k];
+                h1[k] = acc[14 + k];
+            }
+            grp_sum_vec_lds<14>(h0, red, gl);
+            grp_sum_vec_lds<14>(h1, red, gl);
+#pragma unroll
+            for (int k = 0; k < 14; k++) {
+                acc[k] = h0[k];
+                acc[14 + k] = h1[k];
+            }
+        } else {
+            grp_sum_vec<G, P_N>(acc);
+        }
+        grp_max2<G>(rp, worst);
+        const double gap = acc[P_MU] + t * zt;
+        const double mu = gap * inv_ns;
+        if (!isfinite(mu) || !isfinite(rp) || !isfinite(t)) {
+            if (iters_out) *iters_out = it;
+            return 1e300;
+        }
+#ifdef MPCCBF_SOLVE_TRACE
+        if (dbg && it < 32 && gl == 0) {
+            double* dd = (double*)dbg + 128;
+            dd[it * 4 + 0] = rp;
+            dd[it * 4 + 1] = mu;
+            dd[it * 4 + 2] = t;
+            dd[it * 4 + 3] = worst;
+        }
+#endif
+        if (worst <= feas_tol) break;  // feasible within the tolerance
+        if (rp <= cfg.tol && (mu <= cfg.tol * 0.1 || (t >= 1e-4 && gap <= 1e-3 * t))) break;
+        // ---- Newton matrix: A (4x4 + 2x2, ridge eps), t column b, corner c
+        using S4 = Sym<4>;
+        double Mxy[10], dxy[4], Mw[3], dw[2];
+        Mxy[S4::idx(0, 0)] = acc[P_MX + 0] + eps;
+        Mxy[S4::idx(0, 1)] = acc[P_MX + 1];
+        Mxy[S4::idx(1, 1)] = acc[P_MX + 2] + eps;
+        Mxy[S4::idx(2, 2)] = acc[P_MY + 0] + eps;
+        Mxy[S4::idx(2, 3)] = acc[P_MY + 1];
+        Mxy[S4::idx(3, 3)] = acc[P_MY + 2] + eps;
+        Mxy[S4::idx(0, 2)] = acc[P_MC + 0];
+        Mxy[S4::idx(0, 3)] = acc[P_MC + 1];
+        Mxy[S4::idx(1, 2)] = acc[P_MC + 2];
+        Mxy[S4::idx(1, 3)] = acc[P_MC + 3];
+        Mw[0] = acc[P_MW + 0] + eps;
+        Mw[1] = acc[P_MW + 1];
+        Mw[2] = acc[P_MW + 2] + eps;
+        if (!(chol_packed<4>(Mxy, dxy) && chol_packed<2>(Mw, dw))) break;  // the iterate stands
+        const double Dt = zt * rcp(t);
+        double bv[SEP_NZ], u[SEP_NZ];
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) bv[j] = acc[P_B + j];
+        sep_solve(Mxy, dxy, Mw, dw, bv, u);
+        double sch = acc[P_C] + Dt;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) sch = fma(-bv[j], u[j], sch);
+        if (!(sch > 0.0)) break;
+        const double isch = rcp(sch);
+        // solve [A b; b^T c] [dy; dt] = [ry; rt]
+        auto solve7 = [&](const double (&ry)[SEP_NZ], double rt, double (&dy)[SEP_NZ], double& dt) {
+            double w[SEP_NZ];
+            sep_solve(Mxy, dxy, Mw, dw, ry, w);
+            double v = rt;
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) v = fma(-bv[j], w[j], v);
+            dt = v * isch;
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) dy[j] = fma(-u[j], dt, w[j]);
+        };
+        // ---- predictor
+        double ry[SEP_NZ], dya[SEP_NZ], dta;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) ry[j] = fma(-eps, y[j], acc[P_R + j]);
+        solve7(ry, acc[P_RT] - 1.0, dya, dta);
+        double dsl[SEP_D][SB], dsu[SEP_D][SB], dzl[SEP_D][SB], dzu[SEP_D][SB], cds[CB], cdz[CB];
+        double rs = fmax(0.0, -dta * rcp(t)), rz = 1.0 + dta * rcp(t);  // t >= 0 side: s_t = t
+        const double dzta = -zt - Dt * dta;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                const double td = rw.bg[d][k][0] * dya[2 * d] + rw.bg[d][k][1] * dya[2 * d + 1];
+                dsl[d][k] = td + dta + rl[d][k];
+                dsu[d][k] = -td + dta + ru[d][k];
+                const double ql = dsl[d][k] * il[d][k], qu = dsu[d][k] * iu[d][k];
+                dzl[d][k] = -zl[d][k] * (1.0 + ql);
+                dzu[d][k] = -zu[d][k] * (1.0 + qu);
+                rs = fmax(rs, fmax(-ql, -qu));
+                rz = fmax(rz, fmax(1.0 + ql, 1.0 + qu));
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            double td = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) td = fma(rw.cg[c][j], dya[j], td);
+            cds[c] = -td + dta + cr[c];
+            const double qc = cds[c] * ci[c];
+            cdz[c] = -cz[c] * (1.0 + qc);
+            rs = fmax(rs, -qc);
+            rz = fmax(rz, 1.0 + qc);
+        }
+        grp_max2<G>(rs, rz);
+        const double ap = rcp(fmax(1.0, rs)), ad = rcp(fmax(1.0, rz));
+        double mua = 0.0;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                mua = fma(sl[d][k] + ap * dsl[d][k], zl[d][k] + ad * dzl[d][k], mua);
+                mua = fma(su[d][k] + ap * dsu[d][k], zu[d][k] + ad * dzu[d][k], mua);
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++) mua = fma(cs[c] + ap * cds[c], cz[c] + ad * cdz[c], mua);
+        mua = (grp_sum<G>(mua) + (t + ap * dta) * (zt + ad * dzta)) * inv_ns;
+        double sig = mu > 0.0 ? mua * rcp(mu) : 0.0;
+        sig = fmin(sig * sig * sig, 1.0);
+        const double smu = sig * mu;
+        // ---- corrector right-hand side
+        double vc[SEP_NZ + 1];
+#pragma unroll
+        for (int j = 0; j <= SEP_NZ; j++) vc[j] = 0.0;
+        double kl[SEP_D][SB], ku[SEP_D][SB], kc[CB];
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                kl[d][k] = smu - dsl[d][k] * dzl[d][k];
+                ku[d][k] = smu - dsu[d][k] * dzu[d][k];
+                const double a = kl[d][k] * il[d][k], b = ku[d][k] * iu[d][k];
+                vc[2 * d] = fma(rw.bg[d][k][0], a - b, vc[2 * d]);
+                vc[2 * d + 1] = fma(rw.bg[d][k][1], a - b, vc[2 * d + 1]);
+                vc[SEP_NZ] += a + b;
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            kc[c] = smu - cds[c] * cdz[c];
+            const double a = kc[c] * ci[c];
+#pragma unroll
+            for (int j = 0; j < 4; j++) vc[j] = fma(-rw.cg[c][j], a, vc[j]);
+            vc[SEP_NZ] += a;
+        }
+        grp_sum_vec<G, SEP_NZ + 1>(vc);
+        const double kt = smu - dta * dzta;
+        double vy[SEP_NZ], dyc[SEP_NZ], dtc;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) vy[j] = vc[j];
+        solve7(vy, vc[SEP_NZ] + kt * rcp(t), dyc, dtc);
+        double dy[SEP_NZ];
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) dy[j] = dya[j] + dyc[j];
+        const double dt = dta + dtc;
+        // ---- combined direction, step to the boundary
+        const double dzt = (kt - t * zt - zt * dt) * rcp(t);
+        double rmax = fmax(-dt * rcp(t), -dzt * rcp_fast(zt));
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                const double td = rw.bg[d][k][0] * dy[2 * d] + rw.bg[d][k][1] * dy[2 * d + 1];
+                dsl[d][k] = td + dt + rl[d][k];
+                dsu[d][k] = -td + dt + ru[d][k];
+                dzl[d][k] = (kl[d][k] - sl[d][k] * zl[d][k] - zl[d][k] * dsl[d][k]) * il[d][k];
+                dzu[d][k] = (ku[d][k] - su[d][k] * zu[d][k] - zu[d][k] * dsu[d][k]) * iu[d][k];
+                rmax = fmax(rmax, fmax(-dsl[d][k] * il[d][k], -dsu[d][k] * iu[d][k]));
+                rmax = fmax(rmax, fmax(-dzl[d][k] * rcp_fast(zl[d][k]), -dzu[d][k] * rcp_fast(zu[d][k])));
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            double td = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) td = fma(rw.cg[c][j], dy[j], td);
+            cds[c] = -td + dt + cr[c];
+            cdz[c] = (kc[c] - cs[c] * cz[c] - cz[c] * cds[c]) * ci[c];
+            rmax = fmax(rmax, fmax(-cds[c] * ci[c], -cdz[c] * rcp_fast(cz[c])));
+        }
+        rmax = grp_max<G>(rmax);
+        const double alpha = 0.99 * rcp(fmax(0.99, rmax));
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) y[j] = fma(alpha, dy[j], y[j]);
+        t = fmax(fma(alpha, dt, t), 1e-300);
+        zt = fmax(fma(alpha, dzt, zt), 1e-300);
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) {
+                sl[d][k] = fmax(fma(alpha, dsl[d][k], sl[d][k]), 1e-300);
+                su[d][k] = fmax(fma(alpha, dsu[d][k], su[d][k]), 1e-300);
+                zl[d][k] = fmax(fma(alpha, dzl[d][k], zl[d][k]), 1e-300);
+                zu[d][k] = fmax(fma(alpha, dzu[d][k], zu[d][k]), 1e-300);
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            cs[c] = fmax(fma(alpha, cds[c], cs[c]), 1e-300);
+            cz[c] = fmax(fma(alpha, cdz[c], cz[c]), 1e-300);
+        }
+    }
+    if (iters_out) *iters_out = it;
+    // t* from the iterate: the largest actual row violation at y (>= 0)
+    double worst = 0.0;
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+        for (int k = 0; k < SB; k++) {
+            const double ty = rw.bg[d][k][0] * y[2 * d] + rw.bg[d][k][1] * y[2 * d + 1];
+            worst = fmax(worst, fmax(rw.blo[d][k] - ty, ty - rw.bhi[d][k]));
+        }
+#pragma unroll
+    for (int c = 0; c < CB; c++) {
+        double tc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) tc = fma(rw.cg[c][j], y[j], tc);
+        worst = fmax(worst, tc - rw.chi[c]);
+    }
+    return grp_max<G>(worst);
 }
 
 }  // namespace dev

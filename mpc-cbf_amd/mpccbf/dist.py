@@ -66,6 +66,7 @@ class SwarmShard:
             dist.all_gather_into_tensor(self._full, self.local, group=self.group)
 
     def step(self, solve) -> None:
-        """One control step: next_out <- solve(full, first, count), then publish()."""
-        self.next_out.copy_(solve(self.full, self.first, self.count))
+        """One control step: solve(full, first, count, out=next_out) writes this rank's next
+        states into next_out (no copy), then publish()."""
+        solve(self.full, self.first, self.count, out=self.next_out)
         self.publish()

@@ -1,0 +1,126 @@
+"""GPU status parity on closed-loop-evolved swarms of the bench workload (BASELINE config 3:
+4096 agents, K = 15, 8 nearest within 3 d_min, the example's trajectory fallback and state noise),
+and on captured regression cases.
+
+The QPs the bench counts are the ones these states produce: from step ~14 on, agents that came
+within d_min of a neighbour get INFEASIBLE QPs (ConnectivityIMPCCBF.cpp:199-211 then breaks out of
+the IMPC loop), and iteration-1 QPs with two active neighbours need the phase-1 certificate. Every
+agent whose status is not OPTIMAL, plus a seeded sample of 256 OPTIMAL ones, is re-solved by the
+oracle on the same states and must agree: statuses equal, objectives within 1e-4.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from mpccbf import swarm
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OBJ_TOL = 1e-4
+X_TOL = 1e-5
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a visible MI355X")
+    return torch
+
+
+def _check_agents(cfg, states, targets, agents, g_status, g_obj, g_x=None):
+    p = O.make_params(cfg)
+    refs = swarm.refs_from_targets(targets, cfg["k_hor"])
+    rp, col = swarm.knn_csr(states, 8, 3.0 * cfg["d_min"])
+    for a in agents:
+        r = O.impc_optimize(p, states, a, col[rp[a]:rp[a + 1]], refs[a])
+        assert list(g_status[a]) == list(r["status"]), (a, g_status[a], r["status"])
+        for it in range(cfg["impc_iter"]):
+            if r["status"][it] == O.OPTIMAL:
+                ro = r["obj"][it]
+                assert abs(g_obj[a, it] - ro) <= OBJ_TOL * max(1.0, abs(ro)), (a, it, g_obj[a, it], ro)
+        if g_x is not None:
+            last = [it for it in range(cfg["impc_iter"]) if r["status"][it] == O.OPTIMAL]
+            if last:
+                xr = r["x"][last[-1]][:g_x.shape[1]]
+                assert np.max(np.abs(g_x[a] - xr)) <= X_TOL, (a, np.max(np.abs(g_x[a] - xr)))
+
+
+def test_regression_cases_match_oracle(mpclib):
+    """Captured instances that once failed (tests/golden/regress_cases.json): agent 0 against its
+    listed neighbours, the GPU's statuses / objectives / control points against the oracle."""
+    torch = _torch()
+    cases = json.load(open(os.path.join(HERE, "golden", "regress_cases.json")))["cases"]
+    dev = torch.device("cuda", 0)
+    for case in cases:
+        cfg = swarm.config(case["k_hor"])
+        states = np.array(case["states"])
+        n = len(states)
+        targets = np.tile(np.array(case["target"]), (n, 1))
+        rp = np.array([0, n - 1] + [n - 1] * (n - 1), np.int32)
+        col = np.arange(1, n, dtype=np.int32)
+        ctx = mpclib.Context(cfg)
+        out = ctx.alloc_outputs(1)
+        ctx.impc_solve(torch.tensor(states, device=dev), torch.tensor(rp, device=dev),
+                       torch.tensor(col, device=dev), targets=torch.tensor(targets[:1], device=dev),
+                       num_agents=1, **out)
+        torch.cuda.synchronize()
+        g = {k: v.cpu().numpy() for k, v in out.items()}
+        _check_agents(cfg, states, targets, [0], g["status"], g["obj"], g["x"])
+
+
+@pytest.mark.parametrize("snaps", [(16, 20, 27)])
+def test_bench_workload_statuses_match_oracle(mpclib, snaps):
+    torch = _torch()
+    cfg = swarm.config(15)
+    n = 4096
+    states_h, targets_h = swarm.lattice_swarm(n)
+    dev = torch.device("cuda", 0)
+    ctx = mpclib.Context(cfg)
+    tg = torch.tensor(targets_h, device=dev)
+    out = ctx.alloc_outputs(n)
+    traj_t = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+    steps = max(snaps) + 3
+    status_log = torch.empty((steps, n, 2), dtype=torch.int32, device=dev)
+    iters_log = torch.empty((steps, n, 2), dtype=torch.int32, device=dev)
+    cur = torch.tensor(states_h, device=dev)
+    alt = torch.empty_like(cur)
+    common = dict(targets=tg, knn_k=8, knn_radius=3.0 * cfg["d_min"], x=out["x"], obj=out["obj"],
+                  traj_t=traj_t, pos_std=0.001, vel_std=0.01, noise_seed=20251015)
+    s = 0
+    saved = {}
+
+    def advance(k):
+        nonlocal s, cur, alt
+        r = ctx.run_steps(cur, alt, k, status_log=status_log[s:s + k], iters_log=iters_log[s:s + k],
+                          step_index=s, **common)
+        if r["final"] is not cur:
+            cur, alt = alt, cur
+        s += k
+
+    for b in list(snaps) + [steps]:
+        if b > s:
+            advance(b - s)
+        if b < steps:
+            st_in = cur.cpu().numpy().copy()
+            advance(1)
+            saved[b] = (st_in, out["obj"].cpu().numpy().copy())
+    torch.cuda.synchronize()
+    slog = status_log.cpu().numpy()
+    ilog = iters_log.cpu().numpy()
+    attempted = ~((slog == 5) & (ilog == 0))
+    # no capacity errors and no undecided QPs anywhere in the run
+    assert not np.any((slog == 4) & attempted), "ERROR status in the bench workload"
+    assert not np.any((slog == 5) & attempted), np.argwhere((slog == 5) & attempted)[:5]
+    rng = np.random.default_rng(1234)
+    for b in snaps:
+        st_in, obj = saved[b]
+        stat = slog[b]
+        nonopt = np.nonzero(np.any(stat != 0, axis=1))[0]
+        opt = np.nonzero(np.all(stat == 0, axis=1))[0]
+        sample = rng.choice(opt, size=min(256, len(opt)), replace=False)
+        assert len(nonopt) > 0 or b < 14, f"step {b}: expected infeasible agents in the transient"
+        _check_agents(cfg, st_in, targets_h, np.concatenate([nonopt, sample]), stat, obj)

@@ -26,7 +26,7 @@ def _oracle_solver(cfg, targets):
     p = O.make_params(cfg)
     refs = swarm.refs_from_targets(targets, cfg["k_hor"])
 
-    def solve(full, first, count):
+    def solve(full, first, count, out):
         S = full.numpy().copy()
         rp, col = swarm.knn_csr(S, 8, 3 * cfg["d_min"])
         r = O.impc_batch(p, S, refs, rp, col, first, count, 1)
@@ -35,7 +35,7 @@ def _oracle_solver(cfg, targets):
             if np.any(r["status"][i] == O.OPTIMAL):  # closed-loop update: kept curve at t = h
                 nxt[i, :3] = O.eval_curve(p, r["x_last"][i], cfg["h"], 0)
                 nxt[i, 3:] = O.eval_curve(p, r["x_last"][i], cfg["h"], 1)
-        return torch.tensor(nxt)
+        out.copy_(torch.tensor(nxt))
 
     return solve
 

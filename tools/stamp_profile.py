@@ -43,13 +43,15 @@ for _ in range(WARM):
 torch.cuda.synchronize()
 snap = st.clone()
 PDIP = os.environ.get("MPCCBF_LIB", "").find("prof") >= 0  # profiling build: in-loop stamps
+TRACE = os.environ.get("MPCCBF_LIB", "").find("trace") >= 0  # trace build: per-step traces
 PPH_FOV = ["rows+LDS", "gram (MFMA)", "reduce+Py+rd", "cholesky", "pred solve", "pred rows+red",
            "corr G^T v", "corr solve", "step rows+red", "update y", "tail"]
 PPH = ["rows+acc", "reduce acc", "rp/py/conv", "cholesky", "pred solve", "pred steps+min",
        "mua", "corr rows+vc", "corr solve", "corr steps+min", "update"]
 for v in VARIANTS:
     ctx.set_variant(v)
-    stamps = torch.zeros(N * 8 + (N * 16 if PDIP else 0), dtype=torch.int64, device=dev)
+    stamps = torch.zeros(N * 8 + (N * 16 if PDIP else 0) + (N * 2 * 256 if TRACE else 0), dtype=torch.int64,
+                         device=dev)
     for rep in range(3):  # last rep measured (warm caches)
         ctx.impc_solve(snap, targets=tg, knn_k=8, knn_radius=radius, stamps=stamps, cov=COV, **out)
     torch.cuda.synchronize()
@@ -88,6 +90,10 @@ for v in VARIANTS:
     print(f"   critical agent {crit}: status {status[crit]}, start {start[crit]:.1f}, "
           f"phases {np.round(np.diff(s[crit]), 2)}")
     print(f"   critical agent iters {its[crit]}")
+    w0 = (crit // 4) * 4
+    for a in range(w0, w0 + 4):  # the critical wave (4 agents of 16 lanes)
+        sp = [(int(v) % 100, int(v) // 100 % 100, int(v) // 10000) for v in its[a]] if TRACE else its[a]
+        print(f"      wave agent {a}: status {status[a]} iters (warm, cold, phase1) {sp}")
     # how many agents end late, and the latest end per iteration-0 status
     print(f"   agents ending after 0.8*span: {(end > 0.8 * end.max()).sum()}")
     for stv in np.unique(status[:, 0]):
