@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 8
+#define MPCCBF_ABI_VERSION 9
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -95,9 +95,13 @@ typedef struct mpccbf_options {
     int32_t no_cbf_filter;     /* 1: keep every CBF row (no exact in-kernel redundancy filter) */
     int32_t max_pdip_iters;    /* default 60 */
     double tolerance;          /* PDIP relative tolerance, default 1e-9 */
-    /* IMPC iteration 1 starts from iteration 0's primal-dual point (same box rows and cost) with
-     * a cold retry if that start does not converge; env MPCCBF_WARM_DELTA (read here, default
-     * 0.3, 0 = cold) sets its slack / dual floor. Statuses and optima do not depend on it. */
+    /* IMPC iteration 1 starts from iteration 0's primal-dual point (same box rows and cost),
+     * slacks and duals floored at warm_delta: 0 = default (0.3), < 0 = cold start. A warm start
+     * that does not converge is certified by phase 1 and, when the QP is feasible, re-solved
+     * cold, so statuses do not depend on it; optima agree within the solver tolerance (a warm
+     * start may converge where a cold one would not). Environment variable MPCCBF_WARM_DELTA
+     * (read here, a number) overrides it for tuning. */
+    double warm_delta;
 } mpccbf_options;
 
 /* Validates p like parsing.hpp:37-135,182-214, builds the parameter-only operators on the host
@@ -127,12 +131,23 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *               launch sequence (spatial hash of `states` + in-kernel 3x3-cell query; in
  *               mpccbf_run_steps the IMPC kernel itself fills the next step's hash table);
  *               at most 64 agents within the radius (more: that agent's QP reports ERROR)
+ *               Capacity: the default separable kernel keeps up to 16 live (unfiltered) CBF rows
+ *               per IMPC iteration and agent (slack mode: 16 neighbours); an agent beyond it is
+ *               re-solved in the same call by the 64-lane dense instantiation (up to 256 rows)
  * Outputs (device, any may be NULL):
  *   x           num_agents x n: control points of the last OPTIMAL iteration (the curve the
  *               driver keeps, example :160-164); NaN if no iteration was OPTIMAL
  *   status      num_agents x impc_iter SolveStatus per IMPC iteration (UNKNOWN = not attempted)
  *   obj         num_agents x impc_iter optimal objective x^T H x + c^T x (CPLEX.cpp:144-146)
- *   iters       num_agents x impc_iter interior-point iterations
+ *   iters       num_agents x impc_iter interior-point Newton steps of all attempts of that QP
+ *               (a first attempt that started warm or stopped at the divergence test, plus its
+ *               cold retry; 0 when the unconstrained minimiser satisfies every row; phase-1 steps
+ *               not included)
+ *   primal_res, dual_res  num_agents x impc_iter: OPTIMAL — scaled primal residual
+ *               max_i |r_i| / (1 + |bound_i|) over the condensed QP's rows (bounds every row's
+ *               violation) and relative dual residual ||P y + q + G^T z||_inf / (1 + ||q||_inf)
+ *               of the returned point; INFEASIBLE certified by phase 1 — the minimal uniform row
+ *               violation t* (absolute, > 1e-6) and NaN; otherwise NaN
  *   next_states num_agents x 6: position/velocity of the kept curve at t = h (Jacobi update of
  *               the closed-loop driver, example :188-207, without noise); unchanged input if no
  *               curve was found.
@@ -174,6 +189,8 @@ typedef struct mpccbf_batch {
      * distanceToEllipse for the slack weights. NULL = unknown (infinite: every distance is -5,
      * weights follow the neighbour list order). Ignored otherwise. */
     const double* cov;
+    double* primal_res;       /* out, num_agents x impc_iter, or NULL (see above) */
+    double* dual_res;
 } mpccbf_batch;
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);

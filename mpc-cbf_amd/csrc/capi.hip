@@ -5,6 +5,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -23,6 +24,8 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
                        hipStream_t s);
 const char* impc_kernel_name(const DevOps& op, int variant);
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
+hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
+bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k);
 int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
                      double radius, int32_t* row_ptr, int32_t* col, void* scratch,
                      size_t scratch_bytes, hipStream_t s);
@@ -62,6 +65,8 @@ struct mpccbf_ctx {
     size_t scratch_bytes = 0;
     void* grid_scratch = nullptr;  // three neighbour tables (see GridArgs)
     size_t grid_bytes = 0;
+    int32_t* defer = nullptr;      // capacity-fallback queue [count, blocks done, agents...] (zeroed)
+    int defer_cap = 0;
     int variant = 0;
 };
 
@@ -161,9 +166,29 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.noise_seed = b->noise_seed;
     a.step_index = b->step_index;
     a.cov = b->cov;
+    a.primal_res = b->primal_res;
+    a.dual_res = b->dual_res;
+    // capacity fallback: agents beyond the separable kernel's 16 CBF row slots are deferred to a
+    // second launch of the same solver with 128 slots (only when the slots can be exceeded)
+    const bool fb = c->dev.cbf_mode != 1 && impc_may_defer(c->dev, c->variant, !grid, b->knn_k);
+    if (fb && c->defer_cap < b->num_agents) {
+        if (c->defer) (void)hipFree(c->defer);
+        c->defer = nullptr;
+        c->defer_cap = 0;
+        HIP_TRY(hipMalloc(&c->defer, (size_t)(b->num_agents + 2) * sizeof(int32_t)));
+        HIP_TRY(hipMemsetAsync(c->defer, 0, (size_t)(b->num_agents + 2) * sizeof(int32_t), stream));
+        c->defer_cap = b->num_agents;
+    }
+    a.defer = fb ? c->defer : nullptr;
     if (ev0) HIP_TRY(hipEventRecord(ev0, stream));
     hipError_t e = c->dev.cbf_mode == 1 ? launch_impc_fov(c->dev, c->dbuf, a, stream)
                                         : launch_impc(c->dev, c->dbuf, a, c->variant, stream);
+    if (e == hipSuccess && fb) {
+        ImpcArgs f = a;
+        f.defer = nullptr;
+        f.queue = c->defer;
+        e = launch_impc_fallback(c->dev, c->dbuf, f, stream);
+    }
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, stream);
     if (e == hipErrorInvalidValue)
         return fail(MPCCBF_ERR_CAPACITY, "no kernel instantiation for this reduced dimension / row count");
@@ -326,9 +351,15 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     d.cbf_filter = c->opt.no_cbf_filter ? 0 : 1;
     d.maxit = c->opt.max_pdip_iters > 0 ? c->opt.max_pdip_iters : 60;
     d.tol = c->opt.tolerance > 0 ? c->opt.tolerance : 1e-9;
-    {
-        const char* w = getenv("MPCCBF_WARM_DELTA");  // tuning override of the IMPC warm start
-        d.warm_delta = w ? atof(w) : 0.3;
+    d.warm_delta = c->opt.warm_delta == 0.0 ? 0.3 : (c->opt.warm_delta > 0.0 ? c->opt.warm_delta : 0.0);
+    if (const char* w = getenv("MPCCBF_WARM_DELTA")) {  // tuning override of the IMPC warm start
+        char* end = nullptr;
+        const double v = std::strtod(w, &end);
+        if (end == w || *end != '\0' || !std::isfinite(v)) {
+            delete c;
+            return fail(MPCCBF_ERR_INVALID_ARGUMENT, std::string("MPCCBF_WARM_DELTA is not a number: ") + w);
+        }
+        d.warm_delta = v > 0.0 ? v : 0.0;
     }
     d.feas_tol = 1e-6;  // CPLEX default feasibility tolerance
     d.early_it = 10;
@@ -359,6 +390,7 @@ void mpccbf_destroy(mpccbf_ctx* c) {
     if (c->dbuf) (void)hipFree(c->dbuf);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->grid_scratch) (void)hipFree(c->grid_scratch);
+    if (c->defer) (void)hipFree(c->defer);
     delete c;
 }
 

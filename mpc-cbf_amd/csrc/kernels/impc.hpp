@@ -120,6 +120,15 @@ struct ImpcArgs {
     // FoV slack weights: num_states x 3 position covariances (cxx, cxy, cyy) of the neighbour
     // estimates, or nullptr (unknown)
     const double* cov;
+    // per-iteration residuals of the returned solution (PdipOut::rp / rd; INFEASIBLE: phase 1's
+    // minimal violation t* and NaN), num_agents x impc_iter, or nullptr
+    double* primal_res;
+    double* dual_res;
+    // capacity fallback (impc_sep_kernel): the main launch appends agents beyond its row capacity
+    // to defer ([count, blocks done, agent...], device) and leaves their outputs to the fallback
+    // launch, which solves exactly the agents in queue (the same buffer) with a wider instantiation
+    int32_t* defer;
+    int32_t* queue;
 };
 
 constexpr int NSTAMP = 8;

@@ -463,11 +463,14 @@ __device__ __forceinline__ void stamp(const ImpcArgs& args, int ai, int gl, int 
 }
 
 __device__ __forceinline__ void write_iteration(const ImpcArgs& args, size_t oi, int gl, int st,
-                                                double obj, int iters) {
+                                                double obj, int iters,
+                                                double prs = __builtin_nan(""), double drs = __builtin_nan("")) {
     if (gl == 0) {
         if (args.status) args.status[oi] = st;
         if (args.obj) args.obj[oi] = obj;
         if (args.iters) args.iters[oi] = iters;
+        if (args.primal_res) args.primal_res[oi] = prs;
+        if (args.dual_res) args.dual_res[oi] = drs;
     }
 }
 

@@ -270,6 +270,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         if (it < 2) stamp(args, ai, lane, 3 + 2 * it);
         int st;
         int nit = 0;
+        double prs = __builtin_nan(""), drs = __builtin_nan("");
         double vobj = 0.0;  // slack mode: sum_i w_i v_i (addSlackCost, MPCCBFQPGeneratorBase.cpp:121-130)
         if (mtot > WROWS || nb_overflow || (SLACK && 4 * nchunk + WSL_CROWS > WROWS)) {
             st = ST_ERROR;  // capacity (rows per agent / observed neighbours)
@@ -320,11 +321,16 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                                                       opp(buf, op.o_LP16), cfg, lane, dbg, &sk, &vobj);
             st = po.status;
             nit = po.iters;
+            prs = po.rp;
+            drs = po.rd;
             // slack mode: the slack rows are always satisfiable, phase 1 certifies the box and
             // Voronoi rows (the ordinary image)
             if (st != ST_OPTIMAL) {
                 const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);
-                if (tstar > op.feas_tol) st = ST_INFEASIBLE;
+                if (tstar > op.feas_tol) {
+                    st = ST_INFEASIBLE;
+                    prs = tstar;
+                }
             }
         }
         double objv = __builtin_nan("");
@@ -342,7 +348,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         } else {
             success = false;
         }
-        write_iteration(args, oi, lane, st, objv, nit);
+        write_iteration(args, oi, lane, st, objv, nit, prs, drs);
         if (it < 2) stamp(args, ai, lane, 4 + 2 * it);
         wave_lds_sync();
     }

@@ -133,8 +133,9 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
         }
         int st;
         int nit = 0;
+        double prs = __builtin_nan(""), drs = __builtin_nan("");
         if (count > cap || nb_overflow) {
-            st = ST_ERROR;  // capacity: caller re-runs with a wider instantiation
+            st = ST_ERROR;  // capacity (the 64-lane instantiation takes up to 256 rows)
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
         } else {
@@ -142,10 +143,15 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
                 pdip_solve<NZ, G, R>(rw, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y, cfg);
             st = po.status;
             nit = po.iters;
+            prs = po.rp;
+            drs = po.rd;
             if (st != ST_OPTIMAL) {
                 // certify: minimal uniform row violation above the feasibility tolerance
                 const double tstar = pdip_phase1<NZ, G, R>(rw, cfg);
-                if (tstar > op.feas_tol) st = ST_INFEASIBLE;
+                if (tstar > op.feas_tol) {
+                    st = ST_INFEASIBLE;
+                    prs = tstar;
+                }
             }
         }
         double objv = __builtin_nan("");
@@ -157,7 +163,7 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
         } else {
             success = false;
         }
-        write_iteration(args, oi, gl, st, objv, nit);
+        write_iteration(args, oi, gl, st, objv, nit, prs, drs);
         if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
         wave_lds_sync();  // staging is rewritten by the next iteration
     }
@@ -238,23 +244,23 @@ __device__ double lane_slack_weight(const DevOps& op, const ImpcArgs& args, cons
     return gl < nnb ? op.slack_cost * pow(op.slack_decay, (double)rank) : 1.0;
 }
 
+// Hand agent ai to the fallback launch (lane 0 appends it to args.defer: [count, -, agents...]).
+__device__ __forceinline__ void defer_agent(const ImpcArgs& args, int ai, int gl) {
+    if (gl == 0) {
+        const int slot = atomicAdd(&args.defer[0], 1);
+        args.defer[2 + slot] = ai;
+    }
+}
+
+// One agent's IMPC step on the separable layout (the body of impc_sep_kernel). stage / red / nbs:
+// this group's LDS (CBF-row staging, Newton-sum all-reduce, neighbour query).
 template <int SB, int CB, bool SLACK>
-__global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
-                                                        const ImpcArgs args) {
+__device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
+                               const int ai, const int gl, double* stage, double* red, NbScratch& nbs) {
     constexpr int G = 16;
     constexpr int NZ = SEP_NZ;
-    constexpr int GPB = 256 / G;
     constexpr int cap = CB * G;  // CBF rows per agent
-    const int gl = threadIdx.x & (G - 1);
-    const int gib = threadIdx.x / G;
-    const int ai = blockIdx.x * GPB + gib;
-    grid_clear(args);
-    if (ai >= args.num_agents) return;
     stamp(args, ai, gl, 0);
-
-    __shared__ double stage_all[GPB][SLACK ? 1 : cap * (NZ + 1)];
-    double* stage = stage_all[gib];
-    __shared__ double red_all[GPB][16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
 
     const int self = args.agent_first + ai;
     double s0[6];
@@ -287,17 +293,20 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
 
     const bool grid_mode = args.nb_row_ptr == nullptr;
     int nb0 = 0, nnb = 0;
-    __shared__ NbScratch nb_scratch[GPB];
     if (!grid_mode) {
         nb0 = args.nb_row_ptr[ai];
         nnb = args.nb_row_ptr[ai + 1] - nb0;
     } else {
-        nnb = grid_neighbors<G>(args, self, s0[0], s0[1], nb_scratch[gib], gl);
+        nnb = grid_neighbors<G>(args, self, s0[0], s0[1], nbs, gl);
     }
-    const bool nb_overflow = nnb < 0 || (SLACK && nnb > G);  // slack mode: one lane per neighbour
+    if (SLACK && nnb > G && args.defer) {  // slack mode: one lane per neighbour
+        defer_agent(args, ai, gl);
+        return;
+    }
+    const bool nb_overflow = nnb < 0 || (SLACK && nnb > G);
     if (nb_overflow) nnb = 0;
     double wslack = 0.0, vslack = 0.0;
-    if constexpr (SLACK) wslack = lane_slack_weight<G>(op, args, s0, grid_mode, nb_scratch[gib].idx, nb0, nnb, gl);
+    if constexpr (SLACK) wslack = lane_slack_weight<G>(op, args, s0, grid_mode, nbs.idx, nb0, nnb, gl);
     stamp(args, ai, gl, 2);
 
     double y[NZ], ykeep[NZ];
@@ -319,9 +328,9 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
         bool live = false;
         if constexpr (SLACK) {
             // slack mode: rows stay in their neighbour's lane; a slack row is never infeasible
-            live = lane_cbf_rows<G, CB>(op, buf, args, it, s0, y, grid_mode, nb_scratch[gib].idx, nb0, nnb, gl, rw);
+            live = lane_cbf_rows<G, CB>(op, buf, args, it, s0, y, grid_mode, nbs.idx, nb0, nnb, gl, rw);
         } else {
-            count = stage_cbf_rows<NZ, G>(op, buf, args, it, s0, y, grid_mode, nb_scratch[gib].idx,
+            count = stage_cbf_rows<NZ, G>(op, buf, args, it, s0, y, grid_mode, nbs.idx,
                                           nb0, nnb, stage, cap, gl, &row_infeasible);
             live = count > 0;
 #pragma unroll
@@ -336,8 +345,13 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
             }
         }
         if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
+        if (count > cap && args.defer) {  // beyond this instantiation: the fallback launch solves it
+            defer_agent(args, ai, gl);
+            return;
+        }
         int st;
         int nit = 0;
+        double prs = __builtin_nan(""), drs = __builtin_nan("");
         if (count > cap || nb_overflow) {
             st = ST_ERROR;
         } else if (infeasible || row_infeasible) {
@@ -364,6 +378,7 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
             int tr_warm = 0, tr_cold = 0, tr_p1 = 0;  // diagnostics (MPCCBF_SOLVE_TRACE)
             int attempt = 0, total = 0;
             bool certified = false, infeas = false;
+            double tstar = 0.0;
             PdipOut po{ST_UNKNOWN, 0};
             for (;;) {
                 PdipCfg ca = cfg;
@@ -371,7 +386,7 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
                 ca.fast_start = op.fast_start != 0;
                 ca.robust = attempt == 2;
                 po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y,
-                                                      ca, dbg, wslack, &vslack, red_all[gib], &warm,
+                                                      ca, dbg, wslack, &vslack, red, &warm,
                                                       (attempt == 0 && warm_try) ? warm_delta : 0.0);
                 total += po.iters;
                 ((attempt == 0 && warm_try) ? tr_warm : tr_cold) += po.iters;
@@ -386,8 +401,7 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
                             rp1.chi[c] = 1.0;
                         }
                     }
-                    const double tstar =
-                        pdip_phase1_sep<G, SB, CB>(rp1, cfg, op.feas_tol, y, red_all[gib], &tr_p1, dbg);
+                    tstar = pdip_phase1_sep<G, SB, CB>(rp1, cfg, op.feas_tol, y, red, &tr_p1, dbg);
                     infeas = tstar > op.feas_tol && tstar < 1e300;  // 1e300: phase 1 failed
                     certified = true;
 #ifdef MPCCBF_DEBUG_EXIT
@@ -404,6 +418,8 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
             }
             st = po.status;
             nit = total;
+            prs = st == ST_INFEASIBLE ? tstar : po.rp;
+            drs = po.rd;
 #ifdef MPCCBF_SOLVE_TRACE  // diagnostics build: warm + 100 cold + 10000 phase-1 iterations
             nit = tr_warm + 100 * tr_cold + 10000 * tr_p1;
 #else
@@ -420,12 +436,45 @@ __global__ void __launch_bounds__(256) impc_sep_kernel(const DevOps op, const do
         } else {
             success = false;
         }
-        write_iteration(args, oi, gl, st, objv, nit);
+        write_iteration(args, oi, gl, st, objv, nit, prs, drs);
         if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
         wave_lds_sync();
     }
     write_agent_outputs<NZ, G>(op, buf, args, ai, gl, s0, ykeep, have_curve);
     stamp(args, ai, gl, 7);
+}
+
+// QUEUE = false: one agent per 16-lane group. QUEUE = true (capacity fallback): the agents the main
+// launch deferred (args.queue: [count, blocks done, agents...]), grid-stride; the last block to
+// finish empties the queue for the next step.
+template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false>
+__global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
+                                                       const ImpcArgs args) {
+    constexpr int GPB = BS / 16;
+    __shared__ double stage_all[GPB][SLACK ? 1 : CB * 16 * (SEP_NZ + 1)];
+    __shared__ double red_all[GPB][16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
+    __shared__ NbScratch nb_scratch[GPB];
+    const int gl = threadIdx.x & 15;
+    const int gib = threadIdx.x / 16;
+    if constexpr (!QUEUE) {
+        grid_clear(args);
+        const int ai = blockIdx.x * GPB + gib;
+        if (ai >= args.num_agents) return;
+        impc_sep_agent<SB, CB, SLACK>(op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib]);
+    } else {
+        const int n = args.queue[0];
+        for (int k = blockIdx.x * GPB + gib; k < n; k += gridDim.x * GPB)
+            impc_sep_agent<SB, CB, SLACK>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
+                                          nb_scratch[gib]);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(&args.queue[1], 1) == (int)gridDim.x - 1) {
+                args.queue[0] = 0;
+                args.queue[1] = 0;
+            }
+        }
+    }
 }
 
 }  // namespace dev
@@ -440,21 +489,38 @@ static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcA
     return hipGetLastError();
 }
 
-template <int SB, int CB, bool SLACK>
+template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false>
 static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                     hipStream_t s) {
-    constexpr int GPB = 256 / 16;
-    const int blocks = (a.num_agents + GPB - 1) / GPB;
-    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK>), dim3(blocks), dim3(256), 0, s, op, buf, a);
+    constexpr int GPB = BS / 16;
+    int blocks = (a.num_agents + GPB - 1) / GPB;
+    if (QUEUE) blocks = blocks < 64 ? blocks : 64;  // grid-stride over the deferred agents
+    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE>), dim3(blocks), dim3(BS), 0, s, op, buf, a);
     return hipGetLastError();
+}
+
+// Agents beyond the default separable kernel's capacity (more than 16 live CBF rows in an IMPC
+// iteration) are deferred to this launch: the same solver with 8 CBF row slots per lane (128
+// rows) in 64-thread blocks. Agents beyond that report ERROR.
+hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
+    if (a.num_agents <= 0 || !a.queue || op.slack_mode) return hipSuccess;
+    return launch_impc_sep_t<1, 8, false, 64, true>(op, buf, a, s);
+}
+
+// Whether launch_impc defers agents (so launch_impc_fallback must follow): the separable kernel,
+// when its 16 CBF row slots can be exceeded (caller lists, or k nearest x CBF samples > 16).
+bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k) {
+    if (op.slack_mode) return false;
+    if (!(variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)) return false;
+    return csr || knn_k * op.cbf_h > 16;
 }
 
 // Instantiation launch_impc picks for (operators, variant); nullptr if none fits.
 const char* impc_kernel_name(const DevOps& op, int variant) {
     if (op.slack_mode)  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2
         return (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
-                   ? "impc_sep_kernel<1,2,true>" : nullptr;
-    if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false>";
+                   ? "impc_sep_kernel<1,2,true,256>" : nullptr;
+    if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false,256>";
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
         if (variant == 1 && op.m < 64) return "impc_kernel<6,64,1>";

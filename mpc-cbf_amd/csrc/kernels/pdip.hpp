@@ -130,6 +130,11 @@ struct PdipOut {
     int status;
     int iters;
     bool early = false;  // stopped by the divergence test (phase 1 decides; pdip_solve_sep)
+    // OPTIMAL: scaled primal residual max_i |r_i| / (1 + |bound_i|) (bounds every row's violation)
+    // and relative dual residual ||P y + q + G^T z||_inf / (1 + ||q||_inf) of the returned
+    // iterate (mpccbf_batch.primal_res / dual_res); NaN otherwise
+    double rp = __builtin_nan("");
+    double rd = __builtin_nan("");
 };
 
 // step-to-boundary of s + a ds >= 0 (or z): returns the limiting a, or `big` if ds >= 0
@@ -264,6 +269,8 @@ __device__ PdipOut pdip_solve(const Rows<NZ, R>& rw, const double* __restrict__ 
                 rd_track = rdn * inv_qn;
                 if (rd_track <= cfg.tol) {
                     out.status = ST_OPTIMAL;
+                    out.rp = rp;
+                    out.rd = rd_track;
                     break;
                 }
             }

@@ -18,12 +18,6 @@
 
 #include "pdip.hpp"
 
-#ifndef MPCCBF_RELAX  // relaxed KKT acceptance at a factorisation breakdown / iteration limit
-#define MPCCBF_RELAX 0  // (off: the parity suite needs neither; costs ~2 us per launch)
-#endif
-#ifndef MPCCBF_SHIFT_RETRY  // re-factor with a diagonal shift after a breakdown (keeps the
-#define MPCCBF_SHIFT_RETRY 0  // accumulators live across the factorisation: ~10 % slower)
-#endif
 
 namespace mpccbf {
 namespace dev {
@@ -139,7 +133,19 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #pragma unroll
                     for (int k = 0; k < SB; k++) warm->zl[d][k] = warm->zu[d][k] = 0.0;
             }
-            return PdipOut{ST_OPTIMAL, 0};
+            // residuals of the returned point: rows satisfied exactly, multipliers zero
+            double rdn = 0.0, qn0 = 0.0;
+#pragma unroll
+            for (int d = 0; d < SEP_D; d++) {
+                const int o = 2 * d;
+                rdn = fmax(rdn, fabs(fma(P[o * 6 + o], yu[o], fma(P[o * 6 + o + 1], yu[o + 1], q[o]))));
+                rdn = fmax(rdn, fabs(fma(P[(o + 1) * 6 + o], yu[o], fma(P[(o + 1) * 6 + o + 1], yu[o + 1], q[o + 1]))));
+                qn0 = fmax(qn0, fmax(fabs(q[o]), fabs(q[o + 1])));
+            }
+            PdipOut fo{ST_OPTIMAL, 0};
+            fo.rp = 0.0;
+            fo.rd = rdn / (1.0 + qn0);
+            return fo;
         }
         if (!use_warm) {
 #pragma unroll
@@ -189,6 +195,12 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
     double mu0 = 1.0;
     double rd_track = 1e300;
     bool rd_exact = true;
+    // endgame (primal feasible, mu at target, dual residual not yet): the iterate with the
+    // smallest exact dual residual — lane j < 6 keeps its component j — in case the dual
+    // residual stalls (see below)
+    double ybest_l = 0.0, best_rd = 1e300, best_rp = 0.0;
+    int endgame = 0;
+    const int gl_s = threadIdx.x & (G - 1);
     for (int it = 0;; it++) {
         PSTAMP(0);
         double acc[A_N], accr[SEP_NZ];
@@ -393,33 +405,52 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             }
             return rdn * inv_qn;
         };
+        // At a degenerate optimum (active rows' D = z/s ~1e20) the Newton step's dz carries
+        // rounding of order eps D |ds|, so once mu is at its target the dual residual can stall
+        // above the tolerance (and grow if the iteration goes on). The endgame keeps the iterate
+        // with the smallest exact dual residual; after 3 endgame steps without convergence (or
+        // any other stop) it is accepted if that residual meets the dual tolerance of the parity
+        // rule / CPLEX (PdipCfg::rd_relax).
+        bool stop_best = false;
         if (finite && rp <= cfg.tol && mu <= cfg.tol * 0.1) {
-            // a degenerate optimum (active rows' D = z/s ~1e20) can stall the dual residual above
-            // the tolerance while mu keeps falling; three orders below the mu target it is
-            // accepted at the dual tolerance of the parity rule / CPLEX (PdipCfg::rd_relax)
-            const bool stalled = mu <= cfg.tol * 1e-4;
-            if (rd_track <= cfg.tol || stalled) {
-                rd_track = exact_rd();
-                if (rd_track <= cfg.tol || (stalled && rd_track <= cfg.rd_relax)) {
-                    out.status = ST_OPTIMAL;
-                    break;
-                }
+            rd_track = exact_rd();
+            if (rd_track <= cfg.tol) {
+                out.status = ST_OPTIMAL;
+                out.rp = rp;
+                out.rd = rd_track;
+                break;
             }
+            if (rd_track < best_rd) {
+                best_rd = rd_track;
+                best_rp = rp;
+                double yl = y[0];
+#pragma unroll
+                for (int j = 1; j < SEP_NZ; j++) yl = gl_s == j ? y[j] : yl;
+                ybest_l = yl;
+            }
+            stop_best = ++endgame >= 3;
         }
         if (it == 0) mu0 = mu;
+        auto take_best = [&]() {  // the endgame's best iterate, if it meets the relaxed tolerance
+            if (slk || !(best_rd <= cfg.rd_relax)) return false;  // slack mode: v is not kept
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) y[j] = __shfl(ybest_l, j, G);
+            out.status = ST_OPTIMAL;
+            out.rp = best_rp;
+            out.rd = best_rd;
+            return true;
+        };
+        if (stop_best) {
+            if (!take_best()) out.status = ST_UNKNOWN;
+            break;
+        }
         if (cfg.early_it > 0 && it >= cfg.early_it && mu > cfg.early_mu * mu0) {
             out.status = ST_UNKNOWN;  // diverging: phase 1 decides (see PdipCfg::early_it)
             out.early = true;
             break;
         }
         if (it >= cfg.maxit || !finite || mu > 1e8 * fmax(mu0, 1.0)) {
-            // out of iterations at a degenerate point the normal matrix can no longer resolve:
-            // the same relaxed KKT acceptance as at a factorisation breakdown (below)
-            if (MPCCBF_RELAX && finite && it >= cfg.maxit && rp <= 1e3 * cfg.tol && mu <= 1e2 * cfg.tol &&
-                exact_rd() <= 1e3 * cfg.tol) {
-                out.status = ST_OPTIMAL;
-                break;
-            }
+            if (take_best()) break;
             out.status = ST_UNKNOWN;
 #ifdef MPCCBF_DEBUG_EXIT  // diagnostics build: exit reason in the iteration count
             out.iters = it + 1000 * (it >= cfg.maxit ? 1 : !finite ? 2 : 3);
@@ -453,25 +484,11 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         form(tau0);
         bool ok4 = chol_packed<4>(Mxy, dxy);
         bool ok2 = chol_packed<2>(Mw, dw);
-        if (MPCCBF_SHIFT_RETRY && !(ok4 && ok2)) {
-            // a pivot lost to cancellation (active rows' D = z/s ~1e20 against P ~1e5): retry
-            // with a diagonal shift of 1e-12 of the largest diagonal entry (inexact Newton;
-            // residuals and the convergence test stay exact)
-            const double dmax = fmax(fmax(fmax(acc[A_MX + 0] + P[0], acc[A_MX + 2] + P[7]),
-                                          fmax(acc[A_MY + 0] + P[14], acc[A_MY + 2] + P[21])),
-                                     fmax(acc[A_MW + 0] + P[28], acc[A_MW + 2] + P[35]));
-            form(1e-12 * dmax);
-            ok4 = chol_packed<4>(Mxy, dxy);
-            ok2 = chol_packed<2>(Mw, dw);
-        }
         if (!(ok4 && ok2)) {
-            // Breakdown at a degenerate near-optimal point (D = z/s of the active rows ~1e20
-            // swamps P in the normal matrix): keep the iterate if it meets the KKT conditions to
-            // a relaxed tolerance, as the oracle keeps its best iterate (oracle.cpp pdip).
-            if (MPCCBF_RELAX && finite && rp <= 1e3 * cfg.tol && mu <= 1e2 * cfg.tol && exact_rd() <= 1e3 * cfg.tol) {
-                out.status = ST_OPTIMAL;
-                break;
-            }
+            // breakdown at a degenerate near-optimal point (D = z/s of the active rows ~1e20
+            // swamps P in the normal matrix): the endgame's best iterate, as the oracle keeps
+            // its best iterate (oracle.cpp pdip); else the caller certifies and retries
+            if (take_best()) break;
             out.status = ST_UNKNOWN;
 #ifdef MPCCBF_DEBUG_EXIT
             out.iters = it + 4000;

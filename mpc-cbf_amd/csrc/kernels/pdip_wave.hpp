@@ -523,6 +523,8 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
             // below MPCCBF_SLK_RD is accepted
             if (rd_track <= cfg.tol || (SLK && rd_track <= MPCCBF_SLK_RD)) {
                 out.status = ST_OPTIMAL;
+                out.rp = rp;
+                out.rd = rd_track;
                 break;
             }
         }

@@ -64,7 +64,7 @@ class Params(C.Structure):
 class Options(C.Structure):
     _fields_ = [("device", C.c_int32), ("keep_redundant", C.c_int32),
                 ("no_cbf_filter", C.c_int32), ("max_pdip_iters", C.c_int32),
-                ("tolerance", C.c_double)]
+                ("tolerance", C.c_double), ("warm_delta", C.c_double)]
 
 
 class Batch(C.Structure):
@@ -76,7 +76,7 @@ class Batch(C.Structure):
         ("next_states", C.c_void_p), ("knn_k", C.c_int32), ("knn_radius", C.c_double),
         ("stamps", C.c_void_p), ("traj_t", C.c_void_p), ("pos_std", C.c_double),
         ("vel_std", C.c_double), ("noise_seed", C.c_uint64), ("step_index", C.c_int64),
-        ("cov", C.c_void_p),
+        ("cov", C.c_void_p), ("primal_res", C.c_void_p), ("dual_res", C.c_void_p),
     ]
 
 
@@ -173,12 +173,15 @@ class Context:
     """One controller configuration on one device (mpccbf_create / mpccbf_destroy)."""
 
     def __init__(self, cfg: dict, device: int = 0, keep_redundant: bool = False,
-                 no_cbf_filter: bool = False, max_iters: int = 0, tol: float = 0.0):
+                 no_cbf_filter: bool = False, max_iters: int = 0, tol: float = 0.0,
+                 warm_delta: float = 0.0):
+        """warm_delta: IMPC iteration-1 warm start floor (0 = default 0.3, < 0 = cold start)."""
         L = load()
         self.cfg = dict(cfg)
         self.params = Params.from_dict(cfg)
         o = Options(device=device, keep_redundant=int(keep_redundant),
-                    no_cbf_filter=int(no_cbf_filter), max_pdip_iters=max_iters, tolerance=tol)
+                    no_cbf_filter=int(no_cbf_filter), max_pdip_iters=max_iters, tolerance=tol,
+                    warm_delta=warm_delta)
         h = C.c_void_p()
         _check(L.mpccbf_create(C.byref(self.params), C.byref(o), C.byref(h)))
         self._h = h
@@ -215,7 +218,8 @@ class Context:
     def impc_solve(self, states, nb_row_ptr=None, nb_col=None, targets=None, refs=None,
                    agent_first=0, num_agents=None, x=None, status=None, obj=None, iters=None,
                    next_states=None, knn_k=0, knn_radius=0.0, stream=None, stamps=None,
-                   traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0, cov=None):
+                   traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0, cov=None,
+                   primal_res=None, dual_res=None):
         """CSR neighbours (nb_row_ptr/nb_col) or, with both None, the knn_k nearest within
         knn_radius found on the device in the same launch sequence. traj_t (float64, one per
         agent, initialised to -1) turns on the closed-loop simulator semantics: x persists the
@@ -229,7 +233,7 @@ class Context:
                   next_states=_ptr(next_states), knn_k=int(knn_k), knn_radius=float(knn_radius),
                   stamps=_ptr(stamps), traj_t=_ptr(traj_t), pos_std=float(pos_std),
                   vel_std=float(vel_std), noise_seed=int(noise_seed), step_index=int(step_index),
-                  cov=_ptr(cov))
+                  cov=_ptr(cov), primal_res=_ptr(primal_res), dual_res=_ptr(dual_res))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
 
     def run_steps(self, states, states_alt, num_steps, targets=None, refs=None, agent_first=0,
@@ -275,6 +279,8 @@ class Context:
             obj=torch.empty((num_agents, self.impc_iter), dtype=torch.float64, device=dev),
             iters=torch.empty((num_agents, self.impc_iter), dtype=torch.int32, device=dev),
             next_states=torch.empty((num_agents, 6), dtype=torch.float64, device=dev),
+            primal_res=torch.empty((num_agents, self.impc_iter), dtype=torch.float64, device=dev),
+            dual_res=torch.empty((num_agents, self.impc_iter), dtype=torch.float64, device=dev),
         )
 
 

@@ -335,7 +335,7 @@ def test_slack_mode_matches_oracle(mpclib, scale, k_hor):
     states[:, :2] *= scale
     rp, col = swarm.knn_csr(states, 8, 6.0)
     ctx = mpclib.Context(cfg)
-    assert ctx.kernel_name == "impc_sep_kernel<1,2,true>"
+    assert ctx.kernel_name == "impc_sep_kernel<1,2,true,256>"
     g = run_gpu(ctx, states, targets, rp, col, torch)
     agents = list(range(64))
     ref = run_oracle(cfg, states, targets, rp, col, agents)
@@ -527,25 +527,76 @@ def test_grid_bucket_overflow_falls_back_to_full_scan(mpclib):
             np.testing.assert_array_equal(states, ref)
 
 
-@pytest.mark.parametrize("scale", [0.55, 0.42])
-def test_iteration1_warm_start_matches_cold_start(mpclib, monkeypatch, scale):
+@pytest.mark.parametrize("scale", [0.55, 0.42, 0.3])
+def test_iteration1_warm_start_matches_cold_start(mpclib, scale):
     """IMPC iteration 1 warm-started from iteration 0's primal-dual point (the default,
-    MPCCBF_WARM_DELTA = 0.3) and cold-started (0) reach the same optima: statuses equal,
-    objectives within solver tolerance; the warm start saves Newton steps on iteration 1."""
+    mpccbf_options.warm_delta = 0 -> 0.3) and cold-started (warm_delta < 0) reach the same
+    optima: statuses equal (also on the very crowded 0.3 lattice, where breakdowns and infeasible
+    QPs occur), objectives within solver tolerance; the warm start saves Newton steps."""
     torch = _torch()
     cfg = swarm.config(15)
     states, targets = swarm.lattice_swarm(1024, seed=5)
     states[:, :2] *= scale
     rp, col = swarm.knn_csr(states, 8, 6.0)
-    res = {}
-    for delta in ("0", "0.3"):
-        monkeypatch.setenv("MPCCBF_WARM_DELTA", delta)  # read when the context is created
-        res[delta] = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
-    cold, warm = res["0"], res["0.3"]
+    cold = run_gpu(mpclib.Context(cfg, warm_delta=-1.0), states, targets, rp, col, torch)
+    warm = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
     np.testing.assert_array_equal(cold["status"], warm["status"])
     ok = cold["status"] == 0
-    assert ok[:, 1].sum() > 200
+    if scale < 0.4:  # very crowded: iteration 1 is never reached OPTIMAL; statuses are the check
+        return
+    assert ok[:, 1].sum() > 100
     err = np.abs(cold["obj"][ok] - warm["obj"][ok]) / np.maximum(1.0, np.abs(cold["obj"][ok]))
     assert err.max() <= 1e-7, err.max()
     assert np.nanmax(np.abs(cold["x"] - warm["x"])) <= 1e-5
-    assert warm["iters"][ok[:, 1], 1].mean() < cold["iters"][ok[:, 1], 1].mean()
+    hard = ok[:, 1] & (cold["iters"][:, 1] > 0)  # QPs the fast start does not settle
+    if scale > 0.4:
+        assert warm["iters"][hard, 1].mean() < cold["iters"][hard, 1].mean()
+
+
+def test_invalid_warm_delta_env_rejected(mpclib, monkeypatch):
+    monkeypatch.setenv("MPCCBF_WARM_DELTA", "0.3x")
+    with pytest.raises(mpclib.MpccbfError, match="MPCCBF_WARM_DELTA"):
+        mpclib.Context(swarm.config(15))
+
+
+@pytest.mark.parametrize("n_ring,radius,v0", [(20, 1.99, (0.2, 0.1)), (40, 1.98, (0.1, 0.3))])
+def test_capacity_fallback_many_live_rows(mpclib, n_ring, radius, v0):
+    """An agent with more live CBF rows than the default kernel's 16 slots: n_ring static
+    neighbours on a half circle just inside d_min, all passed as its neighbours (the reference
+    passes every other robot, ConnectivityIMPCCBF.cpp:59-67,135-141). The agent is deferred to the
+    128-row fallback launch in the same call: no ERROR, parity with the oracle. The ring robots
+    themselves (each other's neighbours, all N-1 semantics) are solved too."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    n = n_ring + 1
+    states = np.zeros((n, 6))
+    states[0, 3:5] = v0
+    ang = np.linspace(0.05, np.pi - 0.05, n_ring)
+    states[1:, 0] = radius * np.cos(ang)
+    states[1:, 1] = radius * np.sin(ang)
+    targets = np.zeros((n, 3))
+    targets[:, 1] = -2.0
+    targets[1:, :2] = states[1:, :2]
+    rp, col = swarm.all_csr(n)
+    live = _live_cbf_rows(cfg, states, rp, col)
+    assert live[0] > 16, live[0]
+    ctx = mpclib.Context(cfg)
+    g = run_gpu(ctx, states, targets, rp, col, torch)
+    assert not np.any(g["status"] == O.ERROR), np.argwhere(g["status"] == O.ERROR)[:5]
+    assert g["status"][0, 0] == O.OPTIMAL
+    agents = list(range(n))
+    ref = run_oracle(cfg, states, targets, rp, col, agents)
+    compare(cfg, g, ref, agents)
+
+
+def _live_cbf_rows(cfg, states, rp, col):
+    """Iteration-0 CBF rows per agent that the exact box filter keeps (b < max_u -a^T u)."""
+    amax = np.array(cfg["a_max"])
+    amin = np.array(cfg["a_min"])
+    out = np.zeros(len(states), dtype=int)
+    for i in range(len(states)):
+        for j in col[rp[i]:rp[i + 1]]:
+            a, b = O.safety_cbf(states[i], states[j], cfg["d_min"])
+            bmax = np.sum(np.maximum(-a * amin, -a * amax))
+            out[i] += int(b < bmax)
+    return out

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol(mpclib):
 
 def test_abi_version_and_status_strings(mpclib):
     L = mpclib.load()
-    assert L.mpccbf_abi_version() == 8
+    assert L.mpccbf_abi_version() == 9
     assert [L.mpccbf_status_string(i).decode() for i in range(7)] == mpclib.STATUS_NAMES
 
 
@@ -104,3 +104,36 @@ def test_row_removal_is_exact(mpclib, oracle, K):
     # constant rows: the k = 0 velocity rows (pinned by the initial-velocity equality)
     assert red["mc"] == 3
     assert np.abs(red["Cs"][:, 3:] - np.eye(3)).max() < 1e-12
+
+
+def test_ctypes_structs_match_the_c_header(tmp_path):
+    """The ctypes mirrors in mpccbf/_lib.py have the sizes and field offsets of include/mpccbf.h
+    (compiled here with gcc), so no field is shifted across the boundary."""
+    import ctypes
+    import subprocess
+    from mpccbf import _lib
+    structs = {"mpccbf_params": _lib.Params, "mpccbf_options": _lib.Options,
+               "mpccbf_batch": _lib.Batch, "mpccbf_run": _lib.Run, "mpccbf_dense_qp": _lib.DenseQP,
+               "mpccbf_host_ops": _lib.HostOps, "mpccbf_fov_control_params": _lib.FovControlParams,
+               "mpccbf_fov_control_batch": _lib.FovControlBatch,
+               "mpccbf_connectivity_control_params": _lib.ConnControlParams,
+               "mpccbf_connectivity_control_batch": _lib.ConnControlBatch}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mpccbf.h"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "sizes.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "sizes"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", "-std=c11", "-I", inc, str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    for ln in out:
+        if not ln:
+            continue
+        cname, f, v = ln.split()
+        py = structs[cname]
+        got = ctypes.sizeof(py) if f == "size" else getattr(py, f).offset
+        assert got == int(v), (cname, f, got, v)
