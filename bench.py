@@ -306,7 +306,7 @@ def main():
         # average launch time (HIP events on the launch stream, every step of the replay)
         flops_per_launch = flops_rank0 / nsteps
         achieved_tf = flops_per_launch / (kern_avg * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic(kname)
+        traffic, traffic_src = pmc_traffic(kname, ("fovs" if args.slack else "fov") if fov else "collision")
         abytes = algorithmic_bytes_per_agent(ctx.n, args.knn, cfg["impc_iter"], cov is not None) * per
         bound = "mfma" if kname.startswith("impc_fov") else "valu"
         res = {
@@ -387,22 +387,28 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kname: str):
-    """HBM bytes per launch of kernel `kname` from the newest committed PMC summary
-    (profiles/r*_pmc_summary.json: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
-    gfx950-corrected by tools/pmc_summary.py). The counters cannot be read from inside a timed
-    run, so the value comes from the separate counter pass of the same command; None if absent."""
+def pmc_traffic(kname: str, workload: str):
+    """HBM bytes per launch of kernel `kname` under `workload` ("collision", "fov", "fovs") from
+    the newest committed PMC summary (profiles/r*_pmc_summary.json: rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE passes of this bench, gfx950-corrected by tools/pmc_summary.py). The counters
+    cannot be read inside a timed run, so the value comes from the separate counter passes of
+    the same command; None if absent."""
     import glob
     key = kname.replace(" ", "")
+
+    def norm(n):
+        return n.replace(" ", "").replace("void", "").replace("mpccbf::dev::", "")
+
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        for name, v in d.items():
-            n = name.replace(" ", "").replace("void", "").replace("mpccbf::dev::", "")
-            if n == key and "hbm_bytes_per_launch_corrected" in v:
-                return float(v["hbm_bytes_per_launch_corrected"]), os.path.relpath(f, REPO)
+        tables = [d[workload]] if isinstance(d.get(workload), dict) else [d]
+        for t in tables:
+            for name, v in t.items():
+                if isinstance(v, dict) and norm(name) == key and "hbm_bytes_per_launch_corrected" in v:
+                    return float(v["hbm_bytes_per_launch_corrected"]), os.path.relpath(f, REPO)
     return None, None
 
 

@@ -1,30 +1,55 @@
 #!/bin/bash
-# Round measurement set, run from the repo root on the GPU box:
-#   bench lines (collision = headline config 3, FoV = config 5), rocprofv3 kernel-trace stats of
-#   the same commands, and the PMC traffic passes of the collision bench.
-# Usage: bash tools/profile_round.sh <tag>   (outputs under gpurun_out/<tag>_*)
+# Round measurement set, run from the repo root on the GPU box (outputs under gpurun_out/<tag>_*):
+#   bench lines — the driver's command (config 3, 20 steps), config 3 at 1000 steps (+ CPU
+#   baseline), config 4's 8192 agents on one GPU, config 5 (FoV) and its slack mode;
+#   rocprofv3 --kernel-trace --stats of the same commands; PMC passes (one counter group per run,
+#   never combined with traces): HBM bytes (FETCH_SIZE, WRITE_SIZE), SQ issue / wait counters,
+#   FP64 instruction mix, and the FoV kernels' FP64 MFMA counters.
+# Usage: bash tools/profile_round.sh <tag> [quick]
 set -e -o pipefail
 TAG=${1:-rNN}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 python3 $ROOT/bench.py > $OUT/${TAG}_bench_collision.json 2> $OUT/${TAG}_bench_collision.err
-timeout -k 10 300 python3 $ROOT/bench.py --workload fov > $OUT/${TAG}_bench_fov.json 2> $OUT/${TAG}_bench_fov.err
-timeout -k 10 300 python3 $ROOT/bench.py --workload fov --slack > $OUT/${TAG}_bench_fov_slack.json 2> $OUT/${TAG}_bench_fov_slack.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof_collision -o run \
-    -- python3 $ROOT/bench.py --no-cpu-baseline > $OUT/${TAG}_prof_collision.json 2> $OUT/${TAG}_prof_collision.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof_fov -o run \
-    -- python3 $ROOT/bench.py --workload fov --no-cpu-baseline > $OUT/${TAG}_prof_fov.json 2> $OUT/${TAG}_prof_fov.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof_fov_slack -o run \
-    -- python3 $ROOT/bench.py --workload fov --slack --no-cpu-baseline > $OUT/${TAG}_prof_fov_slack.json 2> $OUT/${TAG}_prof_fov_slack.err
-ARGS="$ROOT/bench.py --no-cpu-baseline --steps 20 --warmup 5"
-timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $ARGS > $OUT/pmc_fetch.log 2>&1
-timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $ARGS > $OUT/pmc_write.log 2>&1
-FARGS="$ROOT/bench.py --workload fov --no-cpu-baseline --steps 20 --warmup 5"
-timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fov_fetch -o run -- python3 $FARGS > $OUT/pmc_fov_fetch.log 2>&1
-timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_fov_write -o run -- python3 $FARGS > $OUT/pmc_fov_write.log 2>&1
-SARGS="$FARGS --slack"
-timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fovs_fetch -o run -- python3 $SARGS > $OUT/pmc_fovs_fetch.log 2>&1
-timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_fovs_write -o run -- python3 $SARGS > $OUT/pmc_fovs_write.log 2>&1
+B="python3 $ROOT/bench.py"
+step() { echo "[$(date +%T)] $*"; }
+step bench driver; timeout -k 10 200 $B --steps 20 --warmup 5 > $OUT/${TAG}_bench_driver.json 2> $OUT/${TAG}_bench_driver.err
+step bench 1000; timeout -k 10 300 $B > $OUT/${TAG}_bench_collision.json 2> $OUT/${TAG}_bench_collision.err
+step bench 8192; timeout -k 10 300 $B --agents-per-gpu 8192 --no-cpu-baseline > $OUT/${TAG}_bench_8192.json 2> $OUT/${TAG}_bench_8192.err
+step bench fov; timeout -k 10 300 $B --workload fov > $OUT/${TAG}_bench_fov.json 2> $OUT/${TAG}_bench_fov.err
+step bench fov slack; timeout -k 10 300 $B --workload fov --slack > $OUT/${TAG}_bench_fov_slack.json 2> $OUT/${TAG}_bench_fov_slack.err
+prof() {  # name, bench args
+  step prof $1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof_$1 -o run \
+    -- python3 $ROOT/bench.py --no-cpu-baseline ${@:2} > $OUT/${TAG}_prof_$1.json 2> $OUT/${TAG}_prof_$1.err
+}
+prof driver --steps 20 --warmup 5
+prof collision
+prof 8192 --agents-per-gpu 8192
+prof fov --workload fov
+prof fov_slack --workload fov --slack
+[ "$2" = "quick" ] && { echo done; exit 0; }
+pmc() {  # dir, bench args..., -- counters
+  local d=$1; shift
+  local args=()
+  while [ "$1" != "--" ]; do args+=("$1"); shift; done; shift
+  step pmc $d "$@"
+  timeout -s KILL 90 rocprofv3 --pmc "$@" --output-format csv -d $OUT/${TAG}_pmc/$d -o run \
+    -- python3 $ROOT/bench.py --no-cpu-baseline --steps 20 --warmup 5 "${args[@]}" > $OUT/${TAG}_pmc_$d.log 2>&1
+}
+SQA="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU"
+SQB="SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_LDS SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"
+SQM="SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES"
+pmc collision_fetch -- FETCH_SIZE
+pmc collision_write -- WRITE_SIZE
+pmc collision_sqa -- $SQA
+pmc collision_sqb -- $SQB
+pmc fov_fetch --workload fov -- FETCH_SIZE
+pmc fov_write --workload fov -- WRITE_SIZE
+pmc fov_sqa --workload fov -- $SQA
+pmc fov_mfma --workload fov -- $SQM
+pmc fovs_fetch --workload fov --slack -- FETCH_SIZE
+pmc fovs_write --workload fov --slack -- WRITE_SIZE
+pmc fovs_mfma --workload fov --slack -- $SQM
 echo done
