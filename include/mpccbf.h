@@ -180,7 +180,10 @@ typedef struct mpccbf_batch {
      * traj_t == NULL: next state = this step's curve at t = h, or the current state if none. */
     double* traj_t;
     double pos_std, vel_std;  /* Gaussian noise added to the next state's position / velocity
-                                 (math::addRandomNoise, Random.cpp:7-28); 0 = off */
+                                 (math::addRandomNoise, Random.cpp:7-28) at each of the int(h / Ts)
+                                 control sub-steps: with a curve only the last draw remains (each
+                                 sub-step re-evaluates the curve); holding position (no curve yet)
+                                 the position draws accumulate; 0 = off */
     uint64_t noise_seed;      /* counter-based: noise(seed, step_index, agent, component) */
     int64_t step_index;       /* mpccbf_run_steps adds the step number */
     /* FoV controller in slack mode (FovBezierIMPCCBF::optimize's other_robot_covs,
@@ -191,6 +194,12 @@ typedef struct mpccbf_batch {
     const double* cov;
     double* primal_res;       /* out, num_agents x impc_iter, or NULL (see above) */
     double* dual_res;
+    /* Closed-loop records (needs traj_t): device, num_agents x int(h / Ts) x 6, the state after
+     * each control sub-step of this step as the example appends them to states.json
+     * (MPCCBFFormationControl_example.cpp:188-221): the kept curve at traj_t + Ts k (clamped) plus
+     * noise, or, with no curve yet, the held position with the noise accumulated over the
+     * sub-steps and a zero velocity plus noise. The last record is the next state. NULL: none. */
+    double* substeps;
 } mpccbf_batch;
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);
@@ -214,6 +223,12 @@ int mpccbf_comm_unique_id(char id_out[MPCCBF_COMM_ID_BYTES]);  /* on one rank; s
 int mpccbf_comm_create(const char id[MPCCBF_COMM_ID_BYTES], int32_t nranks, int32_t rank,
                        int32_t device, mpccbf_comm** out);     /* collective over the nranks */
 void mpccbf_comm_destroy(mpccbf_comm* comm);
+/* In-process group of nranks communicators (comms_out[r] for rank r) on one device: the ranks are
+ * host threads of this process, each running mpccbf_run_steps on its own stream with its own
+ * context and state tables; the per-step all-gather becomes device copies between those tables
+ * (one event per rank and step, a host barrier per step). The multi-GPU data flow on one GPU —
+ * for testing and for running several shards on one device. */
+int mpccbf_comm_create_local(int32_t nranks, int32_t device, mpccbf_comm** comms_out);
 
 typedef struct mpccbf_run {
     int32_t num_steps;

@@ -5,6 +5,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -168,6 +171,9 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.cov = b->cov;
     a.primal_res = b->primal_res;
     a.dual_res = b->dual_res;
+    a.substeps = b->substeps;
+    if (b->substeps && !b->traj_t)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "substeps (closed-loop records) needs traj_t");
     // capacity fallback: agents beyond the separable kernel's 16 CBF row slots are deferred to a
     // second launch of the same solver with 128 slots (only when the slots can be exceeded)
     const bool fb = c->dev.cbf_mode != 1 && impc_may_defer(c->dev, c->variant, !grid, b->knn_k);
@@ -278,6 +284,8 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     pack(v, d.o_EB1, o.EB1);
     pack(v, d.o_cum, o.cum);
     d.eval_step = o.eval_step;
+    d.Ts = p->Ts;
+    d.nsub = (int)(p->h / p->Ts);
     // separable layout: box rows regrouped by channel, 16 per channel (lanes of a group)
     d.sep = 0;
     d.o_Gsep = 0;
@@ -444,9 +452,38 @@ int mpccbf_build_neighbors(mpccbf_ctx* c, const double* states, int32_t num_stat
 // ---------------------------------------------------------------------------------------------
 // Closed-loop stepping + RCCL exchange
 // ---------------------------------------------------------------------------------------------
+// In-process communicator group (mpccbf_comm_create_local): the ranks are host threads of one
+// process on one device; the per-step all-gather becomes device copies between their state
+// tables, ordered by one event per rank and step and a host barrier, so mpccbf_run_steps runs its
+// N-rank data flow (own block written by the IMPC kernel, exchange, the other blocks inserted
+// into the next neighbour table) on a single GPU.
+struct LocalGroup {
+    int nranks = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    long long gen = 0;
+    std::vector<double*> table[2];     // [step & 1][rank]: the table that rank wrote this step
+    std::vector<hipEvent_t> ev[2];     // [step & 1][rank]: that rank's IMPC kernel of the step done
+    // (double-buffered by step parity: a rank rewrites slot s & 1 only after the barrier of step
+    // s + 1, which every peer reaches after enqueueing its step-s copies)
+    void barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        const long long g = gen;
+        if (++arrived == nranks) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
 struct mpccbf_comm {
     ncclComm_t nccl = nullptr;
     int nranks = 1, rank = 0, device = 0;
+    std::shared_ptr<LocalGroup> local;  // set: in-process group (no RCCL)
 };
 
 extern "C" {
@@ -482,9 +519,32 @@ int mpccbf_comm_create(const char id[MPCCBF_COMM_ID_BYTES], int32_t nranks, int3
     return MPCCBF_OK;
 }
 
+int mpccbf_comm_create_local(int32_t nranks, int32_t device, mpccbf_comm** out) {
+    if (!out || nranks < 1) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "bad communicator arguments");
+    HIP_TRY(hipSetDevice(device));
+    auto g = std::make_shared<LocalGroup>();
+    g->nranks = nranks;
+    for (int p = 0; p < 2; p++) {
+        g->table[p].assign(nranks, nullptr);
+        g->ev[p].assign(nranks, nullptr);
+        for (int r = 0; r < nranks; r++) HIP_TRY(hipEventCreateWithFlags(&g->ev[p][r], hipEventDisableTiming));
+    }
+    for (int r = 0; r < nranks; r++) {
+        out[r] = new mpccbf_comm();
+        out[r]->nranks = nranks;
+        out[r]->rank = r;
+        out[r]->device = device;
+        out[r]->local = g;
+    }
+    return MPCCBF_OK;
+}
+
 void mpccbf_comm_destroy(mpccbf_comm* cm) {
     if (!cm) return;
     if (cm->nccl) (void)ncclCommDestroy(cm->nccl);
+    if (cm->local && cm->local.use_count() == 1)
+        for (int p = 0; p < 2; p++)
+            for (hipEvent_t e : cm->local->ev[p]) (void)hipEventDestroy(e);
     delete cm;
 }
 
@@ -544,7 +604,20 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
         const int rc = impc_enqueue(c, &sb, stream, tk ? ev[3 * s + 1] : nullptr, tk ? ev[3 * s + 2] : nullptr,
                                     gtab ? s : -1);
         if (rc != MPCCBF_OK) return rc;
-        if (r->comm && r->comm->nranks > 1) {
+        if (r->comm && r->comm->nranks > 1 && r->comm->local) {
+            // in-process group: every rank's block of this step copied into this rank's table
+            LocalGroup& g = *r->comm->local;
+            const int me = r->comm->rank;
+            g.table[s & 1][me] = nxt;
+            HIP_TRY(hipEventRecord(g.ev[s & 1][me], stream));
+            g.barrier();
+            for (int p = 0; p < g.nranks; p++) {
+                if (p == me) continue;
+                HIP_TRY(hipStreamWaitEvent(stream, g.ev[s & 1][p], 0));
+                HIP_TRY(hipMemcpyAsync(nxt + (size_t)p * count * 6, g.table[s & 1][p] + (size_t)p * count * 6,
+                                       (size_t)count * 6 * sizeof(double), hipMemcpyDeviceToDevice, stream));
+            }
+        } else if (r->comm && r->comm->nranks > 1) {
             const ncclResult_t nr = ncclAllGather(nxt + (size_t)first * 6, nxt, (size_t)count * 6, ncclDouble,
                                                   r->comm->nccl, stream);
             if (nr != ncclSuccess) return fail(MPCCBF_ERR_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(nr));

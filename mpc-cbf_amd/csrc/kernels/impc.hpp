@@ -33,6 +33,8 @@ struct DevOps {
     // value / first derivative, cum: P cumulative piece parameters)
     int32_t P, o_EB0, o_EB1, o_cum;
     double eval_step;
+    double Ts;        // control period: the driver integrates nsub = int(h / Ts) sub-steps per step
+    int32_t nsub;
     // slack mode: one slack variable per neighbour; collision controller: cost
     // slack_cost * slack_decay^rank (ConnectivityIMPCCBF.cpp:73-100); FoV controller: by
     // distanceToEllipse with the reference's idx[i] indexing (FovBezierIMPCCBF.cpp:58-81)
@@ -129,6 +131,9 @@ struct ImpcArgs {
     // launch, which solves exactly the agents in queue (the same buffer) with a wider instantiation
     int32_t* defer;
     int32_t* queue;
+    // closed-loop simulator: the state after every control sub-step (num_agents x nsub x 6), the
+    // records the example writes to states.json, or nullptr
+    double* substeps;
 };
 
 constexpr int NSTAMP = 8;

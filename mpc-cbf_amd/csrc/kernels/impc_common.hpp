@@ -335,10 +335,13 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ double normal_sample(uint64_t seed, int64_t step, int64_t agent, int comp) {
+// sub: control sub-step counted back from the last one (0 = the last draw of the step)
+__device__ __forceinline__ double normal_sample(uint64_t seed, int64_t step, int64_t agent, int comp,
+                                                int sub = 0) {
     uint64_t k = mix64(seed);
     k = mix64(k ^ (uint64_t)step);
     k = mix64(k ^ ((uint64_t)agent * 8u + (uint64_t)comp));
+    if (sub > 0) k = mix64(k ^ ((uint64_t)sub << 40));
     const double u1 = (double)((k >> 11) + 1) * 0x1.0p-53;  // (0, 1]
     const double u2 = (double)(mix64(k) >> 11) * 0x1.0p-53;
     return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
@@ -410,33 +413,56 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
     }
     if (gl >= 6) return;
     double v = 0.0;
+    const double sd = gl < 3 ? args.pos_std : args.vel_std;
+    const int64_t agent = args.agent_first + ai;
     if (sim) {
         const double t_prev = have_curve ? 0.0 : args.traj_t[ai];
         double t_new = t_prev;
+        const double tmax = opp(buf, op.o_cum)[op.P - 1];
         if (have_curve || t_prev >= 0.0) {
-            t_new = fmin(t_prev + op.eval_step, opp(buf, op.o_cum)[op.P - 1]);  // example :190-193
-            v = curve_component<NZ>(op, buf, have_curve ? nullptr : args.x + (size_t)ai * op.n, s0, yk,
-                                    t_new, gl);
-        } else {  // no trajectory yet: hold position, zero velocity (example :210-216)
+            t_new = fmin(t_prev + op.eval_step, tmax);  // example :190-193
+            const double* xr = have_curve ? nullptr : args.x + (size_t)ai * op.n;
+            v = curve_component<NZ>(op, buf, xr, s0, yk, t_new, gl);
+            if (args.substeps) {  // sub-steps 1 .. nsub - 1: the curve at t_prev + Ts k, own draws
+                for (int k = 1; k < op.nsub; k++) {
+                    double u = curve_component<NZ>(op, buf, xr, s0, yk, fmin(t_prev + op.Ts * k, tmax), gl);
+                    if (sd > 0.0) u = fma(sd, normal_sample(args.noise_seed, args.step_index, agent, gl, op.nsub - k), u);
+                    args.substeps[((size_t)ai * op.nsub + k - 1) * 6 + gl] = u;
+                }
+            }
+            if (sd > 0.0) v = fma(sd, normal_sample(args.noise_seed, args.step_index, agent, gl), v);
+        } else {
+            // no trajectory yet: hold the position at zero velocity, with each sub-step's noise
+            // added to the previous sub-step's state (example :210-216): the position draws
+            // accumulate, the velocity keeps the last one
+            double p = 0.0;
 #pragma unroll
             for (int s = 0; s < 3; s++)
-                if (s == gl) v = s0[s];
+                if (s == gl) p = s0[s];
+            for (int k = 1; k <= op.nsub; k++) {
+                const double n = sd > 0.0 ? sd * normal_sample(args.noise_seed, args.step_index, agent, gl, op.nsub - k) : 0.0;
+                p = gl < 3 ? p + n : n;
+                if (args.substeps && k < op.nsub) args.substeps[((size_t)ai * op.nsub + k - 1) * 6 + gl] = p;
+            }
+            v = p;
         }
         if (gl == 0) args.traj_t[ai] = t_new;  // every lane read t_prev above (same wave)
-    } else if (have_curve) {
-        const double* AZ = opp(buf, op.o_AZ);
-        const double* AS = opp(buf, op.o_AS);
-#pragma unroll
-        for (int s = 0; s < 6; s++) v = fma(AS[gl * 6 + s], s0[s], v);
-#pragma unroll
-        for (int j = 0; j < NZ; j++) v = fma(AZ[gl * NZ + j], yk[j], v);
     } else {
+        if (have_curve) {
+            const double* AZ = opp(buf, op.o_AZ);
+            const double* AS = opp(buf, op.o_AS);
 #pragma unroll
-        for (int s = 0; s < 6; s++)
-            if (s == gl) v = s0[s];
+            for (int s = 0; s < 6; s++) v = fma(AS[gl * 6 + s], s0[s], v);
+#pragma unroll
+            for (int j = 0; j < NZ; j++) v = fma(AZ[gl * NZ + j], yk[j], v);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 6; s++)
+                if (s == gl) v = s0[s];
+        }
+        if (sd > 0.0) v = fma(sd, normal_sample(args.noise_seed, args.step_index, agent, gl), v);
     }
-    const double sd = gl < 3 ? args.pos_std : args.vel_std;
-    if (sd > 0.0) v = fma(sd, normal_sample(args.noise_seed, args.step_index, args.agent_first + ai, gl), v);
+    if (args.substeps) args.substeps[((size_t)ai * op.nsub + op.nsub - 1) * 6 + gl] = v;
     if (args.next_states) args.next_states[(size_t)ai * 6 + gl] = v;
     if (args.grid.ins_cnt) {  // the next step's neighbour table gets this row (lane 0: x, lane 1: y)
         const int base = (int)(threadIdx.x & 63u) & ~(G - 1);

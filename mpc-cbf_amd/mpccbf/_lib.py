@@ -22,6 +22,7 @@ EXPORTED = [
     "mpccbf_status_string", "mpccbf_abi_version", "mpccbf_run_steps", "mpccbf_comm_unique_id",
     "mpccbf_comm_create", "mpccbf_comm_destroy", "mpccbf_kernel_name", "mpccbf_fov_control_solve",
     "mpccbf_connectivity_control_solve", "mpccbf_host_operators", "mpccbf_host_last_error",
+    "mpccbf_comm_create_local",
 ]
 
 
@@ -77,6 +78,7 @@ class Batch(C.Structure):
         ("stamps", C.c_void_p), ("traj_t", C.c_void_p), ("pos_std", C.c_double),
         ("vel_std", C.c_double), ("noise_seed", C.c_uint64), ("step_index", C.c_int64),
         ("cov", C.c_void_p), ("primal_res", C.c_void_p), ("dual_res", C.c_void_p),
+        ("substeps", C.c_void_p),
     ]
 
 
@@ -134,6 +136,7 @@ def load():
     L.mpccbf_run_steps.argtypes = [vp, C.POINTER(Batch), C.POINTER(Run), vp]
     L.mpccbf_comm_unique_id.argtypes = [C.c_char_p]
     L.mpccbf_comm_create.argtypes = [C.c_char_p, C.c_int32, C.c_int32, C.c_int32, C.POINTER(vp)]
+    L.mpccbf_comm_create_local.argtypes = [C.c_int32, C.c_int32, C.POINTER(vp)]
     L.mpccbf_comm_destroy.argtypes = [vp]
     L.mpccbf_comm_destroy.restype = None
     L.mpccbf_kernel_name.argtypes = [vp]
@@ -219,7 +222,7 @@ class Context:
                    agent_first=0, num_agents=None, x=None, status=None, obj=None, iters=None,
                    next_states=None, knn_k=0, knn_radius=0.0, stream=None, stamps=None,
                    traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0, cov=None,
-                   primal_res=None, dual_res=None):
+                   primal_res=None, dual_res=None, substeps=None):
         """CSR neighbours (nb_row_ptr/nb_col) or, with both None, the knn_k nearest within
         knn_radius found on the device in the same launch sequence. traj_t (float64, one per
         agent, initialised to -1) turns on the closed-loop simulator semantics: x persists the
@@ -233,7 +236,8 @@ class Context:
                   next_states=_ptr(next_states), knn_k=int(knn_k), knn_radius=float(knn_radius),
                   stamps=_ptr(stamps), traj_t=_ptr(traj_t), pos_std=float(pos_std),
                   vel_std=float(vel_std), noise_seed=int(noise_seed), step_index=int(step_index),
-                  cov=_ptr(cov), primal_res=_ptr(primal_res), dual_res=_ptr(dual_res))
+                  cov=_ptr(cov), primal_res=_ptr(primal_res), dual_res=_ptr(dual_res),
+                  substeps=_ptr(substeps))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
 
     def run_steps(self, states, states_alt, num_steps, targets=None, refs=None, agent_first=0,
@@ -463,13 +467,24 @@ class Comm:
     """RCCL communicator for the per-step all-gather of agent states (mpccbf_comm_create):
     collective — every rank constructs it with the same id."""
 
-    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int, _handle=None):
+        if _handle is not None:
+            self.handle, self.nranks, self.rank = _handle, nranks, rank
+            return
         if len(uid) != COMM_ID_BYTES:
             raise ValueError("communicator id must be 128 bytes")
         h = C.c_void_p()
         _check(load().mpccbf_comm_create(uid, nranks, rank, device, C.byref(h)))
         self.handle = h
         self.nranks, self.rank = nranks, rank
+
+    @classmethod
+    def local_group(cls, nranks: int, device: int = 0) -> list:
+        """mpccbf_comm_create_local: nranks in-process communicators (one host thread per rank,
+        one device), the multi-GPU data flow of mpccbf_run_steps on a single GPU."""
+        hs = (C.c_void_p * nranks)()
+        _check(load().mpccbf_comm_create_local(nranks, device, hs))
+        return [cls(b"", nranks, r, device, _handle=C.c_void_p(hs[r])) for r in range(nranks)]
 
     def close(self):
         if getattr(self, "handle", None):

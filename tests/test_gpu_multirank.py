@@ -1,0 +1,84 @@
+"""The multi-GPU product path of mpccbf_run_steps on one GPU.
+
+Ranks own equal contiguous agent blocks; each step every rank's IMPC kernel writes its block of
+the next state table and inserts those rows into the next step's neighbour table, the blocks are
+exchanged (an RCCL all-gather across GPUs), and the other ranks' rows are inserted after the
+exchange (grid_insert_kernel). Here the ranks are host threads on one device with the in-process
+communicator group (mpccbf_comm_create_local: the all-gather becomes device copies between the
+ranks' tables), so the whole N-rank data flow runs — table rotation, exchange, foreign-row
+insertion — and must reproduce the single-rank closed loop bit for bit. (An N > 1 run over RCCL
+needs several GPUs: the driver's scaling run.)
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from mpccbf import swarm
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a visible MI355X")
+    return torch
+
+
+def _run(mpclib, torch, cfg, states, targets, steps, nranks):
+    dev = torch.device("cuda", 0)
+    n = len(states)
+    per = n // nranks
+    comms = mpclib.Comm.local_group(nranks, 0) if nranks > 1 else [None]
+    results, errors = [None] * nranks, []
+
+    def rank_main(r):
+        try:
+            stream = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(stream):
+                ctx = mpclib.Context(cfg)
+                out = ctx.alloc_outputs(per)
+                a = torch.tensor(states, device=dev)
+                b = torch.empty_like(a)
+                tg = torch.tensor(targets[r * per:(r + 1) * per], device=dev)
+                traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
+                slog = torch.empty((steps, per, 2), dtype=torch.int32, device=dev)
+                res = ctx.run_steps(a, b, steps, targets=tg, agent_first=r * per, num_agents=per,
+                                    knn_k=8, knn_radius=3.0 * cfg["d_min"], x=out["x"], obj=out["obj"],
+                                    traj_t=traj_t, pos_std=0.001, vel_std=0.01, noise_seed=7,
+                                    status_log=slog, comm=comms[r], stream=stream)
+                stream.synchronize()
+                results[r] = (res["final"].cpu().numpy(), slog.cpu().numpy(), out["x"].cpu().numpy())
+        except Exception as e:  # surfaced in the main thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(nranks)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    for c in comms:
+        if c is not None:
+            c.close()
+    assert not errors, errors
+    return results
+
+
+@pytest.mark.parametrize("nranks,n_agents", [(2, 1024), (4, 1024)])
+def test_local_group_matches_single_rank(mpclib, nranks, n_agents):
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(n_agents, seed=13)
+    states[:, :2] *= 0.6  # crowded: CBF rows, infeasible QPs, fallback trajectories
+    steps = 12
+    single = _run(mpclib, torch, cfg, states, targets, steps, 1)[0]
+    multi = _run(mpclib, torch, cfg, states, targets, steps, nranks)
+    per = n_agents // nranks
+    for r, (final, slog, x) in enumerate(multi):
+        # every rank ends with the whole gathered table, equal to the single-rank loop
+        np.testing.assert_array_equal(final, single[0])
+        np.testing.assert_array_equal(slog, single[1][:, r * per:(r + 1) * per])
+        np.testing.assert_array_equal(x, single[2][r * per:(r + 1) * per])
+    assert not np.array_equal(single[0], states)
+    assert np.any(single[1] == 3), "the crowded swarm should produce INFEASIBLE QPs"

@@ -1,0 +1,92 @@
+"""GPU: the closed-loop simulator (mpccbf.sim) — the example's states.json trace
+(MPCCBFFormationControl_example.cpp:127-231), the per-sub-step records from the kernel, the
+accumulated position noise of robots that hold position, and the reference's collision / goal
+metrics on the trace (collision_check.py:48-80)."""
+import json
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from mpccbf import metrics, sim, swarm
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test needs a visible MI355X")
+    return torch
+
+
+def test_states_json_trace_and_metrics(mpclib, tmp_path):
+    _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(36, seed=4)
+    s = sim.Simulator(cfg, states, targets, neighbours="all", pos_std=1e-3, vel_std=1e-2, noise_seed=3)
+    s.run(1.0)  # 10 control steps
+    path = tmp_path / "states.json"
+    s.write_json(str(path))
+    js = json.load(open(path))
+    assert js["dt"] == cfg["h"] and js["Ts"] == cfg["Ts"]
+    nsub = int(cfg["h"] / cfg["Ts"])
+    assert len(js["robots"]) == 36
+    for i in range(36):
+        r = js["robots"][str(i)]
+        assert len(r["states"]) == 10 * nsub and len(r["states"][0]) == 6
+        assert len(r["pred_curve"]) == 10 and len(r["pred_curve"][0]) == 1
+    # the last sub-step record of a step is the next state the loop continues from
+    traj = metrics.trajectories_from_states_json(js)
+    np.testing.assert_array_equal(traj[:, -1, :], s.states.cpu().numpy())
+    # pred_curve of a fresh curve starts at the robot's position at that step (x0 equality)
+    st0 = np.array(states)
+    p0 = np.array(js["robots"]["0"]["pred_curve"][0][0][0])
+    assert np.max(np.abs(p0 - st0[0, :3])) < 1e-9
+    # 31 points at 0.05 over the 1.5 s curve, as the example's loop produces
+    assert len(js["robots"]["0"]["pred_curve"][0][0]) == 31
+    # the collision-free lattice, scored like the reference script: every step's records
+    ok, makespan, hit = metrics.instance_success(traj, targets, 1.0, [0.2, 0.2], "box")
+    assert ok and hit is None, hit
+    assert metrics.min_pair_distance(traj) > 2 * 0.2
+
+
+def test_substeps_follow_the_kept_curve(mpclib):
+    """Without noise every sub-step record is the kept curve at traj_t + Ts k (oracle curve eval)."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(16, seed=8)
+    s = sim.Simulator(cfg, states, targets, neighbours="all")
+    s.step()
+    p = O.make_params(cfg)
+    x = s.out["x"].cpu().numpy()
+    sub = s.substeps.cpu().numpy()
+    for i in range(16):
+        for k in range(int(cfg["h"] / cfg["Ts"])):
+            t = cfg["Ts"] * (k + 1)
+            exp = np.concatenate([O.eval_curve(p, x[i], t, 0), O.eval_curve(p, x[i], t, 1)])
+            assert np.max(np.abs(sub[i, k] - exp)) < 1e-9, (i, k)
+    torch.cuda.synchronize()
+
+
+def test_hold_position_noise_accumulates_over_substeps(mpclib):
+    """Robots with no trajectory yet hold their position at zero velocity, each of the h / Ts
+    sub-steps adding noise to the previous one (example :210-216): position variance nsub
+    pos_std^2, velocity variance vel_std^2."""
+    _torch()
+    cfg = swarm.config(15)
+    n = 4096
+    states, targets = swarm.lattice_swarm(n, seed=2)
+    states[:, 3] = 2.5  # initial velocity outside the box: every QP infeasible, no curve
+    s = sim.Simulator(cfg, states, targets, pos_std=0.01, vel_std=0.02, noise_seed=5, record=False)
+    st = s.step()
+    assert np.all(st[:, 0] == O.INFEASIBLE)
+    nxt = s.states.cpu().numpy()
+    nsub = int(cfg["h"] / cfg["Ts"])
+    dpos = (nxt[:, :3] - states[:, :3]).reshape(-1)
+    assert abs(np.std(dpos) / (0.01 * np.sqrt(nsub)) - 1.0) < 0.05
+    assert abs(np.std(nxt[:, 3:]) / 0.02 - 1.0) < 0.05
+    sub = s.substeps.cpu().numpy()
+    # sub-step k holds the sum of the first k position draws
+    steps = np.diff(np.concatenate([states[:, None, :3], sub[:, :, :3]], axis=1), axis=1)
+    assert abs(np.std(steps) / 0.01 - 1.0) < 0.05
