@@ -43,8 +43,12 @@ def test_states_json_trace_and_metrics(mpclib, tmp_path):
     st0 = np.array(states)
     p0 = np.array(js["robots"]["0"]["pred_curve"][0][0][0])
     assert np.max(np.abs(p0 - st0[0, :3])) < 1e-9
-    # 31 points at 0.05 over the 1.5 s curve, as the example's loop produces
-    assert len(js["robots"]["0"]["pred_curve"][0][0]) == 31
+    # points at 0.05 over the 1.5 s curve, as the example's double accumulation produces them
+    # (t += 0.05 overshoots 1.5 at the 31st point: 30 points)
+    n_pts, t = 0, 0.0
+    while t <= cfg["num_pieces"] * cfg["piece_max_parameter"]:
+        n_pts, t = n_pts + 1, t + 0.05
+    assert len(js["robots"]["0"]["pred_curve"][0][0]) == n_pts == 30
     # the collision-free lattice, scored like the reference script: every step's records
     ok, makespan, hit = metrics.instance_success(traj, targets, 1.0, [0.2, 0.2], "box")
     assert ok and hit is None, hit
