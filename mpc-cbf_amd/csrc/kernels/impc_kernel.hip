@@ -387,7 +387,8 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 ca.robust = attempt == 2;
                 po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y,
                                                       ca, dbg, wslack, &vslack, red, &warm,
-                                                      (attempt == 0 && warm_try) ? warm_delta : 0.0);
+                                                      (attempt == 0 && warm_try) ? warm_delta : 0.0,
+                                                      SLACK ? nullptr : stage);
                 total += po.iters;
                 ((attempt == 0 && warm_try) ? tr_warm : tr_cold) += po.iters;
                 if (po.status == ST_OPTIMAL) break;

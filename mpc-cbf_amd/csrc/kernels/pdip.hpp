@@ -130,6 +130,7 @@ struct PdipOut {
     int status;
     int iters;
     bool early = false;  // stopped by the divergence test (phase 1 decides; pdip_solve_sep)
+    bool polished = false;  // finished by the active-set solve (pdip_solve_sep)
     // OPTIMAL: scaled primal residual max_i |r_i| / (1 + |bound_i|) (bounds every row's violation)
     // and relative dual residual ||P y + q + G^T z||_inf / (1 + ||q||_inf) of the returned
     // iterate (mpccbf_batch.primal_res / dual_res); NaN otherwise

@@ -67,6 +67,180 @@ __device__ __forceinline__ void sep_solve(const double (&Mxy)[10], const double 
     x[5] = xw[1];
 }
 
+// Active-set finish (no slack variables). With the iterate's active sides (slack below dual),
+// the equality-constrained QP  min 1/2 y^T P y + q^T y  s.t.  g_i y = b_i (i active)  is solved
+// exactly in the condensed space:
+//   yu = -P^-1 q,   (G_A P^-1 G_A^T) lam = G_A yu - b_A,   y = yu - P^-1 G_A^T lam
+// (P^-1 by 2x2 channel blocks; the k <= 6 active rows staged in the group's LDS scratch `pol`, the
+// k x k system factored redundantly by every lane). Its dual residual is zero by construction and
+// complementarity exact; it is accepted as the QP's optimum when every row holds at y to the
+// primal tolerance and every multiplier has its side's sign — otherwise the PDIP continues.
+constexpr int POL_K = 6;
+
+template <int G, int SB, int CB>
+__device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
+                           const double (&q)[SEP_NZ], const double (&sl)[SEP_D][SB],
+                           const double (&su)[SEP_D][SB], const double (&zl)[SEP_D][SB],
+                           const double (&zu)[SEP_D][SB], const double (&cs)[CB], const double (&cz)[CB],
+                           const double (&pl)[SEP_D][SB], const double (&pu)[SEP_D][SB],
+                           const double (&pc)[CB], double tol, double* __restrict__ pol,
+                           double (&yo)[SEP_NZ], double& rp_out, SepWarm<SB>* warm) {
+    const int gl = threadIdx.x & (G - 1);
+    double pi[SEP_D][3], yu[SEP_NZ];
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++) {
+        const int o = 2 * d;
+        const double a = P[o * 6 + o], b = P[o * 6 + o + 1], c = P[(o + 1) * 6 + o + 1];
+        const double r = rcp(fma(a, c, -b * b));
+        pi[d][0] = c * r;
+        pi[d][1] = -b * r;
+        pi[d][2] = a * r;
+        yu[o] = -fma(pi[d][0], q[o], pi[d][1] * q[o + 1]);
+        yu[o + 1] = -fma(pi[d][1], q[o], pi[d][2] * q[o + 1]);
+    }
+    // active sides -> compact list (box lower / upper per channel and slot, then CBF rows)
+    constexpr int NS = 2 * SEP_D * SB + CB;
+    bool act[NS];
+    int pos[NS], k = 0;
+    {
+        int s = 0;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int kk = 0; kk < SB; kk++) {
+                act[s++] = sl[d][kk] < zl[d][kk];
+                act[s++] = su[d][kk] < zu[d][kk];
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++) act[s++] = has_cbf && cs[c] < cz[c];
+    }
+#pragma unroll
+    for (int s = 0; s < NS; s++) {
+        const unsigned long long m = grp_ballot<G>(act[s]);
+        pos[s] = k + __popcll(m & ((1ull << gl) - 1ull));
+        k += __popcll(m);
+    }
+    if (k == 0 || k > POL_K) return false;
+    // staged row i: g (6) | b | side sign (+1 upper, -1 lower) | P^-1 g (6)
+    {
+        int s = 0;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int kk = 0; kk < SB; kk++)
+#pragma unroll
+                for (int side = 0; side < 2; side++, s++) {
+                    if (!act[s]) continue;
+                    double* r = pol + pos[s] * 16;
+                    const double g0 = rw.bg[d][kk][0], g1 = rw.bg[d][kk][1];
+#pragma unroll
+                    for (int j = 0; j < SEP_NZ; j++) {
+                        r[j] = j == 2 * d ? g0 : (j == 2 * d + 1 ? g1 : 0.0);
+                        r[8 + j] = j == 2 * d ? fma(pi[d][0], g0, pi[d][1] * g1)
+                                              : (j == 2 * d + 1 ? fma(pi[d][1], g0, pi[d][2] * g1) : 0.0);
+                    }
+                    r[6] = side ? rw.bhi[d][kk] : rw.blo[d][kk];
+                    r[7] = side ? 1.0 : -1.0;
+                }
+#pragma unroll
+        for (int c = 0; c < CB; c++, s++) {
+            if (!act[s]) continue;
+            double* r = pol + pos[s] * 16;
+#pragma unroll
+            for (int d = 0; d < 2; d++) {
+                const double g0 = rw.cg[c][2 * d], g1 = rw.cg[c][2 * d + 1];
+                r[2 * d] = g0;
+                r[2 * d + 1] = g1;
+                r[8 + 2 * d] = fma(pi[d][0], g0, pi[d][1] * g1);
+                r[8 + 2 * d + 1] = fma(pi[d][1], g0, pi[d][2] * g1);
+            }
+            r[4] = r[5] = r[12] = r[13] = 0.0;
+            r[6] = rw.chi[c];
+            r[7] = 1.0;
+        }
+    }
+    wave_lds_sync();
+    using S6 = Sym<POL_K>;
+    double K[S6::P], rhs[POL_K], dk[POL_K], lam[POL_K];
+#pragma unroll
+    for (int i = 0; i < POL_K; i++) {
+        const bool ai = i < k;
+        const double* ri = pol + (ai ? i : 0) * 16;
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], yu[j], t);
+        rhs[i] = ai ? t - ri[6] : 0.0;
+#pragma unroll
+        for (int j = i; j < POL_K; j++) {
+            const double* wj = pol + (j < k ? j : 0) * 16 + 8;
+            double v = 0.0;
+#pragma unroll
+            for (int m = 0; m < SEP_NZ; m++) v = fma(ri[m], wj[m], v);
+            K[S6::idx(i, j)] = (ai && j < k) ? v : (i == j ? 1.0 : 0.0);
+        }
+    }
+    const bool okf = chol_packed<POL_K>(K, dk);
+    chol_solve<POL_K>(K, dk, rhs, lam);
+    double y[SEP_NZ], lmax = 0.0;
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
+    bool bad = !okf;
+#pragma unroll
+    for (int i = 0; i < POL_K; i++) {
+        if (i < k) {
+            const double* wi = pol + i * 16 + 8;
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-lam[i], wi[j], y[j]);
+            lmax = fmax(lmax, fabs(lam[i]));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < POL_K; i++)
+        if (i < k) bad = bad || !(pol[i * 16 + 7] * lam[i] >= -1e-9 * (1.0 + lmax));
+    // every row at y (scaled violation, as the PDIP's primal residual)
+    double rp = 0.0;
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+        for (int kk = 0; kk < SB; kk++) {
+            const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
+            rp = fmax(rp, fmax((rw.blo[d][kk] - t) * pl[d][kk], (t - rw.bhi[d][kk]) * pu[d][kk]));
+        }
+    if (has_cbf) {
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
+            rp = fmax(rp, (t - rw.chi[c]) * pc[c]);
+        }
+    }
+    rp = grp_max<G>(rp);
+    wave_lds_sync();  // the scratch is reused
+    if (bad || !(rp <= tol)) return false;
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
+    rp_out = rp;
+    if (warm != nullptr) {  // the multipliers as the next warm start's box duals
+        int s = 0;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int kk = 0; kk < SB; kk++) {
+                double ml = 0.0, mu = 0.0;
+#pragma unroll
+                for (int i = 0; i < POL_K; i++) {
+                    ml = (act[s] && pos[s] == i) ? -lam[i] : ml;
+                    mu = (act[s + 1] && pos[s + 1] == i) ? lam[i] : mu;
+                }
+                warm->zl[d][kk] = fmax(ml, 0.0);
+                warm->zu[d][kk] = fmax(mu, 0.0);
+                s += 2;
+            }
+    }
+    return true;
+}
+
 // P: 6x6 row-major block-diagonal reduced Hessian, LP its lower Cholesky factor (uniform).
 // has_cbf: group-uniform flag (some CBF slot of the group is live); when false the CBF slots
 // are skipped entirely (and do not count as sides).
@@ -82,7 +256,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                                   const double* __restrict__ LP, const double (&q)[SEP_NZ],
                                   double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg = nullptr,
                                   double wv_cost = 0.0, double* v_out = nullptr, double* red = nullptr,
-                                  SepWarm<SB>* warm = nullptr, double warm_delta = 0.0) {
+                                  SepWarm<SB>* warm = nullptr, double warm_delta = 0.0,
+                                  double* pol = nullptr) {
     (void)dbg;
     const bool slk = SLACK && has_cbf;  // group-uniform
     // slack variable, its bound's slack and dual; the dual starts at the linear cost it carries at
@@ -200,6 +375,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
     // residual stalls (see below)
     double ybest_l = 0.0, best_rd = 1e300, best_rp = 0.0;
     int endgame = 0;
+    double polish_mu = 0.0;
     const int gl_s = threadIdx.x & (G - 1);
     for (int it = 0;; it++) {
         PSTAMP(0);
@@ -430,7 +606,25 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             }
             stop_best = ++endgame >= 3;
         }
-        if (it == 0) mu0 = mu;
+        if (it == 0) {
+            mu0 = mu;
+            polish_mu = 1e-3 * mu;
+        }
+        // active-set finish (sep_polish) once mu has fallen 1000x, then after every further 100x
+        if constexpr (!SLACK) {
+            if (pol != nullptr && finite && it > 0 && mu <= polish_mu) {
+                double rpp = 0.0;
+                if (sep_polish<G, SB, CB>(rw, has_cbf, P, q, sl, su, zl, zu, cs, cz, pl, pu, pc, cfg.tol, pol, y,
+                                          rpp, warm)) {
+                    out.status = ST_OPTIMAL;
+                    out.rp = rpp;
+                    out.rd = 0.0;
+                    out.polished = true;
+                    break;
+                }
+                polish_mu = 1e-2 * mu;
+            }
+        }
         auto take_best = [&]() {  // the endgame's best iterate, if it meets the relaxed tolerance
             if (slk || !(best_rd <= cfg.rd_relax)) return false;  // slack mode: v is not kept
 #pragma unroll
@@ -739,7 +933,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #endif
     }
     if (v_out) *v_out = slk ? v : 0.0;
-    if (warm != nullptr && out.status == ST_OPTIMAL) {
+    if (warm != nullptr && out.status == ST_OPTIMAL && !out.polished) {
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
