@@ -244,6 +244,12 @@ __device__ double lane_slack_weight(const DevOps& op, const ImpcArgs& args, cons
     return gl < nnb ? op.slack_cost * pow(op.slack_decay, (double)rank) : 1.0;
 }
 
+// state row `row` of the batch (re-read where needed instead of held in registers)
+__device__ __forceinline__ void load_state(const ImpcArgs& args, int row, double (&s)[6]) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) s[i] = __builtin_nontemporal_load(args.states + (size_t)row * 6 + i);
+}
+
 // Hand agent ai to the fallback launch (lane 0 appends it to args.defer: [count, -, agents...]).
 __device__ __forceinline__ void defer_agent(const ImpcArgs& args, int ai, int gl) {
     if (gl == 0) {
@@ -256,7 +262,8 @@ __device__ __forceinline__ void defer_agent(const ImpcArgs& args, int ai, int gl
 // this group's LDS (CBF-row staging, Newton-sum all-reduce, neighbour query).
 template <int SB, int CB, bool SLACK>
 __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
-                               const int ai, const int gl, double* stage, double* red, NbScratch& nbs) {
+                               const int ai, const int gl, double* stage, double* red, NbScratch& nbs,
+                               double* keep) {
     constexpr int G = 16;
     constexpr int NZ = SEP_NZ;
     constexpr int cap = CB * G;  // CBF rows per agent
@@ -309,12 +316,15 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     if constexpr (SLACK) wslack = lane_slack_weight<G>(op, args, s0, grid_mode, nbs.idx, nb0, nnb, gl);
     stamp(args, ai, gl, 2);
 
-    double y[NZ], ykeep[NZ];
+    // the kept solution and the warm-start duals live in per-lane LDS slots (keep: [ykeep 6 x 16 |
+    // warm 2 x 3 x SB x 16]), not registers: they are touched once per IMPC iteration
+    double y[NZ];
+    double* ykeep = keep + gl;  // ykeep[16 * i]
 #pragma unroll
-    for (int i = 0; i < NZ; i++) y[i] = ykeep[i] = 0.0;
+    for (int i = 0; i < NZ; i++) y[i] = ykeep[16 * i] = 0.0;
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
-    SepWarm<SB> warm;  // box duals of the previous OPTIMAL solve (iteration 1 warm start)
+    SepWarm<SB> warm{keep + 16 * NZ};  // box duals of the previous OPTIMAL solve (iteration 1 warm start)
     const double warm_delta = SLACK ? 0.0 : op.warm_delta;
 
     for (int it = 0; it < op.impc_iter; it++) {
@@ -328,9 +338,13 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         bool live = false;
         if constexpr (SLACK) {
             // slack mode: rows stay in their neighbour's lane; a slack row is never infeasible
-            live = lane_cbf_rows<G, CB>(op, buf, args, it, s0, y, grid_mode, nbs.idx, nb0, nnb, gl, rw);
+            double sx[6];  // the state again (not kept in registers across the solves)
+            load_state(args, self, sx);
+            live = lane_cbf_rows<G, CB>(op, buf, args, it, sx, y, grid_mode, nbs.idx, nb0, nnb, gl, rw);
         } else {
-            count = stage_cbf_rows<NZ, G>(op, buf, args, it, s0, y, grid_mode, nbs.idx,
+            double sx[6];  // the state again (not kept in registers across the solves)
+            load_state(args, self, sx);
+            count = stage_cbf_rows<NZ, G>(op, buf, args, it, sx, y, grid_mode, nbs.idx,
                                           nb0, nnb, stage, cap, gl, &row_infeasible);
             live = count > 0;
 #pragma unroll
@@ -432,7 +446,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
             objv = reduced_objective<NZ>(op, buf, q, y, kconst);
             if constexpr (SLACK) objv += grp_sum<G>(live ? wslack * vslack : 0.0);  // + w^T v
 #pragma unroll
-            for (int i = 0; i < NZ; i++) ykeep[i] = y[i];
+            for (int i = 0; i < NZ; i++) ykeep[16 * i] = y[i];
             have_curve = true;
         } else {
             success = false;
@@ -441,7 +455,11 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
         wave_lds_sync();
     }
-    write_agent_outputs<NZ, G>(op, buf, args, ai, gl, s0, ykeep, have_curve);
+    double yk[NZ], sx[6];
+#pragma unroll
+    for (int i = 0; i < NZ; i++) yk[i] = ykeep[16 * i];
+    load_state(args, self, sx);
+    write_agent_outputs<NZ, G>(op, buf, args, ai, gl, sx, yk, have_curve);
     stamp(args, ai, gl, 7);
 }
 
@@ -455,18 +473,20 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     __shared__ double stage_all[GPB][SLACK ? 1 : CB * 16 * (SEP_NZ + 1)];
     __shared__ double red_all[GPB][16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
+    __shared__ double keep_all[GPB][16 * (SEP_NZ + 2 * SEP_D * SB)];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     if constexpr (!QUEUE) {
         grid_clear(args);
         const int ai = blockIdx.x * GPB + gib;
         if (ai >= args.num_agents) return;
-        impc_sep_agent<SB, CB, SLACK>(op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib]);
+        impc_sep_agent<SB, CB, SLACK>(op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib],
+                                      keep_all[gib]);
     } else {
         const int n = args.queue[0];
         for (int k = blockIdx.x * GPB + gib; k < n; k += gridDim.x * GPB)
             impc_sep_agent<SB, CB, SLACK>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
-                                          nb_scratch[gib]);
+                                          nb_scratch[gib], keep_all[gib]);
         __syncthreads();
         if (threadIdx.x == 0) {
             __threadfence();

@@ -49,8 +49,14 @@ __device__ __forceinline__ void acc_blk2(double* a, double D, double g0, double 
 // Box-row duals of the last OPTIMAL solve: IMPC iteration 1 has the same box rows and cost as
 // iteration 0 and differs only in its CBF rows, so it starts from iteration 0's primal-dual point.
 template <int SB>
-struct SepWarm {
-    double zl[SEP_D][SB], zu[SEP_D][SB];
+struct SepWarm {  // per-lane slots in the group's LDS ([2][SEP_D][SB][16] doubles): no registers
+    double* base;
+    __device__ __forceinline__ double& zl(int d, int k) const {
+        return base[(d * SB + k) * 16 + (threadIdx.x & 15)];
+    }
+    __device__ __forceinline__ double& zu(int d, int k) const {
+        return base[((SEP_D + d) * SB + k) * 16 + (threadIdx.x & 15)];
+    }
 };
 
 // Solve with the separable Newton matrix: 4x4 packed (x, y) factor + 2x2 packed yaw factor.
@@ -233,8 +239,8 @@ __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double
                     ml = (act[s] && pos[s] == i) ? -lam[i] : ml;
                     mu = (act[s + 1] && pos[s + 1] == i) ? lam[i] : mu;
                 }
-                warm->zl[d][kk] = fmax(ml, 0.0);
-                warm->zu[d][kk] = fmax(mu, 0.0);
+                warm->zl(d, kk) = fmax(ml, 0.0);
+                warm->zu(d, kk) = fmax(mu, 0.0);
                 s += 2;
             }
     }
@@ -306,7 +312,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #pragma unroll
                 for (int d = 0; d < SEP_D; d++)
 #pragma unroll
-                    for (int k = 0; k < SB; k++) warm->zl[d][k] = warm->zu[d][k] = 0.0;
+                    for (int k = 0; k < SB; k++) warm->zl(d, k) = warm->zu(d, k) = 0.0;
             }
             // residuals of the returned point: rows satisfied exactly, multipliers zero
             double rdn = 0.0, qn0 = 0.0;
@@ -338,8 +344,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             if (use_warm) {
                 sl[d][k] = fmax(t - rw.blo[d][k], wd);
                 su[d][k] = fmax(rw.bhi[d][k] - t, wd);
-                zl[d][k] = fmax(warm->zl[d][k], wd);
-                zu[d][k] = fmax(warm->zu[d][k], wd);
+                zl[d][k] = fmax(warm->zl(d, k), wd);
+                zu[d][k] = fmax(warm->zu(d, k), wd);
             } else {
                 sl[d][k] = fmax(t - rw.blo[d][k], 1.0);
                 su[d][k] = fmax(rw.bhi[d][k] - t, 1.0);
@@ -938,8 +944,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
             for (int k = 0; k < SB; k++) {
-                warm->zl[d][k] = zl[d][k];
-                warm->zu[d][k] = zu[d][k];
+                warm->zl(d, k) = zl[d][k];
+                warm->zu(d, k) = zu[d][k];
             }
     }
 #ifdef MPCCBF_DEBUG_EXIT

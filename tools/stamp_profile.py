@@ -64,8 +64,12 @@ for v in VARIANTS:
         tot = ps[okp, 11] - ps[okp, 0]
         print(f"variant {v}: Newton step 2 of solve 0, {okp.sum()} agents, cycles mean {tot.mean():.0f} "
               f"p50 {np.median(tot):.0f}")
+        s_tmp = allst[:N * 8].reshape(N, 8)
+        crit0 = int(np.argmax(s_tmp[:, 7] - s_tmp[:, 0].min()))
+        dc = np.diff(ps[crit0, :12]) if okp[crit0] else None
         for k, name in enumerate(PPH_FOV if FOV else PPH):
-            print(f"   {name:15s} mean {d[:, k].mean():7.0f}  p50 {np.median(d[:, k]):7.0f} cycles")
+            print(f"   {name:15s} mean {d[:, k].mean():7.0f}  p50 {np.median(d[:, k]):7.0f} cycles"
+                  + (f"   critical agent {dc[k]:7.0f}" if dc is not None else ""))
     status = out["status"].cpu().numpy()
     t0 = s[:, 0].min()
     start = s[:, 0] - t0
