@@ -372,11 +372,14 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     d.feas_tol = 1e-6;  // CPLEX default feasibility tolerance
     d.early_it = 10;
     d.fast_start = 1;
+    d.dual_as = 24;
     {  // tuning overrides (diagnostics)
         const char* e = getenv("MPCCBF_EARLY_IT");
         if (e) d.early_it = atoi(e);
         const char* f = getenv("MPCCBF_FAST_START");
         if (f) d.fast_start = atoi(f);
+        const char* g = getenv("MPCCBF_DUAL_AS");
+        if (g) d.dual_as = atoi(g);
     }
     c->variant = 0;
     hipError_t e = hipSetDevice(c->device);

@@ -46,6 +46,7 @@ struct DevOps {
     // divergence test of the first solve (PdipCfg::early_it; 0 = off)
     int32_t early_it;
     int32_t fast_start;  // PdipCfg::fast_start
+    int32_t dual_as;     // PdipCfg::dual_as (first attempt)
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;

@@ -399,6 +399,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 ca.early_it = attempt == 0 ? op.early_it : 0;
                 ca.fast_start = op.fast_start != 0;
                 ca.robust = attempt == 2;
+                ca.dual_as = attempt == 0 ? op.dual_as : 0;
                 po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y,
                                                       ca, dbg, wslack, &vslack, red, &warm,
                                                       (attempt == 0 && warm_try) ? warm_delta : 0.0,

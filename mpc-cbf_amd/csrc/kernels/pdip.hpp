@@ -124,6 +124,9 @@ struct PdipCfg {
     // pdip_solve_sep: relative dual residual accepted once primal feasibility and mu are three
     // orders past their targets (SURVEY.md §8c parity rule; CPLEX's default optimality tolerance)
     double rd_relax = 1e-6;
+    // pdip_solve_sep (no slack variables): when the unconstrained minimiser violates a row, the
+    // dual active-set method (sep_dual_as) with at most this many steps first; 0: off
+    int dual_as = 0;
 };
 
 struct PdipOut {

@@ -73,26 +73,21 @@ __device__ __forceinline__ void sep_solve(const double (&Mxy)[10], const double 
     x[5] = xw[1];
 }
 
-// Active-set finish (no slack variables). With the iterate's active sides (slack below dual),
-// the equality-constrained QP  min 1/2 y^T P y + q^T y  s.t.  g_i y = b_i (i active)  is solved
-// exactly in the condensed space:
+// ---- Active-set solves (no slack variables)
+// The equality-constrained QP on a set A of active sides,
+//   min 1/2 y^T P y + q^T y  s.t.  g_i y = b_i (i in A),
+// is solved exactly in the condensed space:
 //   yu = -P^-1 q,   (G_A P^-1 G_A^T) lam = G_A yu - b_A,   y = yu - P^-1 G_A^T lam
-// (P^-1 by 2x2 channel blocks; the k <= 6 active rows staged in the group's LDS scratch `pol`, the
-// k x k system factored redundantly by every lane). Its dual residual is zero by construction and
-// complementarity exact; it is accepted as the QP's optimum when every row holds at y to the
-// primal tolerance and every multiplier has its side's sign — otherwise the PDIP continues.
+// (P^-1 by 2x2 channel blocks; the k <= 6 rows staged in the group's LDS scratch `pol`, the k x k
+// system factored redundantly by every lane). Its dual residual is zero up to rounding and
+// complementarity exact; it is the QP's optimum when every row holds at y to the primal
+// tolerance and every multiplier has its side's sign.
 constexpr int POL_K = 6;
+// staged row (16 doubles): g (6) | b | side sign (+1 upper, -1 lower) | P^-1 g (6) | side id | -
+constexpr int POL_B = 6, POL_SGN = 7, POL_W = 8, POL_ID = 14;
 
-template <int G, int SB, int CB>
-__device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
-                           const double (&q)[SEP_NZ], const double (&sl)[SEP_D][SB],
-                           const double (&su)[SEP_D][SB], const double (&zl)[SEP_D][SB],
-                           const double (&zu)[SEP_D][SB], const double (&cs)[CB], const double (&cz)[CB],
-                           const double (&pl)[SEP_D][SB], const double (&pu)[SEP_D][SB],
-                           const double (&pc)[CB], double tol, double* __restrict__ pol,
-                           double (&yo)[SEP_NZ], double& rp_out, SepWarm<SB>* warm) {
-    const int gl = threadIdx.x & (G - 1);
-    double pi[SEP_D][3], yu[SEP_NZ];
+// inverse of P's 2x2 channel blocks: pi[d] = (a, b, c) of [[a b] [b c]]
+__device__ __forceinline__ void sep_pinv(const double* __restrict__ P, double (&pi)[SEP_D][3]) {
 #pragma unroll
     for (int d = 0; d < SEP_D; d++) {
         const int o = 2 * d;
@@ -101,6 +96,179 @@ __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double
         pi[d][0] = c * r;
         pi[d][1] = -b * r;
         pi[d][2] = a * r;
+    }
+}
+
+// Side s of this lane (s = 2 (d SB + kk) + upper for the box rows, 2 SEP_D SB + c for the CBF
+// rows) staged as the 16-double row r; s may be a run-time value (the unrolled compares select).
+template <int SB, int CB>
+__device__ __forceinline__ void sep_stage_side(const SepRows<SB, CB>& rw, const double (&pi)[SEP_D][3], int s,
+                                               int gl, double* __restrict__ r) {
+    double g[SEP_NZ], b = 0.0, sg = 1.0;
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) g[j] = 0.0;
+    int i = 0;
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+        for (int kk = 0; kk < SB; kk++)
+#pragma unroll
+            for (int side = 0; side < 2; side++, i++) {
+                if (i != s) continue;
+                g[2 * d] = rw.bg[d][kk][0];
+                g[2 * d + 1] = rw.bg[d][kk][1];
+                b = side ? rw.bhi[d][kk] : rw.blo[d][kk];
+                sg = side ? 1.0 : -1.0;
+            }
+#pragma unroll
+    for (int c = 0; c < CB; c++, i++) {
+        if (i != s) continue;
+#pragma unroll
+        for (int j = 0; j < 4; j++) g[j] = rw.cg[c][j];
+        b = rw.chi[c];
+        sg = 1.0;
+    }
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) r[j] = g[j];
+    r[POL_B] = b;
+    r[POL_SGN] = sg;
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++) {
+        r[POL_W + 2 * d] = fma(pi[d][0], g[2 * d], pi[d][1] * g[2 * d + 1]);
+        r[POL_W + 2 * d + 1] = fma(pi[d][1], g[2 * d], pi[d][2] * g[2 * d + 1]);
+    }
+    r[POL_ID] = (double)(s * 16 + gl);
+}
+
+// The EQP on the k staged rows of pol, verified: returns true (yo, scaled primal residual, relative
+// dual residual ||P y + q + G_A^T lam||_inf / (1 + ||q||_inf) — RD false: 0, its value by
+// construction, not re-evaluated where registers are short — and the multipliers as the next
+// warm start's box duals) when every row holds at y to tol and every multiplier has its side's
+// sign. sc: the sides' violation scales 1 / (1 + |bound|) (box lower, upper per slot, then CBF).
+template <int G, int SB, int CB, bool RD>
+__device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
+                               const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], int k,
+                               const double* __restrict__ pol, const double (&sc)[2 * SEP_D * SB + CB],
+                               double tol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
+                               SepWarm<SB>* warm) {
+    const int gl = threadIdx.x & (G - 1);
+    using S6 = Sym<POL_K>;
+    double K[S6::P], rhs[POL_K], dk[POL_K], lam[POL_K];
+#pragma unroll
+    for (int i = 0; i < POL_K; i++) {
+        const bool ai = i < k;
+        const double* ri = pol + (ai ? i : 0) * 16;
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], yu[j], t);
+        rhs[i] = ai ? t - ri[POL_B] : 0.0;
+#pragma unroll
+        for (int j = i; j < POL_K; j++) {
+            const double* wj = pol + (j < k ? j : 0) * 16 + POL_W;
+            double v = 0.0;
+#pragma unroll
+            for (int m = 0; m < SEP_NZ; m++) v = fma(ri[m], wj[m], v);
+            K[S6::idx(i, j)] = (ai && j < k) ? v : (i == j ? 1.0 : 0.0);
+        }
+    }
+    const bool okf = chol_packed<POL_K>(K, dk);
+    chol_solve<POL_K>(K, dk, rhs, lam);
+    double y[SEP_NZ], lmax = 0.0;
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
+#pragma unroll
+    for (int i = 0; i < POL_K; i++) {
+        if (i < k) {
+            const double* wi = pol + i * 16 + POL_W;
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-lam[i], wi[j], y[j]);
+            lmax = fmax(lmax, fabs(lam[i]));
+        }
+    }
+    bool bad = !okf;
+#pragma unroll
+    for (int i = 0; i < POL_K; i++)
+        if (i < k) bad = bad || !(pol[i * 16 + POL_SGN] * lam[i] >= -1e-9 * (1.0 + lmax));
+    // every row at y (scaled violation, as the PDIP's primal residual)
+    double rp = 0.0;
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+        for (int kk = 0; kk < SB; kk++) {
+            const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
+            rp = fmax(rp, fmax((rw.blo[d][kk] - t) * sc[2 * (d * SB + kk)], (t - rw.bhi[d][kk]) * sc[2 * (d * SB + kk) + 1]));
+        }
+    if (has_cbf) {
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
+            rp = fmax(rp, (t - rw.chi[c]) * sc[2 * SEP_D * SB + c]);
+        }
+    }
+    rp = grp_max<G>(rp);
+    const bool ok = !bad && rp <= tol;
+    if (ok) {
+        // dual residual P y + q + G_A^T lam (group-uniform)
+        double rd = 0.0, qn = 0.0;
+#pragma unroll
+        for (int d = 0; d < (RD ? SEP_D : 0); d++) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int o = 2 * d + h;
+                double v = fma(P[o * 6 + 2 * d], y[2 * d], fma(P[o * 6 + 2 * d + 1], y[2 * d + 1], q[o]));
+#pragma unroll
+                for (int i = 0; i < POL_K; i++)
+                    if (i < k) v = fma(lam[i], pol[i * 16 + o], v);
+                rd = fmax(rd, fabs(v));
+                qn = fmax(qn, fabs(q[o]));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
+        rp_out = rp;
+        rd_out = rd * rcp(1.0 + qn);
+        if (warm != nullptr) {  // the multipliers as the next warm start's box duals
+#pragma unroll
+            for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+                for (int kk = 0; kk < SB; kk++) {
+                    const double il = (double)((2 * (d * SB + kk)) * 16 + gl), iu = il + 16.0;
+                    double ml = 0.0, mu = 0.0;
+#pragma unroll
+                    for (int i = 0; i < POL_K; i++) {
+                        if (i < k) {
+                            const double id = pol[i * 16 + POL_ID];
+                            ml = id == il ? -lam[i] : ml;
+                            mu = id == iu ? lam[i] : mu;
+                        }
+                    }
+                    warm->zl(d, kk) = fmax(ml, 0.0);
+                    warm->zu(d, kk) = fmax(mu, 0.0);
+                }
+        }
+    }
+    wave_lds_sync();  // the scratch is reused
+    return ok;
+}
+
+// Active-set finish of the PDIP: A = the iterate's active sides (slack below dual), when there
+// are at most 6 of them.
+template <int G, int SB, int CB>
+__device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
+                           const double (&q)[SEP_NZ], const double (&sl)[SEP_D][SB],
+                           const double (&su)[SEP_D][SB], const double (&zl)[SEP_D][SB],
+                           const double (&zu)[SEP_D][SB], const double (&cs)[CB], const double (&cz)[CB],
+                           const double (&pl)[SEP_D][SB], const double (&pu)[SEP_D][SB],
+                           const double (&pc)[CB], double tol, double* __restrict__ pol,
+                           double (&yo)[SEP_NZ], double& rp_out, double& rd_out, SepWarm<SB>* warm) {
+    const int gl = threadIdx.x & (G - 1);
+    double pi[SEP_D][3], yu[SEP_NZ];
+    sep_pinv(P, pi);
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++) {
+        const int o = 2 * d;
         yu[o] = -fma(pi[d][0], q[o], pi[d][1] * q[o + 1]);
         yu[o + 1] = -fma(pi[d][1], q[o], pi[d][2] * q[o + 1]);
     }
@@ -127,124 +295,206 @@ __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double
         k += __popcll(m);
     }
     if (k == 0 || k > POL_K) return false;
-    // staged row i: g (6) | b | side sign (+1 upper, -1 lower) | P^-1 g (6)
+#pragma unroll
+    for (int s = 0; s < NS; s++)
+        if (act[s]) sep_stage_side<SB, CB>(rw, pi, s, gl, pol + pos[s] * 16);
+    wave_lds_sync();
+    double sc[NS];
     {
         int s = 0;
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
-            for (int kk = 0; kk < SB; kk++)
-#pragma unroll
-                for (int side = 0; side < 2; side++, s++) {
-                    if (!act[s]) continue;
-                    double* r = pol + pos[s] * 16;
-                    const double g0 = rw.bg[d][kk][0], g1 = rw.bg[d][kk][1];
-#pragma unroll
-                    for (int j = 0; j < SEP_NZ; j++) {
-                        r[j] = j == 2 * d ? g0 : (j == 2 * d + 1 ? g1 : 0.0);
-                        r[8 + j] = j == 2 * d ? fma(pi[d][0], g0, pi[d][1] * g1)
-                                              : (j == 2 * d + 1 ? fma(pi[d][1], g0, pi[d][2] * g1) : 0.0);
-                    }
-                    r[6] = side ? rw.bhi[d][kk] : rw.blo[d][kk];
-                    r[7] = side ? 1.0 : -1.0;
-                }
-#pragma unroll
-        for (int c = 0; c < CB; c++, s++) {
-            if (!act[s]) continue;
-            double* r = pol + pos[s] * 16;
-#pragma unroll
-            for (int d = 0; d < 2; d++) {
-                const double g0 = rw.cg[c][2 * d], g1 = rw.cg[c][2 * d + 1];
-                r[2 * d] = g0;
-                r[2 * d + 1] = g1;
-                r[8 + 2 * d] = fma(pi[d][0], g0, pi[d][1] * g1);
-                r[8 + 2 * d + 1] = fma(pi[d][1], g0, pi[d][2] * g1);
+            for (int kk = 0; kk < SB; kk++) {
+                sc[s++] = pl[d][kk];
+                sc[s++] = pu[d][kk];
             }
-            r[4] = r[5] = r[12] = r[13] = 0.0;
-            r[6] = rw.chi[c];
-            r[7] = 1.0;
-        }
+#pragma unroll
+        for (int c = 0; c < CB; c++) sc[s++] = pc[c];
     }
-    wave_lds_sync();
-    using S6 = Sym<POL_K>;
-    double K[S6::P], rhs[POL_K], dk[POL_K], lam[POL_K];
-#pragma unroll
-    for (int i = 0; i < POL_K; i++) {
-        const bool ai = i < k;
-        const double* ri = pol + (ai ? i : 0) * 16;
-        double t = 0.0;
-#pragma unroll
-        for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], yu[j], t);
-        rhs[i] = ai ? t - ri[6] : 0.0;
-#pragma unroll
-        for (int j = i; j < POL_K; j++) {
-            const double* wj = pol + (j < k ? j : 0) * 16 + 8;
-            double v = 0.0;
-#pragma unroll
-            for (int m = 0; m < SEP_NZ; m++) v = fma(ri[m], wj[m], v);
-            K[S6::idx(i, j)] = (ai && j < k) ? v : (i == j ? 1.0 : 0.0);
-        }
-    }
-    const bool okf = chol_packed<POL_K>(K, dk);
-    chol_solve<POL_K>(K, dk, rhs, lam);
-    double y[SEP_NZ], lmax = 0.0;
-#pragma unroll
-    for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
-    bool bad = !okf;
-#pragma unroll
-    for (int i = 0; i < POL_K; i++) {
-        if (i < k) {
-            const double* wi = pol + i * 16 + 8;
-#pragma unroll
-            for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-lam[i], wi[j], y[j]);
-            lmax = fmax(lmax, fabs(lam[i]));
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < POL_K; i++)
-        if (i < k) bad = bad || !(pol[i * 16 + 7] * lam[i] >= -1e-9 * (1.0 + lmax));
-    // every row at y (scaled violation, as the PDIP's primal residual)
-    double rp = 0.0;
-#pragma unroll
-    for (int d = 0; d < SEP_D; d++)
-#pragma unroll
-        for (int kk = 0; kk < SB; kk++) {
-            const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
-            rp = fmax(rp, fmax((rw.blo[d][kk] - t) * pl[d][kk], (t - rw.bhi[d][kk]) * pu[d][kk]));
-        }
-    if (has_cbf) {
-#pragma unroll
-        for (int c = 0; c < CB; c++) {
-            double t = 0.0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
-            rp = fmax(rp, (t - rw.chi[c]) * pc[c]);
-        }
-    }
-    rp = grp_max<G>(rp);
-    wave_lds_sync();  // the scratch is reused
-    if (bad || !(rp <= tol)) return false;
-#pragma unroll
-    for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
-    rp_out = rp;
-    if (warm != nullptr) {  // the multipliers as the next warm start's box duals
+    return sep_eqp_finish<G, SB, CB, false>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm);
+}
+
+// Dual active-set solve (Goldfarb & Idnani's method, range-space form) from the unconstrained
+// minimiser yu: the most violated side (scaled as the primal residual) is the candidate; the
+// direction z that keeps the active sides exact moves y onto it unless an active multiplier
+// reaches zero first, in which case that side leaves and the step is retried. Every step keeps
+// the iterate dual feasible and raises the objective, and costs one k x k factorisation (k <= 6,
+// rows in pol, the candidate in row POL_K). The converged active set's EQP is verified by
+// sep_eqp_finish. Returns 1: optimal (yo, residuals, warm duals set); -1: no step reaches the
+// candidate (its side is a combination of the active ones and no multiplier can leave: no
+// feasible point, phase 1 decides; yo = last iterate); 0: gave up (step limit, breakdown, or the
+// verification failed) — the PDIP solves the QP.
+template <int G, int SB, int CB>
+__device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
+                           const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
+                           double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
+                           int& steps, SepWarm<SB>* warm) {
+    static_assert(G == 16, "rows of pol are copied one column per lane");
+    const int gl = threadIdx.x & (G - 1);
+    double pi[SEP_D][3];
+    sep_pinv(P, pi);
+    constexpr int NS = 2 * SEP_D * SB + CB;
+    double sc[NS];  // violation scale 1 / (1 + |bound|) per side
+    {
         int s = 0;
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
             for (int kk = 0; kk < SB; kk++) {
-                double ml = 0.0, mu = 0.0;
-#pragma unroll
-                for (int i = 0; i < POL_K; i++) {
-                    ml = (act[s] && pos[s] == i) ? -lam[i] : ml;
-                    mu = (act[s + 1] && pos[s + 1] == i) ? lam[i] : mu;
-                }
-                warm->zl(d, kk) = fmax(ml, 0.0);
-                warm->zu(d, kk) = fmax(mu, 0.0);
-                s += 2;
+                sc[s++] = rcp(1.0 + fabs(rw.blo[d][kk]));
+                sc[s++] = rcp(1.0 + fabs(rw.bhi[d][kk]));
             }
+#pragma unroll
+        for (int c = 0; c < CB; c++) sc[s++] = rcp(1.0 + fabs(rw.chi[c]));
     }
-    return true;
+    double y[SEP_NZ], u[POL_K];
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
+#pragma unroll
+    for (int i = 0; i < POL_K; i++) u[i] = 0.0;
+    int k = 0;
+    steps = 0;
+    const double add_tol = 0.1 * tol;
+    double* cand = pol + POL_K * 16;
+    for (;;) {
+        // the most violated side of the group (lowest lane on ties)
+        double vb = -1.0;
+        int sb = 0;
+        {
+            int s = 0;
+#pragma unroll
+            for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+                for (int kk = 0; kk < SB; kk++) {
+                    const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
+                    const double vl = (rw.blo[d][kk] - t) * sc[s];
+                    if (vl > vb) vb = vl, sb = s;
+                    s++;
+                    const double vu = (t - rw.bhi[d][kk]) * sc[s];
+                    if (vu > vb) vb = vu, sb = s;
+                    s++;
+                }
+            if (has_cbf) {
+#pragma unroll
+                for (int c = 0; c < CB; c++, s++) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
+                    const double vc = (t - rw.chi[c]) * sc[s];
+                    if (vc > vb) vb = vc, sb = s;
+                }
+            }
+        }
+        const double m = grp_max<G>(vb);
+        if (!(m > add_tol)) break;
+        if (steps >= maxstep) return 0;
+        const int owner = __ffsll((long long)grp_ballot<G>(vb == m)) - 1;
+        if (gl == owner) sep_stage_side<SB, CB>(rw, pi, sb, gl, cand);
+        wave_lds_sync();
+        double up = 0.0;  // the candidate's multiplier
+        for (;;) {
+            if (++steps > maxstep) return 0;
+            double gp[SEP_NZ], wp[SEP_NZ];
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) {
+                gp[j] = cand[j];
+                wp[j] = cand[POL_W + j];
+            }
+            const double bp = cand[POL_B], sp = cand[POL_SGN];
+            // rho = (G_A P^-1 G_A^T)^-1 G_A P^-1 g_p: the active multipliers' change per unit step
+            using S6 = Sym<POL_K>;
+            double K[S6::P], c[POL_K], dk[POL_K], rho[POL_K], sgn[POL_K];
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) {
+                const bool ai = i < k;
+                const double* ri = pol + (ai ? i : 0) * 16;
+                double t = 0.0;
+#pragma unroll
+                for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], wp[j], t);
+                c[i] = ai ? sp * t : 0.0;
+                sgn[i] = ri[POL_SGN];
+#pragma unroll
+                for (int j = i; j < POL_K; j++) {
+                    const double* wj = pol + (j < k ? j : 0) * 16 + POL_W;
+                    double v = 0.0;
+#pragma unroll
+                    for (int mm = 0; mm < SEP_NZ; mm++) v = fma(ri[mm], wj[mm], v);
+                    K[S6::idx(i, j)] = (ai && j < k) ? v : (i == j ? 1.0 : 0.0);
+                }
+            }
+            if (!chol_packed<POL_K>(K, dk)) return 0;
+            chol_solve<POL_K>(K, dk, c, rho);
+            // primal direction z = P^-1 (n_p - N_A r), n = sign * g
+            double z[SEP_NZ];
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) z[j] = sp * wp[j];
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) {
+                if (i < k) {
+                    const double* wi = pol + i * 16 + POL_W;
+#pragma unroll
+                    for (int j = 0; j < SEP_NZ; j++) z[j] = fma(-rho[i], wi[j], z[j]);
+                }
+            }
+            double zn = 0.0, nw = 0.0, vp = 0.0;
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) {
+                zn = fma(gp[j], z[j], zn);
+                nw = fma(gp[j], wp[j], nw);
+                vp = fma(gp[j], y[j], vp);
+            }
+            zn *= sp;
+            vp = sp * (vp - bp);
+            // dual step: the first active multiplier to reach zero
+            double t1 = 1e300;
+            int l = -1;
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) {
+                const double r = sgn[i] * rho[i];
+                if (i < k && r > 0.0) {
+                    const double ti = u[i] / r;
+                    if (ti < t1) t1 = ti, l = i;
+                }
+            }
+            const bool full = zn > 1e-10 * nw;  // else n_p lies in the span of the active sides
+            const double t2 = full ? vp / zn : 1e300;
+            if (l < 0 && !full) {
+#pragma unroll
+                for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
+                wave_lds_sync();
+                return -1;
+            }
+            const double t = fmin(t1, t2);
+            if (full) {
+#pragma unroll
+                for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-t, z[j], y[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < POL_K; i++)
+                if (i < k) u[i] = fma(-t, sgn[i] * rho[i], u[i]);
+            up += t;
+            wave_lds_sync();  // every lane has read the rows it is about to move
+            if (t2 <= t1) {  // the candidate joins the active set
+                if (k == POL_K) return 0;
+                pol[k * 16 + gl] = cand[gl];
+#pragma unroll
+                for (int i = 0; i < POL_K; i++) u[i] = i == k ? up : u[i];
+                k++;
+                wave_lds_sync();
+                break;
+            }
+            // side l leaves: the rows above it move down (one column per lane)
+#pragma unroll
+            for (int i = 0; i < POL_K - 1; i++)
+                if (i >= l && i < k - 1) pol[i * 16 + gl] = pol[(i + 1) * 16 + gl];
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) u[i] = i >= l ? (i + 1 < POL_K ? u[i + 1] : 0.0) : u[i];
+            k--;
+            wave_lds_sync();
+        }
+    }
+    return sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm) ? 1 : 0;
 }
 
 // P: 6x6 row-major block-diagonal reduced Hessian, LP its lower Cholesky factor (uniform).
@@ -273,6 +523,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
     // duals, both floored at delta (complementarity >= delta^2), CBF rows centred at delta^2
     const bool use_warm = warm != nullptr && warm_delta > 0.0;
     const double wd = warm_delta, wd2 = warm_delta * warm_delta;
+    int as_steps = 0;  // dual active-set steps before the PDIP (counted in iters)
     // ---- start: unconstrained minimiser (block-diagonal P: per-channel 2x2 solves). When it
     // satisfies every row it is the optimum (convex QP, all multipliers zero; slack mode: v = 0
     // since its cost is positive): no Newton step needed.
@@ -327,6 +578,28 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             fo.rp = 0.0;
             fo.rd = rdn / (1.0 + qn0);
             return fo;
+        }
+        // dual active-set solve (PdipCfg::dual_as): the PDIP below runs only when it gives up
+        if constexpr (!SLACK) {
+            if (cfg.dual_as > 0 && pol != nullptr) {
+                double yg[SEP_NZ], rpg = 0.0, rdg = 0.0;
+                const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
+                                                     rdg, as_steps, warm);
+                if (r != 0) {
+                    PdipOut fo{r > 0 ? ST_OPTIMAL : ST_UNKNOWN, as_steps};
+#pragma unroll
+                    for (int j = 0; j < SEP_NZ; j++) y[j] = yg[j];
+                    if (r > 0) {
+                        fo.rp = rpg;
+                        fo.rd = rdg;
+                        fo.polished = true;
+                    } else {
+                        fo.early = true;  // no feasible point in sight: phase 1 decides
+                    }
+                    return fo;
+                }
+                wave_lds_sync();  // the scratch is reused by the polish
+            }
         }
         if (!use_warm) {
 #pragma unroll
@@ -554,7 +827,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             rd_track = rdn * inv_qn;
             rd_exact = false;
         }
-        out.iters = it;
+        out.iters = as_steps + it;
         const bool finite = isfinite(rp) && isfinite(rd_track) && isfinite(mu) && isfinite(acc[0]);
         // exact dual residual (relative), group-uniform
         auto exact_rd = [&]() {
@@ -619,12 +892,12 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         // active-set finish (sep_polish) once mu has fallen 1000x, then after every further 100x
         if constexpr (!SLACK) {
             if (pol != nullptr && finite && it > 0 && mu <= polish_mu) {
-                double rpp = 0.0;
+                double rpp = 0.0, rdp = 0.0;
                 if (sep_polish<G, SB, CB>(rw, has_cbf, P, q, sl, su, zl, zu, cs, cz, pl, pu, pc, cfg.tol, pol, y,
-                                          rpp, warm)) {
+                                          rpp, rdp, warm)) {
                     out.status = ST_OPTIMAL;
                     out.rp = rpp;
-                    out.rd = 0.0;
+                    out.rd = rdp;
                     out.polished = true;
                     break;
                 }

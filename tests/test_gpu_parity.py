@@ -528,12 +528,14 @@ def test_grid_bucket_overflow_falls_back_to_full_scan(mpclib):
 
 
 @pytest.mark.parametrize("scale", [0.55, 0.42, 0.3])
-def test_iteration1_warm_start_matches_cold_start(mpclib, scale):
+def test_iteration1_warm_start_matches_cold_start(mpclib, scale, monkeypatch):
     """IMPC iteration 1 warm-started from iteration 0's primal-dual point (the default,
     mpccbf_options.warm_delta = 0 -> 0.3) and cold-started (warm_delta < 0) reach the same
     optima: statuses equal (also on the very crowded 0.3 lattice, where breakdowns and infeasible
-    QPs occur), objectives within solver tolerance; the warm start saves Newton steps."""
+    QPs occur), objectives within solver tolerance; the warm start saves Newton steps. The PDIP
+    path alone (dual active-set solve off), which is the one the warm start feeds."""
     torch = _torch()
+    monkeypatch.setenv("MPCCBF_DUAL_AS", "0")
     cfg = swarm.config(15)
     states, targets = swarm.lattice_swarm(1024, seed=5)
     states[:, :2] *= scale
@@ -551,6 +553,36 @@ def test_iteration1_warm_start_matches_cold_start(mpclib, scale):
     hard = ok[:, 1] & (cold["iters"][:, 1] > 0)  # QPs the fast start does not settle
     if scale > 0.4:
         assert warm["iters"][hard, 1].mean() < cold["iters"][hard, 1].mean()
+
+
+@pytest.mark.parametrize("scale", [0.3, 0.45, 0.55, 1.0])
+def test_dual_active_set_matches_pdip(mpclib, scale, monkeypatch):
+    """The dual active-set solve (default first attempt) and the PDIP alone (MPCCBF_DUAL_AS=0)
+    give the same statuses — INFEASIBLE included: a QP the active-set method finds unreachable is
+    certified by phase 1 as before — and the same optima to the PDIP's tolerance; the active-set
+    solve takes fewer steps than the PDIP takes Newton steps on the QPs the fast start does not
+    settle."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(1024, seed=5)
+    states[:, :2] *= scale
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    monkeypatch.setenv("MPCCBF_DUAL_AS", "0")
+    pdip = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    monkeypatch.delenv("MPCCBF_DUAL_AS")
+    das = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    np.testing.assert_array_equal(pdip["status"], das["status"])
+    ok = pdip["status"] == 0
+    if scale < 0.4:  # very crowded: mostly infeasible QPs; statuses are the check
+        assert (pdip["status"][:, 0] == 3).sum() > 100
+        return
+    assert ok[:, 0].sum() > 100
+    err = np.abs(pdip["obj"][ok] - das["obj"][ok]) / np.maximum(1.0, np.abs(pdip["obj"][ok]))
+    assert err.max() <= 1e-7, err.max()
+    assert np.nanmax(np.abs(pdip["x"] - das["x"])) <= 1e-5
+    hard = ok[:, 0] & (pdip["iters"][:, 0] > 0)
+    if hard.sum() > 10:
+        assert das["iters"][hard, 0].mean() < pdip["iters"][hard, 0].mean()
 
 
 def test_invalid_warm_delta_env_rejected(mpclib, monkeypatch):
