@@ -315,22 +315,59 @@ __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double
     return sep_eqp_finish<G, SB, CB, false>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm);
 }
 
+// K = G_A P^-1 G_A^T of the k staged rows of pol (packed upper, identity beyond k)
+template <int NR>
+__device__ __forceinline__ void sep_gram(const double* __restrict__ pol, int k, double (&K)[Sym<NR>::P]) {
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        const double* ri = pol + (i < k ? i : 0) * 16;
+#pragma unroll
+        for (int j = i; j < NR; j++) {
+            const double* wj = pol + (j < k ? j : 0) * 16 + POL_W;
+            double v = 0.0;
+#pragma unroll
+            for (int m = 0; m < SEP_NZ; m++) v = fma(ri[m], wj[m], v);
+            K[Sym<NR>::idx(i, j)] = (i < k && j < k) ? v : (i == j ? 1.0 : 0.0);
+        }
+    }
+}
+
 // Dual active-set solve (Goldfarb & Idnani's method, range-space form) from the unconstrained
 // minimiser yu: the most violated side (scaled as the primal residual) is the candidate; the
 // direction z that keeps the active sides exact moves y onto it unless an active multiplier
 // reaches zero first, in which case that side leaves and the step is retried. Every step keeps
-// the iterate dual feasible and raises the objective, and costs one k x k factorisation (k <= 6,
-// rows in pol, the candidate in row POL_K). The converged active set's EQP is verified by
-// sep_eqp_finish. Returns 1: optimal (yo, residuals, warm duals set); -1: no step reaches the
-// candidate (its side is a combination of the active ones and no multiplier can leave: no
-// feasible point, phase 1 decides; yo = last iterate); 0: gave up (step limit, breakdown, or the
-// verification failed) — the PDIP solves the QP.
+// the iterate dual feasible and raises the objective. The Cholesky factor L of
+// K = G_A P^-1 G_A^T (k <= 6 active rows staged in pol, the candidate in row POL_K) stays in
+// registers: a step costs one forward and one backward substitution with the candidate's column
+// c = G_A P^-1 g_p, and when the candidate joins, L^-1 c is L's new row and the Schur complement
+// g_p P^-1 g_p - |L^-1 c|^2 its squared diagonal; a leaving side refactors K. Converged (no side
+// violated beyond tol / 10), the iterate is returned when its dual residual meets tol (the
+// updates hold stationarity up to rounding), else the active set's EQP (sep_eqp_finish) re-solves
+// it. Returns 1: optimal (yo, residuals, warm duals set); -1: no step reaches the candidate (its
+// side is a combination of the active ones and no multiplier can leave: no feasible point, phase
+// 1 decides; yo = last iterate); 0: gave up (step limit, breakdown, failed verification) — the
+// PDIP solves the QP.
+#ifdef MPCCBF_PDIP_STAMPS  // profiling build: shader-clock stamps of the first solve's first steps
+#define GSTAMP(k, cond)                                                              \
+    do {                                                                             \
+        if (dbg && (cond)) dbg[k] = (long long)__builtin_amdgcn_s_memtime();         \
+    } while (0)
+#else
+#define GSTAMP(k, cond) \
+    do {                \
+    } while (0)
+#endif
 template <int G, int SB, int CB>
 __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                            const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
                            double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
-                           int& steps, SepWarm<SB>* warm) {
+                           int& steps, SepWarm<SB>* warm, long long* dbg = nullptr) {
     static_assert(G == 16, "rows of pol are copied one column per lane");
+    (void)dbg;
+    GSTAMP(0, true);
+#ifdef MPCCBF_PDIP_STAMPS
+    if (dbg) dbg[15] = 1;
+#endif
     const int gl = threadIdx.x & (G - 1);
     double pi[SEP_D][3];
     sep_pinv(P, pi);
@@ -357,7 +394,18 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     steps = 0;
     const double add_tol = 0.1 * tol;
     double* cand = pol + POL_K * 16;
-    for (;;) {
+    using S6 = Sym<POL_K>;
+    double L[S6::P], dl[POL_K];  // chol_packed layout of K's factor (identity beyond k), 1 / diagonal
+#pragma unroll
+    for (int i = 0; i < POL_K; i++) {
+        dl[i] = 1.0;
+#pragma unroll
+        for (int j = i; j < POL_K; j++) L[S6::idx(i, j)] = i == j ? 1.0 : 0.0;
+    }
+    double m = 0.0;
+    GSTAMP(1, true);
+    for (int outer = 0;; outer++) {
+        (void)outer;
         // the most violated side of the group (lowest lane on ties)
         double vb = -1.0;
         int sb = 0;
@@ -386,66 +434,55 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 }
             }
         }
-        const double m = grp_max<G>(vb);
+        m = grp_max<G>(vb);
+        GSTAMP(2 + 6 * outer, outer < 2);
         if (!(m > add_tol)) break;
         if (steps >= maxstep) return 0;
         const int owner = __ffsll((long long)grp_ballot<G>(vb == m)) - 1;
         if (gl == owner) sep_stage_side<SB, CB>(rw, pi, sb, gl, cand);
         wave_lds_sync();
+        GSTAMP(3, outer == 0);
         double up = 0.0;  // the candidate's multiplier
         for (;;) {
             if (++steps > maxstep) return 0;
-            double gp[SEP_NZ], wp[SEP_NZ];
+            double gp[SEP_NZ];
 #pragma unroll
-            for (int j = 0; j < SEP_NZ; j++) {
-                gp[j] = cand[j];
-                wp[j] = cand[POL_W + j];
-            }
-            const double bp = cand[POL_B], sp = cand[POL_SGN];
-            // rho = (G_A P^-1 G_A^T)^-1 G_A P^-1 g_p: the active multipliers' change per unit step
-            using S6 = Sym<POL_K>;
-            double K[S6::P], c[POL_K], dk[POL_K], rho[POL_K], sgn[POL_K];
+            for (int j = 0; j < SEP_NZ; j++) gp[j] = cand[j];
+            const double sp = cand[POL_SGN];
+            // v = L^-1 (sp c), c_i = g_i P^-1 g_p: the forward substitution fused with the dots
+            double v[POL_K], sgn[POL_K];
 #pragma unroll
             for (int i = 0; i < POL_K; i++) {
-                const bool ai = i < k;
-                const double* ri = pol + (ai ? i : 0) * 16;
+                const double* ri = pol + (i < k ? i : 0) * 16;
                 double t = 0.0;
 #pragma unroll
-                for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], wp[j], t);
-                c[i] = ai ? sp * t : 0.0;
+                for (int j = 0; j < SEP_NZ; j++) t = fma(ri[POL_W + j], gp[j], t);
                 sgn[i] = ri[POL_SGN];
+                double s = i < k ? sp * t : 0.0;
 #pragma unroll
-                for (int j = i; j < POL_K; j++) {
-                    const double* wj = pol + (j < k ? j : 0) * 16 + POL_W;
-                    double v = 0.0;
-#pragma unroll
-                    for (int mm = 0; mm < SEP_NZ; mm++) v = fma(ri[mm], wj[mm], v);
-                    K[S6::idx(i, j)] = (ai && j < k) ? v : (i == j ? 1.0 : 0.0);
-                }
+                for (int mm = 0; mm < i; mm++) s = fma(-L[S6::idx(mm, i)], v[mm], s);
+                v[i] = s * dl[i];
             }
-            if (!chol_packed<POL_K>(K, dk)) return 0;
-            chol_solve<POL_K>(K, dk, c, rho);
-            // primal direction z = P^-1 (n_p - N_A r), n = sign * g
-            double z[SEP_NZ];
+            // rho = L^-T v = K^-1 G_A P^-1 n_p: the active multipliers' change per unit step
+            double rho[POL_K];
 #pragma unroll
-            for (int j = 0; j < SEP_NZ; j++) z[j] = sp * wp[j];
+            for (int i = POL_K - 1; i >= 0; i--) {
+                double s = v[i];
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) {
-                if (i < k) {
-                    const double* wi = pol + i * 16 + POL_W;
-#pragma unroll
-                    for (int j = 0; j < SEP_NZ; j++) z[j] = fma(-rho[i], wi[j], z[j]);
-                }
+                for (int mm = i + 1; mm < POL_K; mm++) s = fma(-L[S6::idx(i, mm)], rho[mm], s);
+                rho[i] = s * dl[i];
             }
-            double zn = 0.0, nw = 0.0, vp = 0.0;
+            GSTAMP(4, outer == 0);
+            double nw = 0.0, vv = 0.0, vp = 0.0;
 #pragma unroll
             for (int j = 0; j < SEP_NZ; j++) {
-                zn = fma(gp[j], z[j], zn);
-                nw = fma(gp[j], wp[j], nw);
+                nw = fma(gp[j], cand[POL_W + j], nw);
                 vp = fma(gp[j], y[j], vp);
             }
-            zn *= sp;
-            vp = sp * (vp - bp);
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) vv = fma(v[i], v[i], vv);
+            const double zn = nw - vv;  // n_p z: the Schur complement of K in [K c; c^T nw]
+            vp = sp * (vp - cand[POL_B]);
             // dual step: the first active multiplier to reach zero
             double t1 = 1e300;
             int l = -1;
@@ -453,12 +490,12 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             for (int i = 0; i < POL_K; i++) {
                 const double r = sgn[i] * rho[i];
                 if (i < k && r > 0.0) {
-                    const double ti = u[i] / r;
+                    const double ti = u[i] * rcp(r);
                     if (ti < t1) t1 = ti, l = i;
                 }
             }
             const bool full = zn > 1e-10 * nw;  // else n_p lies in the span of the active sides
-            const double t2 = full ? vp / zn : 1e300;
+            const double t2 = full ? vp * rcp(zn) : 1e300;
             if (l < 0 && !full) {
 #pragma unroll
                 for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
@@ -467,24 +504,42 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             }
             const double t = fmin(t1, t2);
             if (full) {
+                // primal direction z = P^-1 (n_p - N_A r), n = sign * g (rows re-read: the
+                // compiler barrier keeps them from staying live across the substitutions)
+                asm volatile("" ::: "memory");
 #pragma unroll
-                for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-t, z[j], y[j]);
+                for (int j = 0; j < SEP_NZ; j++) {
+                    double zj = sp * cand[POL_W + j];
+#pragma unroll
+                    for (int i = 0; i < POL_K; i++)
+                        if (i < k) zj = fma(-rho[i], pol[i * 16 + POL_W + j], zj);
+                    y[j] = fma(-t, zj, y[j]);
+                }
             }
 #pragma unroll
             for (int i = 0; i < POL_K; i++)
                 if (i < k) u[i] = fma(-t, sgn[i] * rho[i], u[i]);
             up += t;
             wave_lds_sync();  // every lane has read the rows it is about to move
-            if (t2 <= t1) {  // the candidate joins the active set
+            GSTAMP(5, outer == 0);
+            if (t2 <= t1) {  // the candidate joins: L gains the row L^-1 c, diagonal sqrt(zn)
                 if (k == POL_K) return 0;
                 pol[k * 16 + gl] = cand[gl];
+                const double rz = rsqrt(zn);
 #pragma unroll
-                for (int i = 0; i < POL_K; i++) u[i] = i == k ? up : u[i];
+                for (int i = 0; i < POL_K; i++) {
+                    u[i] = i == k ? up : u[i];
+                    dl[i] = i == k ? rz : dl[i];
+#pragma unroll
+                    for (int j = i; j < POL_K; j++)
+                        if (j == k) L[S6::idx(i, j)] = i < k ? sp * v[i] : (i == k ? zn * rz : L[S6::idx(i, j)]);
+                }
                 k++;
                 wave_lds_sync();
+                GSTAMP(6, outer == 0);
                 break;
             }
-            // side l leaves: the rows above it move down (one column per lane)
+            // side l leaves: the rows above it move down (one column per lane); K refactored
 #pragma unroll
             for (int i = 0; i < POL_K - 1; i++)
                 if (i >= l && i < k - 1) pol[i * 16 + gl] = pol[(i + 1) * 16 + gl];
@@ -492,9 +547,56 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             for (int i = 0; i < POL_K; i++) u[i] = i >= l ? (i + 1 < POL_K ? u[i + 1] : 0.0) : u[i];
             k--;
             wave_lds_sync();
+            sep_gram<POL_K>(pol, k, L);
+            if (!chol_packed<POL_K>(L, dl)) return 0;
         }
     }
-    return sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm) ? 1 : 0;
+    // converged: primal residual = the last scan's worst violation; the iterate's dual residual
+    // P y + q + G_A^T lam (lam = sign * u)
+    double rd = 0.0, qn = 0.0;
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int o = 2 * d + h;
+            double r = fma(P[o * 6 + 2 * d], y[2 * d], fma(P[o * 6 + 2 * d + 1], y[2 * d + 1], q[o]));
+#pragma unroll
+            for (int i = 0; i < POL_K; i++)
+                if (i < k) r = fma(pol[i * 16 + POL_SGN] * u[i], pol[i * 16 + o], r);
+            rd = fmax(rd, fabs(r));
+            qn = fmax(qn, fabs(q[o]));
+        }
+    }
+    rd *= rcp(1.0 + qn);
+    GSTAMP(9, true);
+    if (!(rd <= tol))
+        return sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm) ? 1 : 0;
+#pragma unroll
+    for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
+    rp_out = fmax(m, 0.0);
+    rd_out = rd;
+    if (warm != nullptr) {  // the multipliers as the next warm start's box duals
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int kk = 0; kk < SB; kk++) {
+                const double il = (double)((2 * (d * SB + kk)) * 16 + gl), iu = il + 16.0;
+                double ml = 0.0, mu = 0.0;
+#pragma unroll
+                for (int i = 0; i < POL_K; i++) {
+                    if (i < k) {
+                        const double id = pol[i * 16 + POL_ID];
+                        ml = id == il ? u[i] : ml;
+                        mu = id == iu ? u[i] : mu;
+                    }
+                }
+                warm->zl(d, kk) = ml;
+                warm->zu(d, kk) = mu;
+            }
+    }
+    wave_lds_sync();  // the scratch is reused
+    GSTAMP(10, true);
+    return 1;
 }
 
 // P: 6x6 row-major block-diagonal reduced Hessian, LP its lower Cholesky factor (uniform).
@@ -516,6 +618,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                                   double* pol = nullptr) {
     (void)dbg;
     const bool slk = SLACK && has_cbf;  // group-uniform
+    GSTAMP(12, true);
     // slack variable, its bound's slack and dual; the dual starts at the linear cost it carries at
     // the optimum (w = sum_rows z + z_bound with inactive rows)
     double v = 1.0, sb = 1.0, zb = SLACK ? fmax(wv_cost, 1.0) : 1.0;
@@ -580,11 +683,12 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             return fo;
         }
         // dual active-set solve (PdipCfg::dual_as): the PDIP below runs only when it gives up
+        GSTAMP(13, true);
         if constexpr (!SLACK) {
             if (cfg.dual_as > 0 && pol != nullptr) {
                 double yg[SEP_NZ], rpg = 0.0, rdg = 0.0;
                 const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
-                                                     rdg, as_steps, warm);
+                                                     rdg, as_steps, warm, dbg);
                 if (r != 0) {
                     PdipOut fo{r > 0 ? ST_OPTIMAL : ST_UNKNOWN, as_steps};
 #pragma unroll

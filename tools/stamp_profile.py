@@ -70,6 +70,21 @@ for v in VARIANTS:
         for k, name in enumerate(PPH_FOV if FOV else PPH):
             print(f"   {name:15s} mean {d[:, k].mean():7.0f}  p50 {np.median(d[:, k]):7.0f} cycles"
                   + (f"   critical agent {dc[k]:7.0f}" if dc is not None else ""))
+    if PDIP and v == 0 and not FOV:  # dual active-set stamps (solve 0, first steps)
+        ps = allst[N * 8:].reshape(N, 16).astype(np.float64)
+        its0 = out["iters"].cpu().numpy()[:, 0]
+        names = [("fast-start test", 12, 13), ("call", 13, 0), ("init", 0, 1), ("scan 1", 1, 2),
+                 ("stage", 2, 3), ("substitutions", 3, 4), ("step+update", 4, 5), ("add", 5, 6),
+                 ("scan 2", 6, 8), ("dual residual", 8, 9), ("warm+exit", 9, 10)]
+        for nstep in (1, 2):
+            m = (ps[:, 15] == 1) & (its0 == nstep) & (ps[:, 10] > 0)
+            if m.sum() == 0:
+                continue
+            print(f"variant {v}: dual active-set solves with {nstep} step(s): {m.sum()} agents, "
+                  f"cycles entry->exit mean {np.mean(ps[m, 10] - ps[m, 12]):.0f}")
+            for name, a, b in names:
+                d = ps[m, b] - ps[m, a]
+                print(f"   {name:15s} mean {d.mean():7.0f}  p50 {np.median(d):7.0f} cycles")
     status = out["status"].cpu().numpy()
     t0 = s[:, 0].min()
     start = s[:, 0] - t0
