@@ -316,6 +316,16 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
                 r[9] = o.hi[i];
             }
             pack(v, d.o_Gsep, B);
+            std::vector<double> Pi((size_t)DIM * 3, 0.0);  // [[a b] [b c]]^-1 per channel
+            for (int dd = 0; dd < DIM; dd++) {
+                const int r0 = dd * o.nzd;
+                const double a = o.Pr(r0, r0), b = o.Pr(r0, r0 + 1), cc = o.Pr(r0 + 1, r0 + 1);
+                const double det = a * cc - b * b;
+                Pi[dd * 3 + 0] = cc / det;
+                Pi[dd * 3 + 1] = -b / det;
+                Pi[dd * 3 + 2] = a / det;
+            }
+            pack(v, d.o_Pinv, Pi);
             d.sep = 1;
             d.nzd = o.nzd;
             d.sep_rows_per_dim = rpd;

@@ -23,6 +23,7 @@ struct DevOps {
     // [g0, g1, Gs(6), lo, hi] (SEP_ROW doubles), 16 rows per channel (unused: inert g = 0, [-1, 1])
     int32_t sep, nzd, sep_rows_per_dim;
     int32_t o_Gsep;
+    int32_t o_Pinv;  // separable layout: per-channel inverse 2x2 blocks of Pr, (a, b, c) x 3
     // FoV controller (cbf_mode 1, impc_fov_kernel): Voronoi operators VZ (C x 2 x nz), VS (C x 2 x 6),
     // box rows as dense 16-wide rows [g(16) | Gs(6) | lo | hi] (WBOX_ROW doubles), P and its
     // Cholesky factor padded to 16 x 16 with the identity

@@ -388,7 +388,8 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
             // violation above the tolerance, from the failed solve's last iterate), so an
             // infeasible QP needs no retry and statuses never depend on the first attempt's
             // warm start or divergence test.
-            const bool warm_try = it > 0 && warm_delta > 0.0;
+            // (with the dual active-set solve first, the PDIP runs cold: no warm-start duals kept)
+            const bool warm_try = it > 0 && warm_delta > 0.0 && op.dual_as <= 0;
             int tr_warm = 0, tr_cold = 0, tr_p1 = 0;  // diagnostics (MPCCBF_SOLVE_TRACE)
             int attempt = 0, total = 0;
             bool certified = false, infeas = false;
@@ -400,7 +401,8 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 ca.fast_start = op.fast_start != 0;
                 ca.robust = attempt == 2;
                 ca.dual_as = attempt == 0 ? op.dual_as : 0;
-                po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_LPr), q, y,
+                ca.want_rd = args.dual_res != nullptr;
+                po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_Pinv), q, y,
                                                       ca, dbg, wslack, &vslack, red, &warm,
                                                       (attempt == 0 && warm_try) ? warm_delta : 0.0,
                                                       SLACK ? nullptr : stage);

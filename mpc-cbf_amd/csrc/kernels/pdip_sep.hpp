@@ -86,17 +86,13 @@ constexpr int POL_K = 6;
 // staged row (16 doubles): g (6) | b | side sign (+1 upper, -1 lower) | P^-1 g (6) | side id | -
 constexpr int POL_B = 6, POL_SGN = 7, POL_W = 8, POL_ID = 14;
 
-// inverse of P's 2x2 channel blocks: pi[d] = (a, b, c) of [[a b] [b c]]
-__device__ __forceinline__ void sep_pinv(const double* __restrict__ P, double (&pi)[SEP_D][3]) {
+// inverse of P's 2x2 channel blocks (DevOps::o_Pinv, computed on the host): pi[d] = (a, b, c)
+// of [[a b] [b c]]
+__device__ __forceinline__ void sep_pinv(const double* __restrict__ Pinv, double (&pi)[SEP_D][3]) {
 #pragma unroll
-    for (int d = 0; d < SEP_D; d++) {
-        const int o = 2 * d;
-        const double a = P[o * 6 + o], b = P[o * 6 + o + 1], c = P[(o + 1) * 6 + o + 1];
-        const double r = rcp(fma(a, c, -b * b));
-        pi[d][0] = c * r;
-        pi[d][1] = -b * r;
-        pi[d][2] = a * r;
-    }
+    for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+        for (int e = 0; e < 3; e++) pi[d][e] = Pinv[d * 3 + e];
 }
 
 // Side s of this lane (s = 2 (d SB + kk) + upper for the box rows, 2 SEP_D SB + c for the CBF
@@ -177,18 +173,16 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
 #pragma unroll
-    for (int i = 0; i < POL_K; i++) {
-        if (i < k) {
-            const double* wi = pol + i * 16 + POL_W;
+    for (int i = 0; i < POL_K; i++) {  // (lam_i = 0 beyond k: the padded rows read row 0)
+        const double* wi = pol + (i < k ? i : 0) * 16 + POL_W;
 #pragma unroll
-            for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-lam[i], wi[j], y[j]);
-            lmax = fmax(lmax, fabs(lam[i]));
-        }
+        for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-lam[i], wi[j], y[j]);
+        lmax = fmax(lmax, fabs(lam[i]));
     }
     bool bad = !okf;
 #pragma unroll
     for (int i = 0; i < POL_K; i++)
-        if (i < k) bad = bad || !(pol[i * 16 + POL_SGN] * lam[i] >= -1e-9 * (1.0 + lmax));
+        bad = bad || (i < k && !(pol[(i < k ? i : 0) * 16 + POL_SGN] * lam[i] >= -1e-9 * (1.0 + lmax)));
     // every row at y (scaled violation, as the PDIP's primal residual)
     double rp = 0.0;
 #pragma unroll
@@ -219,8 +213,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
                 const int o = 2 * d + h;
                 double v = fma(P[o * 6 + 2 * d], y[2 * d], fma(P[o * 6 + 2 * d + 1], y[2 * d + 1], q[o]));
 #pragma unroll
-                for (int i = 0; i < POL_K; i++)
-                    if (i < k) v = fma(lam[i], pol[i * 16 + o], v);
+                for (int i = 0; i < POL_K; i++) v = fma(lam[i], pol[(i < k ? i : 0) * 16 + o], v);
                 rd = fmax(rd, fabs(v));
                 qn = fmax(qn, fabs(q[o]));
             }
@@ -238,11 +231,9 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
                     double ml = 0.0, mu = 0.0;
 #pragma unroll
                     for (int i = 0; i < POL_K; i++) {
-                        if (i < k) {
-                            const double id = pol[i * 16 + POL_ID];
-                            ml = id == il ? -lam[i] : ml;
-                            mu = id == iu ? lam[i] : mu;
-                        }
+                        const double id = i < k ? pol[(i < k ? i : 0) * 16 + POL_ID] : -1.0;
+                        ml = id == il ? -lam[i] : ml;
+                        mu = id == iu ? lam[i] : mu;
                     }
                     warm->zl(d, kk) = fmax(ml, 0.0);
                     warm->zu(d, kk) = fmax(mu, 0.0);
@@ -257,7 +248,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
 // are at most 6 of them.
 template <int G, int SB, int CB>
 __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
-                           const double (&q)[SEP_NZ], const double (&sl)[SEP_D][SB],
+                           const double* __restrict__ Pinv, const double (&q)[SEP_NZ], const double (&sl)[SEP_D][SB],
                            const double (&su)[SEP_D][SB], const double (&zl)[SEP_D][SB],
                            const double (&zu)[SEP_D][SB], const double (&cs)[CB], const double (&cz)[CB],
                            const double (&pl)[SEP_D][SB], const double (&pu)[SEP_D][SB],
@@ -265,7 +256,7 @@ __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double
                            double (&yo)[SEP_NZ], double& rp_out, double& rd_out, SepWarm<SB>* warm) {
     const int gl = threadIdx.x & (G - 1);
     double pi[SEP_D][3], yu[SEP_NZ];
-    sep_pinv(P, pi);
+    sep_pinv(Pinv, pi);
 #pragma unroll
     for (int d = 0; d < SEP_D; d++) {
         const int o = 2 * d;
@@ -359,9 +350,9 @@ __device__ __forceinline__ void sep_gram(const double* __restrict__ pol, int k, 
 #endif
 template <int G, int SB, int CB>
 __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
-                           const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
+                           const double* __restrict__ Pinv, const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
                            double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
-                           int& steps, SepWarm<SB>* warm, long long* dbg = nullptr) {
+                           int& steps, SepWarm<SB>* warm, bool want_rd, long long* dbg = nullptr) {
     static_assert(G == 16, "rows of pol are copied one column per lane");
     (void)dbg;
     GSTAMP(0, true);
@@ -370,7 +361,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #endif
     const int gl = threadIdx.x & (G - 1);
     double pi[SEP_D][3];
-    sep_pinv(P, pi);
+    sep_pinv(Pinv, pi);
     constexpr int NS = 2 * SEP_D * SB + CB;
     double sc[NS];  // violation scale 1 / (1 + |bound|) per side
     {
@@ -483,17 +474,19 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             for (int i = 0; i < POL_K; i++) vv = fma(v[i], v[i], vv);
             const double zn = nw - vv;  // n_p z: the Schur complement of K in [K c; c^T nw]
             vp = sp * (vp - cand[POL_B]);
-            // dual step: the first active multiplier to reach zero
-            double t1 = 1e300;
+            // dual step: the first active multiplier to reach zero (smallest u_i / r_i, compared
+            // by cross products: one reciprocal)
+            double un = 1.0, rn = 0.0;  // (un / rn = +inf until a blocking multiplier is found)
             int l = -1;
 #pragma unroll
             for (int i = 0; i < POL_K; i++) {
                 const double r = sgn[i] * rho[i];
-                if (i < k && r > 0.0) {
-                    const double ti = u[i] * rcp(r);
-                    if (ti < t1) t1 = ti, l = i;
-                }
+                const bool better = i < k && r > 0.0 && u[i] * rn < un * r;
+                un = better ? u[i] : un;
+                rn = better ? r : rn;
+                l = better ? i : l;
             }
+            const double t1 = l >= 0 ? un * rcp(rn) : 1e300;
             const bool full = zn > 1e-10 * nw;  // else n_p lies in the span of the active sides
             const double t2 = full ? vp * rcp(zn) : 1e300;
             if (l < 0 && !full) {
@@ -506,19 +499,24 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             if (full) {
                 // primal direction z = P^-1 (n_p - N_A r), n = sign * g (rows re-read: the
                 // compiler barrier keeps them from staying live across the substitutions)
+                // (loads never under a condition: inactive rows read row 0 and weigh 0)
                 asm volatile("" ::: "memory");
+                double z[SEP_NZ];
 #pragma unroll
-                for (int j = 0; j < SEP_NZ; j++) {
-                    double zj = sp * cand[POL_W + j];
+                for (int j = 0; j < SEP_NZ; j++) z[j] = sp * cand[POL_W + j];
 #pragma unroll
-                    for (int i = 0; i < POL_K; i++)
-                        if (i < k) zj = fma(-rho[i], pol[i * 16 + POL_W + j], zj);
-                    y[j] = fma(-t, zj, y[j]);
+                for (int i = 0; i < POL_K; i++) {
+                    const double* wi = pol + (i < k ? i : 0) * 16 + POL_W;
+                    const double ri = i < k ? rho[i] : 0.0;
+#pragma unroll
+                    for (int j = 0; j < SEP_NZ; j++) z[j] = fma(-ri, wi[j], z[j]);
                 }
+#pragma unroll
+                for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-t, z[j], y[j]);
             }
 #pragma unroll
             for (int i = 0; i < POL_K; i++)
-                if (i < k) u[i] = fma(-t, sgn[i] * rho[i], u[i]);
+                u[i] = i < k ? fma(-t, sgn[i] * rho[i], u[i]) : u[i];
             up += t;
             wave_lds_sync();  // every lane has read the rows it is about to move
             GSTAMP(5, outer == 0);
@@ -552,17 +550,20 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         }
     }
     // converged: primal residual = the last scan's worst violation; the iterate's dual residual
-    // P y + q + G_A^T lam (lam = sign * u)
+    // P y + q + G_A^T lam (lam = sign * u) when it is reported (want_rd): the updates hold
+    // stationarity by construction, so the check only guards against rounding
     double rd = 0.0, qn = 0.0;
 #pragma unroll
-    for (int d = 0; d < SEP_D; d++) {
+    for (int d = 0; d < (want_rd ? SEP_D : 0); d++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int o = 2 * d + h;
             double r = fma(P[o * 6 + 2 * d], y[2 * d], fma(P[o * 6 + 2 * d + 1], y[2 * d + 1], q[o]));
 #pragma unroll
-            for (int i = 0; i < POL_K; i++)
-                if (i < k) r = fma(pol[i * 16 + POL_SGN] * u[i], pol[i * 16 + o], r);
+            for (int i = 0; i < POL_K; i++) {
+                const double* ri = pol + (i < k ? i : 0) * 16;
+                r = fma(i < k ? ri[POL_SGN] * u[i] : 0.0, ri[o], r);
+            }
             rd = fmax(rd, fabs(r));
             qn = fmax(qn, fabs(q[o]));
         }
@@ -584,11 +585,9 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 double ml = 0.0, mu = 0.0;
 #pragma unroll
                 for (int i = 0; i < POL_K; i++) {
-                    if (i < k) {
-                        const double id = pol[i * 16 + POL_ID];
-                        ml = id == il ? u[i] : ml;
-                        mu = id == iu ? u[i] : mu;
-                    }
+                    const double id = i < k ? pol[(i < k ? i : 0) * 16 + POL_ID] : -1.0;
+                    ml = id == il ? u[i] : ml;
+                    mu = id == iu ? u[i] : mu;
                 }
                 warm->zl(d, kk) = ml;
                 warm->zu(d, kk) = mu;
@@ -599,7 +598,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     return 1;
 }
 
-// P: 6x6 row-major block-diagonal reduced Hessian, LP its lower Cholesky factor (uniform).
+// P: 6x6 row-major block-diagonal reduced Hessian, Pinv its per-channel inverse blocks (uniform).
 // has_cbf: group-uniform flag (some CBF slot of the group is live); when false the CBF slots
 // are skipped entirely (and do not count as sides).
 //
@@ -611,7 +610,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 // and dv = (rhs_v - u^T dy) / d is recovered lane-locally after each solve.
 template <int G, int SB, int CB, bool SLACK = false>
 __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
-                                  const double* __restrict__ LP, const double (&q)[SEP_NZ],
+                                  const double* __restrict__ Pinv, const double (&q)[SEP_NZ],
                                   double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg = nullptr,
                                   double wv_cost = 0.0, double* v_out = nullptr, double* red = nullptr,
                                   SepWarm<SB>* warm = nullptr, double warm_delta = 0.0,
@@ -635,11 +634,9 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
 #pragma unroll
         for (int d = 0; d < SEP_D; d++) {
             const int o = 2 * d;
-            const double l00 = LP[o * 6 + o], l10 = LP[(o + 1) * 6 + o], l11 = LP[(o + 1) * 6 + o + 1];
-            const double w0 = -q[o] * rcp(l00);
-            const double w1 = (-q[o + 1] - l10 * w0) * rcp(l11);
-            yu[o + 1] = w1 * rcp(l11);
-            yu[o] = (w0 - l10 * yu[o + 1]) * rcp(l00);
+            const double a = Pinv[3 * d], b = Pinv[3 * d + 1], c = Pinv[3 * d + 2];
+            yu[o] = -fma(a, q[o], b * q[o + 1]);
+            yu[o + 1] = -fma(b, q[o], c * q[o + 1]);
         }
         bool bad = false;
 #pragma unroll
@@ -683,12 +680,13 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             return fo;
         }
         // dual active-set solve (PdipCfg::dual_as): the PDIP below runs only when it gives up
+        // (no warm-start duals: the caller's PDIP attempts run cold when it is on)
         GSTAMP(13, true);
         if constexpr (!SLACK) {
             if (cfg.dual_as > 0 && pol != nullptr) {
                 double yg[SEP_NZ], rpg = 0.0, rdg = 0.0;
-                const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
-                                                     rdg, as_steps, warm, dbg);
+                const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, Pinv, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
+                                                     rdg, as_steps, nullptr, cfg.want_rd, dbg);
                 if (r != 0) {
                     PdipOut fo{r > 0 ? ST_OPTIMAL : ST_UNKNOWN, as_steps};
 #pragma unroll
@@ -997,7 +995,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         if constexpr (!SLACK) {
             if (pol != nullptr && finite && it > 0 && mu <= polish_mu) {
                 double rpp = 0.0, rdp = 0.0;
-                if (sep_polish<G, SB, CB>(rw, has_cbf, P, q, sl, su, zl, zu, cs, cz, pl, pu, pc, cfg.tol, pol, y,
+                if (sep_polish<G, SB, CB>(rw, has_cbf, P, Pinv, q, sl, su, zl, zu, cs, cz, pl, pu, pc, cfg.tol, pol, y,
                                           rpp, rdp, warm)) {
                     out.status = ST_OPTIMAL;
                     out.rp = rpp;
