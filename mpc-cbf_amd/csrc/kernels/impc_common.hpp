@@ -42,7 +42,20 @@ struct NbScratch {
     int32_t tmp[NB_CAP];   // sorted output
     double d2[NB_CAP];     // candidate squared distances
     int32_t keep[NB_CAP];  // k-nearest flags
+    int32_t src[NB_CAP];   // final neighbour i -> its candidate slot
+    double cst[4][NB_CAP];  // candidates' (px, py, vx, vy), read once by the query for the CBF rows
 };
+
+// Broadcast of lane K's 32-bit value within a 16-lane DPP row (row_newbcast).
+template <int K>
+__device__ __forceinline__ int row_bcast_i(int v) {
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + K, 0xF, 0xF, true);
+}
+
+// (d_a, j_a) before (d_b, j_b): nearer first, ties by agent index
+__device__ __forceinline__ bool nb_before(double da, int ja, double db, int jb) {
+    return da < db || (da == db && ja < jb);
+}
 
 // k nearest other agents (planar distance, ties by index) within the radius, found through the
 // spatial hash; the result is left in sc.idx sorted by agent index. Returns the count, or -1 if
@@ -83,7 +96,7 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         const uint32_t t = t0 + gl;
         bool keep = false;
         int j = -1;
-        double d2 = 0.0;
+        double d2 = 0.0, nx = 0.0, ny = 0.0, nvx = 0.0, nvy = 0.0;
         if (t < total) {
             if (full) {
                 j = (int)t;
@@ -94,8 +107,12 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
                     if (off[c] <= t && t - off[c] < nc[c]) e = (t - off[c]) * (gr.mask + 1u) + hs[c];
                 j = (int)gr.slots[e];
             }
-            const double ex = args.states[(size_t)j * 6] - px;
-            const double ey = args.states[(size_t)j * 6 + 1] - py;
+            nx = args.states[(size_t)j * 6];
+            ny = args.states[(size_t)j * 6 + 1];
+            nvx = args.states[(size_t)j * 6 + 3];
+            nvy = args.states[(size_t)j * 6 + 4];
+            const double ex = nx - px;
+            const double ey = ny - py;
             d2 = ex * ex + ey * ey;
             keep = (j != self) && (d2 <= r2);
             if (keep && gr.cone > 0.0) {  // inside the field of view (strict)
@@ -109,6 +126,10 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         if (keep && slot < NB_CAP) {
             sc.idx[slot] = j;
             sc.d2[slot] = d2;
+            sc.cst[0][slot] = nx;
+            sc.cst[1][slot] = ny;
+            sc.cst[2][slot] = nvx;
+            sc.cst[3][slot] = nvy;
         }
         cnt += __popcll(msk);
     }
@@ -116,6 +137,54 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
     wave_lds_sync();
     // rank by (d2, index): keep the k nearest
     const int k = gr.k;
+    const int nk = cnt < k ? cnt : k;
+    if constexpr (G == 16) {
+        if (cnt <= 2 * G) {
+            // two candidates per lane (slots gl, gl + 16) compared against all by DPP row
+            // broadcasts, in registers; then ordered by agent index the same way
+            const bool v0 = gl < cnt, v1 = gl + G < cnt;
+            const double d0 = v0 ? sc.d2[gl] : 1e300, d1 = v1 ? sc.d2[gl + G] : 1e300;
+            const int j0 = v0 ? sc.idx[gl] : 0x7fffffff, j1 = v1 ? sc.idx[gl + G] : 0x7fffffff;
+            int r0 = 0, r1 = 0;
+            auto rank_step = [&](double dm, int jm) {
+                r0 += nb_before(dm, jm, d0, j0) ? 1 : 0;
+                r1 += nb_before(dm, jm, d1, j1) ? 1 : 0;
+            };
+#define MPCCBF_NB_RANK(K)                                           \
+    rank_step(row_bcast_k<K>(d0), row_bcast_i<K>(j0));              \
+    rank_step(row_bcast_k<K>(d1), row_bcast_i<K>(j1));
+            MPCCBF_NB_RANK(0) MPCCBF_NB_RANK(1) MPCCBF_NB_RANK(2) MPCCBF_NB_RANK(3)
+            MPCCBF_NB_RANK(4) MPCCBF_NB_RANK(5) MPCCBF_NB_RANK(6) MPCCBF_NB_RANK(7)
+            MPCCBF_NB_RANK(8) MPCCBF_NB_RANK(9) MPCCBF_NB_RANK(10) MPCCBF_NB_RANK(11)
+            MPCCBF_NB_RANK(12) MPCCBF_NB_RANK(13) MPCCBF_NB_RANK(14) MPCCBF_NB_RANK(15)
+#undef MPCCBF_NB_RANK
+            const bool k0 = v0 && r0 < k, k1 = v1 && r1 < k;
+            // order the kept set by agent index: position = kept candidates with a smaller index
+            const int jk0 = k0 ? j0 : 0x7fffffff, jk1 = k1 ? j1 : 0x7fffffff;
+            int p0 = 0, p1 = 0;
+            auto pos_step = [&](int jm) {
+                p0 += jm < j0 ? 1 : 0;
+                p1 += jm < j1 ? 1 : 0;
+            };
+#define MPCCBF_NB_POS(K) pos_step(row_bcast_i<K>(jk0)); pos_step(row_bcast_i<K>(jk1));
+            MPCCBF_NB_POS(0) MPCCBF_NB_POS(1) MPCCBF_NB_POS(2) MPCCBF_NB_POS(3)
+            MPCCBF_NB_POS(4) MPCCBF_NB_POS(5) MPCCBF_NB_POS(6) MPCCBF_NB_POS(7)
+            MPCCBF_NB_POS(8) MPCCBF_NB_POS(9) MPCCBF_NB_POS(10) MPCCBF_NB_POS(11)
+            MPCCBF_NB_POS(12) MPCCBF_NB_POS(13) MPCCBF_NB_POS(14) MPCCBF_NB_POS(15)
+#undef MPCCBF_NB_POS
+            wave_lds_sync();  // every lane has read its candidates
+            if (k0) {
+                sc.idx[p0] = j0;
+                sc.src[p0] = gl;
+            }
+            if (k1) {
+                sc.idx[p1] = j1;
+                sc.src[p1] = gl + G;
+            }
+            wave_lds_sync();
+            return nk;
+        }
+    }
     for (int i = gl; i < cnt; i += G) {
         const double di = sc.d2[i];
         const int ji = sc.idx[i];
@@ -126,7 +195,6 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         }
         sc.keep[i] = rank < k ? 1 : 0;
     }
-    const int nk = cnt < k ? cnt : k;
     wave_lds_sync();
     // order the kept set by agent index
     for (int i = gl; i < cnt; i += G) {
@@ -135,6 +203,7 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
             int pos = 0;
             for (int m = 0; m < cnt; m++) pos += (sc.keep[m] && sc.idx[m] < ji) ? 1 : 0;
             sc.tmp[pos] = ji;
+            sc.src[pos] = i;
         }
     }
     wave_lds_sync();
@@ -249,7 +318,7 @@ __device__ __forceinline__ void cbf_ego_state(const DevOps& op, const double* bu
 template <int NZ, int G>
 __device__ int stage_cbf_rows(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
                               const double (&s0)[6], const double (&y)[NZ], bool grid_mode,
-                              const int32_t* nbl, int nb0, int nnb, double* stage, int cap, int gl,
+                              const NbScratch* nbs, int nb0, int nnb, double* stage, int cap, int gl,
                               bool* infeasible) {
     const double* UZ = opp(buf, op.o_UZ);
     const double* US = opp(buf, op.o_US);
@@ -275,9 +344,21 @@ __device__ int stage_cbf_rows(const DevOps& op, const double* buf, const ImpcArg
             bool keep = false;
             double a[3] = {0.0, 0.0, 0.0}, b = 0.0;
             if (j < nnb) {
-                const int nbi = grid_mode ? nbl[j] : args.nb_col[nb0 + j];
-                const double* ns = args.states + (size_t)nbi * 6;
-                safety_cbf(e, ns[0], ns[1], ns[3], ns[4], op.d_min, a, b);
+                double npx, npy, nvx, nvy;
+                if (grid_mode) {  // read by the neighbour query (LDS)
+                    const int c = nbs->src[j];
+                    npx = nbs->cst[0][c];
+                    npy = nbs->cst[1][c];
+                    nvx = nbs->cst[2][c];
+                    nvy = nbs->cst[3][c];
+                } else {
+                    const double* ns = args.states + (size_t)args.nb_col[nb0 + j] * 6;
+                    npx = ns[0];
+                    npy = ns[1];
+                    nvx = ns[3];
+                    nvy = ns[4];
+                }
+                safety_cbf(e, npx, npy, nvx, nvy, op.d_min, a, b);
                 // max / min of -a^T u over the acceleration box at sample k (those box rows
                 // are part of every QP): b >= max  -> the row is implied (exactly redundant);
                 // b < min - tol -> no acceleration satisfies it (infeasible).

@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
             continue;
         }
         bool row_infeasible = false;
-        const int count = stage_cbf_rows<NZ, G>(op, buf, args, it, s0, y, grid_mode, nb_scratch[gib].idx,
+        const int count = stage_cbf_rows<NZ, G>(op, buf, args, it, s0, y, grid_mode, &nb_scratch[gib],
                                                 nb0, nnb, stage, cap, gl, &row_infeasible);
         if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
         // ---- CBF rows into the free slots (previous iteration's CBF rows are replaced)
@@ -245,9 +245,10 @@ __device__ double lane_slack_weight(const DevOps& op, const ImpcArgs& args, cons
 }
 
 // state row `row` of the batch (re-read where needed instead of held in registers)
-__device__ __forceinline__ void load_state(const ImpcArgs& args, int row, double (&s)[6]) {
+__device__ __forceinline__ void load_state_lds(const double* s0k, double (&s)[6]) {
+    wave_lds_sync();  // (written by lanes 0..5 of the group)
 #pragma unroll
-    for (int i = 0; i < 6; i++) s[i] = __builtin_nontemporal_load(args.states + (size_t)row * 6 + i);
+    for (int i = 0; i < 6; i++) s[i] = s0k[i];
 }
 
 // Hand agent ai to the fallback launch (lane 0 appends it to args.defer: [count, -, agents...]).
@@ -322,6 +323,15 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     double* ykeep = keep + gl;  // ykeep[16 * i]
 #pragma unroll
     for (int i = 0; i < NZ; i++) y[i] = ykeep[16 * i] = 0.0;
+    // the agent's state, kept for the CBF rows and the outputs (group-uniform: LDS broadcast reads
+    // instead of further global round trips)
+    double* s0k = keep + 16 * (SEP_NZ + 2 * SEP_D * SB);
+    {
+        double v = s0[0];
+#pragma unroll
+        for (int i = 1; i < 6; i++) v = gl == i ? s0[i] : v;
+        if (gl < 6) s0k[gl] = v;
+    }
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
     SepWarm<SB> warm{keep + 16 * NZ};  // box duals of the previous OPTIMAL solve (iteration 1 warm start)
@@ -339,12 +349,12 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         if constexpr (SLACK) {
             // slack mode: rows stay in their neighbour's lane; a slack row is never infeasible
             double sx[6];  // the state again (not kept in registers across the solves)
-            load_state(args, self, sx);
+            load_state_lds(s0k, sx);
             live = lane_cbf_rows<G, CB>(op, buf, args, it, sx, y, grid_mode, nbs.idx, nb0, nnb, gl, rw);
         } else {
             double sx[6];  // the state again (not kept in registers across the solves)
-            load_state(args, self, sx);
-            count = stage_cbf_rows<NZ, G>(op, buf, args, it, sx, y, grid_mode, nbs.idx,
+            load_state_lds(s0k, sx);
+            count = stage_cbf_rows<NZ, G>(op, buf, args, it, sx, y, grid_mode, &nbs,
                                           nb0, nnb, stage, cap, gl, &row_infeasible);
             live = count > 0;
 #pragma unroll
@@ -461,7 +471,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     double yk[NZ], sx[6];
 #pragma unroll
     for (int i = 0; i < NZ; i++) yk[i] = ykeep[16 * i];
-    load_state(args, self, sx);
+    load_state_lds(s0k, sx);
     write_agent_outputs<NZ, G>(op, buf, args, ai, gl, sx, yk, have_curve);
     stamp(args, ai, gl, 7);
 }
@@ -476,7 +486,7 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     __shared__ double stage_all[GPB][SLACK ? 1 : CB * 16 * (SEP_NZ + 1)];
     __shared__ double red_all[GPB][16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
-    __shared__ double keep_all[GPB][16 * (SEP_NZ + 2 * SEP_D * SB)];
+    __shared__ double keep_all[GPB][16 * (SEP_NZ + 2 * SEP_D * SB) + 8];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     if constexpr (!QUEUE) {
