@@ -359,6 +359,28 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
             }
         pack(v, d.o_P16, P16);
         pack(v, d.o_LP16, L16);
+        // P^-1 (padded with the identity) for the dual active-set solve: columns of
+        // L^-T L^-1 e_b by forward / backward substitution with the factor L = LPr
+        std::vector<double> Pi16(256, 0.0);
+        for (int b = 0; b < 16; b++) {
+            if (b >= o.nz) {
+                Pi16[b * 16 + b] = 1.0;
+                continue;
+            }
+            std::vector<double> x(o.nz, 0.0);
+            for (int a = 0; a < o.nz; a++) {  // L x = e_b
+                double s = a == b ? 1.0 : 0.0;
+                for (int k = 0; k < a; k++) s -= o.LPr(a, k) * x[k];
+                x[a] = s / o.LPr(a, a);
+            }
+            for (int a = o.nz - 1; a >= 0; a--) {  // L^T x = x
+                double s = x[a];
+                for (int k = a + 1; k < o.nz; k++) s -= o.LPr(k, a) * x[k];
+                x[a] = s / o.LPr(a, a);
+            }
+            for (int a = 0; a < o.nz; a++) Pi16[a * 16 + b] = x[a];
+        }
+        pack(v, d.o_Pinv16, Pi16);
     }
     v.push_back(0.0);  // keep every offset addressable even for empty operators
     for (int i = 0; i < 3; i++) {

@@ -1,0 +1,227 @@
+// das_wave.hpp — dual active-set solve (Goldfarb & Idnani's method, range-space form) of one QP
+// per wavefront on the layouts of pdip_wave.hpp: the FoV controller's first attempt, the PDIP
+// solving only the QPs it hands on.
+//
+// From the unconstrained minimiser y = -P^-1 q, the most violated side (scaled as the primal
+// residual) is the candidate; the direction z = P^-1 (n_p - N_A r) keeps the active sides exact
+// and moves y onto the candidate unless an active multiplier reaches zero first, in which case
+// that side leaves and the step is retried. Every step keeps the iterate dual feasible and raises
+// the objective. With K = G_A P^-1 G_A^T = L L^T (k <= 15 active rows):
+//   c = G_A P^-1 n_p,  v = L^-1 c,  r = L^-T v,  zn = n_p P^-1 n_p - |v|^2 (> 0: n_p independent)
+// and a joining side appends (v^T, sqrt(zn)) to L; a leaving side refactors K.
+//
+// Layouts (64 lanes, i = lane & 15, the four 16-lane rows replicate): vectors of the reduced
+// dimension and the per-active-row quantities (c, v, r, multipliers u) on the row layout — lane i
+// holds element / active row i; L row i in lane i's registers and row-major in sc.M (the
+// backward substitution reads its columns); the active rows' P^-1 g, image row, side sign and
+// bound in LDS (WaveAS). Rows are read from the wave's row image Gs (16 doubles per row).
+#pragma once
+
+#include "pdip_wave.hpp"
+
+namespace mpccbf {
+namespace dev {
+
+struct WaveAS {
+    double W[WNZ * WNZ];     // active row a: P^-1 g_a (16 doubles)
+    double Pi[WNZ * 17];     // P^-1, rows padded to 17 doubles (lane i reads row i: spread banks)
+    double w[WNZ];           // the candidate's P^-1 g
+    double b[WNZ], sg[WNZ];  // active rows' bound and side sign (+1 upper, -1 lower)
+    double u[WNZ];           // multipliers (shift scratch)
+    int32_t row[WNZ];        // active rows' image row
+};
+
+// first half of solve_rows: v = L^-1 b on the row layout
+__device__ __forceinline__ double fwd_rows(const double (&L)[WNZ], double inv_i, double b, int i) {
+    double res = b, wl = 0.0;
+#pragma unroll
+    for (int k = 0; k < WNZ; k++) {
+        const double wk = bcast16v(k, res * inv_i);
+        res = fma(-L[k], wk, res);
+        wl = (i == k) ? wk : wl;
+    }
+    return wl;
+}
+
+// second half of solve_rows: x = L^-T v (L's columns from the row-major copy Lm)
+__device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double inv_i, double v, int i) {
+    double res = v, xl = 0.0;
+#pragma unroll
+    for (int k = WNZ - 1; k >= 0; k--) {
+        const double xk = bcast16v(k, res * inv_i);
+        res = fma(-Lm[k * WNZ + i], xk, res);
+        xl = (i == k) ? xk : xl;
+    }
+    return xl;
+}
+
+// Returns 1: optimal (sc.y, rp_out, rd_out); -1: no step reaches the candidate (no feasible
+// point: phase 1 decides); 0: gave up (step limit, breakdown, dual residual) — the PDIP solves.
+// Pinv: P^-1 padded to 16 x 16 (global); P for the dual residual (want_rd).
+__device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, WaveScratch& sc,
+                              WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
+                              double tol, int maxstep, bool want_rd, int lane, double& rp_out,
+                              double& rd_out, int& steps) {
+    const int i = lane & 15;
+    steps = 0;
+    for (int e = lane; e < WNZ * WNZ; e += 64) ws.Pi[(e >> 4) * 17 + (e & 15)] = Pinv[e];
+    // per-slot violation scales, the factor of the empty active set (identity)
+    double pl[WR], pu[WR];
+#pragma unroll
+    for (int s = 0; s < WR; s++) {
+        pl[s] = rw.ml[s] * rcp(1.0 + fabs(rw.lo[s]));
+        pu[s] = rcp(1.0 + fabs(rw.hi[s]));
+    }
+    double L[WNZ], inv_i = 1.0, ui = 0.0;
+#pragma unroll
+    for (int k = 0; k < WNZ; k++) L[k] = k == i ? 1.0 : 0.0;
+    if (lane < WNZ) {
+#pragma unroll
+        for (int k = 0; k < WNZ; k++) sc.M[lane * WNZ + k] = k == lane ? 1.0 : 0.0;
+    }
+    wave_lds_sync();
+    // y = -P^-1 q
+    double yi;
+    {
+        double a = 0.0;
+#pragma unroll
+        for (int j = 0; j < WNZ; j++) a = fma(ws.Pi[i * 17 + j], sc.q[j], a);
+        yi = -a;
+    }
+    publish16(sc.y, yi, lane);
+    int k = 0;
+    double m = 0.0;
+    const double add_tol = 0.1 * tol;
+    for (;;) {
+        // the most violated side of the wave (lowest lane on ties)
+        double vb = -1.0;
+        int rb = 0, sdb = 1;
+        double bb = 0.0;
+#pragma unroll
+        for (int s = 0; s < WR; s++) {
+            const double t = dotl(rw.g[s], sc.y);
+            const double vl = rw.ml[s] > 0.0 ? (rw.lo[s] - t) * pl[s] : -1.0;
+            const double vu = (t - rw.hi[s]) * pu[s];
+            const int r = wave_owner_row(lane, s);
+            if (vl > vb) vb = vl, rb = r, sdb = 0, bb = rw.lo[s];
+            if (vu > vb) vb = vu, rb = r, sdb = 1, bb = rw.hi[s];
+        }
+        m = wave_reduce<Op::Max>(vb);
+        if (!(m > add_tol)) break;
+        if (steps >= maxstep) return 0;
+        const int owner = __ffsll((long long)__ballot(vb == m)) - 1;
+        const int rp = __shfl(rb, owner, 64);
+        const double sp = __shfl(sdb, owner, 64) ? 1.0 : -1.0;
+        const double bp = __shfl(bb, owner, 64);
+        const double* gp = Gs + rp * WNZ;
+        // the candidate's P^-1 g on the row layout, published
+        double wi = 0.0;
+#pragma unroll
+        for (int j = 0; j < WNZ; j++) wi = fma(ws.Pi[i * 17 + j], gp[j], wi);
+        publish16(ws.w, wi, lane);
+        const double nw = dotl(gp, ws.w);
+        double up = 0.0;  // the candidate's multiplier
+        for (;;) {
+            if (++steps > maxstep) return 0;
+            // c_a = n_a-side coefficient: g_a P^-1 n_p (lane a < k), v = L^-1 c, r = L^-T v
+            const int ra = i < k ? ws.row[i] : rp;
+            const double ci = i < k ? sp * dotl(Gs + ra * WNZ, ws.w) : 0.0;
+            const double sgi = i < k ? ws.sg[i] : 0.0;
+            const double vi = fwd_rows(L, inv_i, ci, i);
+            const double rhoi = bwd_rows(sc.M, inv_i, vi, i);
+            const double zn = nw - grp_sum<16>(vi * vi);
+            const double vp = sp * (dotl(gp, sc.y) - bp);
+            // dual step: the first active multiplier to reach zero
+            const double r_i = sgi * rhoi;
+            const double ratio = (i < k && r_i > 0.0) ? ui * rcp(r_i) : 1e300;
+            const double t1 = grp_min<16>(ratio);
+            const int l = t1 < 1e300 ? __ffsll((long long)grp_ballot<16>(ratio == t1)) - 1 : -1;
+            const bool full = zn > 1e-10 * nw;  // else n_p lies in the span of the active sides
+            const double t2 = full ? vp * rcp(zn) : 1e300;
+            if (l < 0 && !full) return -1;
+            const double t = fmin(t1, t2);
+            if (full) {
+                double zi = sp * wi;
+#pragma unroll
+                for (int a = 0; a < WNZ - 1; a++) {
+                    const double ra_ = bcast16v(a, rhoi);
+                    zi = fma(a < k ? -ra_ : 0.0, ws.W[(a < k ? a : 0) * WNZ + i], zi);
+                }
+                yi = fma(-t, zi, yi);
+            }
+            ui = i < k ? fma(-t, r_i, ui) : ui;
+            up += t;
+            publish16(sc.y, yi, lane);
+            if (t2 <= t1) {  // the candidate joins: L gains (v^T, sqrt(zn))
+                if (k == WNZ - 1) return 0;
+                const double dz = sqrt(zn), rz = rcp(dz);
+                // K's new column (g-form) is c / sp: L's new row is L^-1 c / sp = sp v
+                if (lane < WNZ) {
+                    ws.W[k * WNZ + lane] = wi;
+                    sc.M[k * WNZ + lane] = lane < k ? sp * vi : (lane == k ? dz : 0.0);
+                }
+                if (lane == 0) {
+                    ws.row[k] = rp;
+                    ws.sg[k] = sp;
+                    ws.b[k] = bp;
+                }
+#pragma unroll
+                for (int j = 0; j < WNZ; j++) {
+                    const double vj = sp * bcast16v(j, vi);
+                    L[j] = (i == k) ? (j < k ? vj : (j == k ? dz : 0.0)) : L[j];
+                }
+                inv_i = i == k ? rz : inv_i;
+                ui = i == k ? up : ui;
+                k++;
+                wave_lds_sync();
+                break;
+            }
+            // side l leaves: rows above it move down (lane j: column j), K refactored
+            if (lane < WNZ) ws.u[lane] = ui;
+            wave_lds_sync();
+            if (lane < WNZ) {
+                for (int a = l; a < k - 1; a++) ws.W[a * WNZ + lane] = ws.W[(a + 1) * WNZ + lane];
+            }
+            if (lane == 0) {
+                for (int a = l; a < k - 1; a++) {
+                    ws.row[a] = ws.row[a + 1];
+                    ws.sg[a] = ws.sg[a + 1];
+                    ws.b[a] = ws.b[a + 1];
+                }
+            }
+            ui = i >= l ? (i + 1 < k ? ws.u[i + 1] : 0.0) : ui;
+            k--;
+            wave_lds_sync();
+            double Kr[WNZ];
+            {
+                const double* gi_ = Gs + (i < k ? ws.row[i] : 0) * WNZ;
+#pragma unroll
+                for (int b = 0; b < WNZ; b++)
+                    Kr[b] = (i < k && b < k) ? dotl(gi_, ws.W + b * WNZ) : (i == b ? 1.0 : 0.0);
+            }
+            if (!chol_rows(Kr, L, inv_i, sc.M, lane)) return 0;
+        }
+    }
+    // converged: primal residual = the last scan's worst violation; dual residual of the iterate
+    // P y + q + G_A^T lam (lam_a = sign_a u_a) when reported
+    double rd = 0.0;
+    if (want_rd) {
+        double r = sc.q[i];
+#pragma unroll
+        for (int j = 0; j < WNZ; j++) r = fma(P[i * WNZ + j], sc.y[j], r);
+#pragma unroll
+        for (int a = 0; a < WNZ - 1; a++) {
+            const double la = bcast16v(a, ui * (i < k ? ws.sg[i < k ? i : 0] : 0.0));
+            r = fma(a < k ? la : 0.0, Gs[(a < k ? ws.row[a] : 0) * WNZ + i], r);
+        }
+        double qn = fabs(sc.q[i]);
+        rd = grp_max<16>(fabs(r)) * rcp(1.0 + grp_max<16>(qn));
+        if (!(rd <= tol)) return 0;
+    }
+    rp_out = fmax(m, 0.0);
+    rd_out = rd;
+    return 1;
+}
+
+}  // namespace dev
+}  // namespace mpccbf

@@ -30,6 +30,7 @@ struct DevOps {
     int32_t cbf_mode, C;
     double fov_beta, fov_Ds, fov_Rs, bbox[3];
     int32_t o_VZ, o_VS, o_Wbox, o_P16, o_LP16;
+    int32_t o_Pinv16;  // FoV: P^-1 padded to 16 x 16 (dual active-set solve)
     // closed-loop simulator: stored-curve evaluation (EB0 / EB1: C x C Bernstein monomials of
     // value / first derivative, cum: P cumulative piece parameters)
     int32_t P, o_EB0, o_EB1, o_cum;

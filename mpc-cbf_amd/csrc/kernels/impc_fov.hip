@@ -16,7 +16,7 @@
 #include "impc.hpp"
 #include "impc_common.hpp"
 #include "fov_cbf.hpp"
-#include "pdip_wave.hpp"
+#include "das_wave.hpp"
 
 namespace mpccbf {
 namespace dev {
@@ -53,6 +53,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     __shared__ double rlo[WROWS], rhi[WROWS], rml[WROWS];
     __shared__ WaveScratch sc;
     __shared__ NbScratch nb_scratch;
+    __shared__ WaveAS was;  // dual active-set workspace
 
     const int self = args.agent_first + ai;
     double s0[6];
@@ -317,19 +318,46 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 sk.live = slk->live[lane];
                 sk.w = (lane >> 3) < nnb ? slk->w[lane >> 3] : 0.0;
             }
-            const PdipOut po = pdip_solve_wave<SLACK>(rw, Gimg, nchunk, sc, opp(buf, op.o_P16),
-                                                      opp(buf, op.o_LP16), cfg, lane, dbg, &sk, &vobj);
-            st = po.status;
-            nit = po.iters;
-            prs = po.rp;
-            drs = po.rd;
-            // slack mode: the slack rows are always satisfiable, phase 1 certifies the box and
-            // Voronoi rows (the ordinary image)
-            if (st != ST_OPTIMAL) {
+            // first attempt (no slack variables): the dual active-set solve; a QP it finds
+            // without a feasible point goes to phase 1 directly, one it gives up on to the PDIP
+            int das = 0, dsteps = 0;
+            double drp = 0.0, drd = 0.0;
+            if constexpr (!SLACK) {
+                if (op.dual_as > 0)
+                    das = das_solve_wave(rw, Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16), op.tol,
+                                         2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps);
+            }
+            bool settled = false;
+            if (das == 1) {
+                st = ST_OPTIMAL;
+                nit = dsteps;
+                prs = drp;
+                drs = drd;
+                settled = true;
+            } else if (das < 0) {
                 const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);
-                if (tstar > op.feas_tol) {
+                if (tstar > op.feas_tol && tstar < 1e300) {  // (1e300: phase 1 failed, the PDIP decides)
                     st = ST_INFEASIBLE;
+                    nit = dsteps;
                     prs = tstar;
+                    settled = true;
+                }
+            }
+            if (!settled) {
+                const PdipOut po = pdip_solve_wave<SLACK>(rw, Gimg, nchunk, sc, opp(buf, op.o_P16),
+                                                          opp(buf, op.o_LP16), cfg, lane, dbg, &sk, &vobj);
+                st = po.status;
+                nit = dsteps + po.iters;
+                prs = po.rp;
+                drs = po.rd;
+                // slack mode: the slack rows are always satisfiable, phase 1 certifies the box and
+                // Voronoi rows (the ordinary image)
+                if (st != ST_OPTIMAL) {
+                    const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);
+                    if (tstar > op.feas_tol) {
+                        st = ST_INFEASIBLE;
+                        prs = tstar;
+                    }
                 }
             }
         }

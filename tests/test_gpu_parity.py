@@ -322,6 +322,38 @@ def test_fov_grid_neighbours_match_csr(mpclib):
     np.testing.assert_allclose(out["obj"].cpu().numpy()[ok], g_csr["obj"][ok], rtol=1e-10, atol=1e-9)
 
 
+@pytest.mark.parametrize("scale", [1.0, 0.6, 0.45])
+def test_fov_dual_active_set_matches_pdip(mpclib, scale, monkeypatch):
+    """Config 5: the dual active-set solve (default first attempt, das_wave.hpp) and the PDIP alone
+    (MPCCBF_DUAL_AS=0) give the same statuses — INFEASIBLE included (an unreachable candidate
+    goes to phase 1 directly) — and the same optima to the PDIP's tolerance, except where the
+    PDIP alone fails (UNKNOWN): there the active-set result is checked against the oracle."""
+    torch = _torch()
+    cfg = swarm.fov_config(20)
+    states, targets = swarm.heading_swarm(256, seed=4)
+    states[:, :2] *= scale
+    rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+    monkeypatch.setenv("MPCCBF_DUAL_AS", "0")
+    pdip = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    monkeypatch.delenv("MPCCBF_DUAL_AS")
+    das = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    mism = np.nonzero(np.any(pdip["status"] != das["status"], axis=1))[0]
+    assert len(mism) <= 0.02 * len(states), mism
+    if len(mism):
+        assert np.all(np.any(pdip["status"][mism] == O.UNKNOWN, axis=1)), (pdip["status"][mism], das["status"][mism])
+        ref = run_oracle(cfg, states, targets, rp, col, list(mism))
+        sub = {k: v[mism] for k, v in das.items()}
+        compare(cfg, sub, ref, list(range(len(mism))))
+    same = np.ones(len(states), dtype=bool)
+    same[mism] = False
+    ok = (pdip["status"] == 0) & same[:, None]
+    assert ok[:, 0].sum() > 50
+    err = np.abs(pdip["obj"][ok] - das["obj"][ok]) / np.maximum(1.0, np.abs(pdip["obj"][ok]))
+    assert err.max() <= 1e-7, err.max()
+    assert np.nanmax(np.abs(pdip["x"][same] - das["x"][same])) <= 1e-5
+    assert np.all(das["dual_res"][ok] <= 1e-9) and np.all(das["primal_res"][ok] <= 1e-9)
+
+
 @pytest.mark.parametrize("scale,k_hor", [(0.42, 15), (0.6, 10)])
 def test_slack_mode_matches_oracle(mpclib, scale, k_hor):
     """slack_mode (ConnectivityIMPCCBF.cpp:73-119, MPCCBFQPGeneratorBase.cpp:28-130): one
