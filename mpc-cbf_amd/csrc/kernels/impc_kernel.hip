@@ -174,13 +174,13 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
 // ---------------------------------------------------------------------------------------------
 // Separable layout (x / y / yaw channels, 2 reduced variables each; pdip_sep.hpp)
 // ---------------------------------------------------------------------------------------------
-// Slack mode: lane j builds the CBF rows of neighbour j itself (slot k = sample k), so all rows
-// of one slack variable live in the lane that owns it. Filtered rows stay inert (ccv = 0).
-// Returns the group-uniform "some row is live" flag.
-template <int G, int CB>
+// Slack mode: a lane builds the CBF rows of its neighbour (list position jn, -1: none) itself
+// (slot k = sample k), so all rows of one slack variable live in the lane that owns it. Filtered
+// rows stay inert (ccv = 0). Returns whether some row of this lane is live.
+template <int CB>
 __device__ bool lane_cbf_rows(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
                               const double (&s0)[6], const double (&y)[SEP_NZ], bool grid_mode,
-                              const int32_t* nbl, int nb0, int nnb, int gl, SepRows<1, CB>& rw) {
+                              const int32_t* nbl, int nb0, int jn, SepRows<1, CB>& rw) {
     const double* UZ = opp(buf, op.o_UZ);
     const double* US = opp(buf, op.o_US);
     const int nk = (it == 0) ? 1 : op.cbf_h;
@@ -191,10 +191,10 @@ __device__ bool lane_cbf_rows(const DevOps& op, const double* buf, const ImpcArg
         for (int j = 0; j < 4; j++) rw.cg[k][j] = 0.0;
         rw.chi[k] = 1.0;
         rw.ccv[k] = 0.0;
-        if (k < nk && gl < nnb) {
+        if (k < nk && jn >= 0) {
             double e[6];
             cbf_ego_state<SEP_NZ>(op, buf, it, k, s0, y, e);
-            const int nbi = grid_mode ? nbl[gl] : args.nb_col[nb0 + gl];
+            const int nbi = grid_mode ? nbl[jn] : args.nb_col[nb0 + jn];
             const double* ns = args.states + (size_t)nbi * 6;
             double a[3], b;
             safety_cbf(e, ns[0], ns[1], ns[3], ns[4], op.d_min, a, b);
@@ -221,27 +221,95 @@ __device__ bool lane_cbf_rows(const DevOps& op, const double* buf, const ImpcArg
             }
         }
     }
-    return grp_ballot<G>(live) != 0ull;
+    return live;
 }
 
-// Slack weight of this lane's neighbour: slack_cost * decay^rank, rank by planar distance
-// (ConnectivityIMPCCBF.cpp:73-100; ties by list position — the reference's std::sort leaves
-// them unspecified). Lanes without a neighbour get cost 1 (their slack has no rows: v -> 0).
+// Whether neighbour jn (-1: none) has a CBF row the acceleration box does not imply (the filter of
+// lane_cbf_rows without the row coefficients).
+__device__ bool lane_cbf_live(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
+                              const double (&s0)[6], const double (&y)[SEP_NZ], bool grid_mode,
+                              const int32_t* nbl, int nb0, int jn) {
+    if (jn < 0) return false;
+    const int nk = (it == 0) ? 1 : op.cbf_h;
+    const int nbi = grid_mode ? nbl[jn] : args.nb_col[nb0 + jn];
+    const double* ns = args.states + (size_t)nbi * 6;
+    bool live = false;
+    for (int k = 0; k < nk; k++) {
+        double e[6], a[3], b;
+        cbf_ego_state<SEP_NZ>(op, buf, it, k, s0, y, e);
+        safety_cbf(e, ns[0], ns[1], ns[3], ns[4], op.d_min, a, b);
+        double bmax = 0.0;
+#pragma unroll
+        for (int d = 0; d < 3; d++) bmax += fmax(-a[d] * op.a_lo[d], -a[d] * op.a_hi[d]);
+        live = live || !(op.cbf_filter && b >= bmax);
+    }
+    return live;
+}
+
 template <int G>
 __device__ double lane_slack_weight(const DevOps& op, const ImpcArgs& args, const double (&s0)[6],
-                                    bool grid_mode, const int32_t* nbl, int nb0, int nnb, int gl) {
-    double dist = 0.0;
-    if (gl < nnb) {
-        const int nbi = grid_mode ? nbl[gl] : args.nb_col[nb0 + gl];
+                                    bool grid_mode, const int32_t* nbl, int nb0, int nnb, int jn);
+
+// Slack mode with more than G neighbours: the ones with a live row in IMPC iteration `it` are
+// compacted into the lanes (lane l takes the l-th: jn, its weight); returns their count (more than
+// G: capacity exceeded, jn = -1). State and kept solution from LDS.
+template <int G>
+__device__ int slack_compact(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
+                                          const double* s0k, const double* ykeep, bool grid_mode,
+                                          const int32_t* nbl, int nb0, int nnb, int gl, int& jn,
+                                          double& wslack) {
+    double sx[6], y[SEP_NZ];
+#pragma unroll
+    for (int i = 0; i < 6; i++) sx[i] = s0k[i];
+#pragma unroll
+    for (int i = 0; i < SEP_NZ; i++) y[i] = ykeep[16 * i];
+    int nlive = 0;
+    jn = -1;
+    for (int base = 0; base < nnb; base += G) {
+        const bool lv = lane_cbf_live(op, buf, args, it, sx, y, grid_mode, nbl, nb0, base + gl < nnb ? base + gl : -1);
+        const unsigned long long msk = grp_ballot<G>(lv);
+        const int want = gl - nlive;
+        int c = 0;
+        for (int b = 0; b < G; b++) {
+            if ((msk >> b) & 1ull) {
+                if (c == want) jn = base + b;
+                c++;
+            }
+        }
+        nlive += c;
+    }
+    if (nlive > G) jn = -1;
+    wslack = lane_slack_weight<G>(op, args, sx, grid_mode, nbl, nb0, nnb, jn);
+    return nlive;
+}
+
+// Slack weight of the lane's neighbour (list position jn, -1: none): slack_cost * decay^rank,
+// rank by planar distance among all nnb neighbours (ConnectivityIMPCCBF.cpp:73-100; ties by list
+// position — the reference's std::sort leaves them unspecified). Lanes without a neighbour get
+// cost 1 (their slack has no rows: v -> 0). Up to G neighbours by lane shuffles, beyond by a
+// scan of the whole list.
+template <int G>
+__device__ double lane_slack_weight(const DevOps& op, const ImpcArgs& args, const double (&s0)[6],
+                                    bool grid_mode, const int32_t* nbl, int nb0, int nnb, int jn) {
+    auto dist_of = [&](int j) {
+        const int nbi = grid_mode ? nbl[j] : args.nb_col[nb0 + j];
         const double dx = args.states[(size_t)nbi * 6] - s0[0], dy = args.states[(size_t)nbi * 6 + 1] - s0[1];
-        dist = sqrt(dx * dx + dy * dy);
-    }
+        return sqrt(dx * dx + dy * dy);
+    };
+    const double dist = jn >= 0 ? dist_of(jn) : 0.0;
     int rank = 0;
-    for (int k = 0; k < nnb; k++) {
-        const double dk = __shfl(dist, k, G);
-        rank += (dk < dist || (dk == dist && k < gl)) ? 1 : 0;
+    if (nnb <= G) {  // (jn = this lane's index)
+        for (int k = 0; k < nnb; k++) {
+            const double dk = __shfl(dist, k, G);
+            rank += (dk < dist || (dk == dist && k < jn)) ? 1 : 0;
+        }
+    } else {
+        for (int k = 0; k < nnb; k++) {
+            const double dk = dist_of(k);
+            rank += (dk < dist || (dk == dist && k < jn)) ? 1 : 0;
+        }
     }
-    return gl < nnb ? op.slack_cost * pow(op.slack_decay, (double)rank) : 1.0;
+    return jn >= 0 ? op.slack_cost * pow(op.slack_decay, (double)rank) : 1.0;
 }
 
 // state row `row` of the batch (re-read where needed instead of held in registers)
@@ -261,7 +329,7 @@ __device__ __forceinline__ void defer_agent(const ImpcArgs& args, int ai, int gl
 
 // One agent's IMPC step on the separable layout (the body of impc_sep_kernel). stage / red / nbs:
 // this group's LDS (CBF-row staging, Newton-sum all-reduce, neighbour query).
-template <int SB, int CB, bool SLACK>
+template <int SB, int CB, bool SLACK, bool QUEUE>
 __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
                                const int ai, const int gl, double* stage, double* red, NbScratch& nbs,
                                double* keep) {
@@ -307,14 +375,17 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     } else {
         nnb = grid_neighbors<G>(args, self, s0[0], s0[1], nbs, gl);
     }
-    if (SLACK && nnb > G && args.defer) {  // slack mode: one lane per neighbour
+    if (SLACK && !QUEUE && nnb > G && args.defer) {  // slack mode: beyond one lane per neighbour
         defer_agent(args, ai, gl);
         return;
     }
-    const bool nb_overflow = nnb < 0 || (SLACK && nnb > G);
+    const bool nb_overflow = nnb < 0 || (SLACK && !QUEUE && nnb > G);
     if (nb_overflow) nnb = 0;
     double wslack = 0.0, vslack = 0.0;
-    if constexpr (SLACK) wslack = lane_slack_weight<G>(op, args, s0, grid_mode, nbs.idx, nb0, nnb, gl);
+    // slack mode: one lane per neighbour; with more than G neighbours (the fallback launch), per
+    // IMPC iteration the ones with a live row (a slack without rows is 0 at the optimum)
+    if constexpr (SLACK)
+        if (nnb <= G) wslack = lane_slack_weight<G>(op, args, s0, grid_mode, nbs.idx, nb0, nnb, gl < nnb ? gl : -1);
     stamp(args, ai, gl, 2);
 
     // the kept solution and the warm-start duals live in per-lane LDS slots (keep: [ykeep 6 x 16 |
@@ -346,11 +417,18 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         bool row_infeasible = false;
         int count = 0;
         bool live = false;
+        bool slack_overflow = false;
         if constexpr (SLACK) {
             // slack mode: rows stay in their neighbour's lane; a slack row is never infeasible
             double sx[6];  // the state again (not kept in registers across the solves)
             load_state_lds(s0k, sx);
-            live = lane_cbf_rows<G, CB>(op, buf, args, it, sx, y, grid_mode, nbs.idx, nb0, nnb, gl, rw);
+            int jn = gl < nnb ? gl : -1;
+            if (QUEUE && nnb > G) {
+                const int nlive = slack_compact<G>(op, buf, args, it, s0k, ykeep, grid_mode, nbs.idx, nb0, nnb,
+                                                   gl, jn, wslack);
+                slack_overflow = nlive > G;
+            }
+            live = grp_ballot<G>(lane_cbf_rows<CB>(op, buf, args, it, sx, y, grid_mode, nbs.idx, nb0, jn, rw)) != 0ull;
         } else {
             double sx[6];  // the state again (not kept in registers across the solves)
             load_state_lds(s0k, sx);
@@ -376,7 +454,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         int st;
         int nit = 0;
         double prs = __builtin_nan(""), drs = __builtin_nan("");
-        if (count > cap || nb_overflow) {
+        if (count > cap || nb_overflow || slack_overflow) {
             st = ST_ERROR;
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
@@ -493,12 +571,12 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
         grid_clear(args);
         const int ai = blockIdx.x * GPB + gib;
         if (ai >= args.num_agents) return;
-        impc_sep_agent<SB, CB, SLACK>(op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib],
+        impc_sep_agent<SB, CB, SLACK, false>(op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib],
                                       keep_all[gib]);
     } else {
         const int n = args.queue[0];
         for (int k = blockIdx.x * GPB + gib; k < n; k += gridDim.x * GPB)
-            impc_sep_agent<SB, CB, SLACK>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
+            impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
                                           nb_scratch[gib], keep_all[gib]);
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -533,18 +611,21 @@ static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const I
     return hipGetLastError();
 }
 
-// Agents beyond the default separable kernel's capacity (more than 16 live CBF rows in an IMPC
-// iteration) are deferred to this launch: the same solver with 8 CBF row slots per lane (128
-// rows) in 64-thread blocks. Agents beyond that report ERROR.
+// Agents beyond the default separable kernel's capacity are deferred to this launch: more than
+// 16 live CBF rows in an IMPC iteration — the same solver with 8 CBF row slots per lane (128
+// rows) in 64-thread blocks; slack mode with more than 16 neighbours — the slack solver, the
+// neighbours with a live row compacted into the lanes. Agents beyond that report ERROR.
 hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
-    if (a.num_agents <= 0 || !a.queue || op.slack_mode) return hipSuccess;
+    if (a.num_agents <= 0 || !a.queue) return hipSuccess;
+    if (op.slack_mode) return launch_impc_sep_t<1, 2, true, 64, true>(op, buf, a, s);
     return launch_impc_sep_t<1, 8, false, 64, true>(op, buf, a, s);
 }
 
 // Whether launch_impc defers agents (so launch_impc_fallback must follow): the separable kernel,
 // when its 16 CBF row slots can be exceeded (caller lists, or k nearest x CBF samples > 16).
 bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k) {
-    if (op.slack_mode) return false;
+    if (op.slack_mode)
+        return op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2 && (csr || knn_k > 16);
     if (!(variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)) return false;
     return csr || knn_k * op.cbf_h > 16;
 }

@@ -1278,6 +1278,32 @@ int impc(const orc_params* p, int N, const double* states, int self, int nb, con
         }
         DenseQP q = as.build(st, ref, nb, nbs.data(), sw.data(), it, pred.data());
         Solution sol = solve(q);
+        if (p->slack_mode && sol.status == ORC_OPTIMAL && nb > 0) {
+            // slack polish: at the optimum v_i = max(0, max over its rows of the control points'
+            // excess g x - h) exactly. The dense solve stops on a dual residual relative to the
+            // largest slack cost, so a slack with a tiny weight (decay^rank down to 1e-14) whose
+            // rows have astronomically far bounds (h ~ 1e26, 5 h^3 of a distant neighbour) can
+            // stall far above that minimum: visible in the objective, not in the curve.
+            const int ncp = n - nb;
+            for (int j = ncp; j < n; j++) {
+                double v = 0.0;
+                for (int r = 0; r < q.m; r++) {
+                    const double a = q.A[(size_t)r * n + j];
+                    if (!(a < 0.0) || is_pos_inf(q.hi[r])) continue;
+                    double gx = 0.0;
+                    for (int k = 0; k < ncp; k++) gx += q.A[(size_t)r * n + k] * sol.x[k];
+                    v = std::max(v, (gx - q.hi[r]) / -a);
+                }
+                sol.x[j] = v;
+            }
+            double ob = q.c0;
+            for (int i = 0; i < n; i++) {
+                double hx = 0.0;
+                for (int j = 0; j < n; j++) hx += q.H[(size_t)i * n + j] * sol.x[j];
+                ob += sol.x[i] * hx + q.c[i] * sol.x[i];
+            }
+            sol.obj = ob;
+        }
         attempted++;
         status[it] = sol.status;
         obj[it] = sol.obj;
