@@ -52,4 +52,6 @@ pmc fov_mfma --workload fov -- $SQM
 pmc fovs_fetch --workload fov --slack -- FETCH_SIZE
 pmc fovs_write --workload fov --slack -- WRITE_SIZE
 pmc fovs_mfma --workload fov --slack -- $SQM
+pmc collision_cache -- SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES
+step stamps; MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 $ROOT/tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1
 echo done
