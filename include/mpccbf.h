@@ -139,10 +139,10 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *               driver keeps, example :160-164); NaN if no iteration was OPTIMAL
  *   status      num_agents x impc_iter SolveStatus per IMPC iteration (UNKNOWN = not attempted)
  *   obj         num_agents x impc_iter optimal objective x^T H x + c^T x (CPLEX.cpp:144-146)
- *   iters       num_agents x impc_iter interior-point Newton steps of all attempts of that QP
- *               (a first attempt that started warm or stopped at the divergence test, plus its
- *               cold retry; 0 when the unconstrained minimiser satisfies every row; phase-1 steps
- *               not included)
+ *   iters       num_agents x impc_iter solver steps of that QP: dual active-set steps plus the
+ *               interior-point Newton steps of every PDIP attempt (when the active-set solve
+ *               gives up, or in slack mode); 0 when the unconstrained minimiser satisfies every
+ *               row; phase-1 steps not included
  *   primal_res, dual_res  num_agents x impc_iter: OPTIMAL — scaled primal residual
  *               max_i |r_i| / (1 + |bound_i|) over the condensed QP's rows (bounds every row's
  *               violation) and relative dual residual ||P y + q + G^T z||_inf / (1 + ||q||_inf)
