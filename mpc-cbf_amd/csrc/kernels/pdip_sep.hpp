@@ -433,6 +433,32 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         if (gl == owner) sep_stage_side<SB, CB>(rw, pi, sb, gl, cand);
         wave_lds_sync();
         GSTAMP(3, outer == 0);
+        if (k == 0) {
+            // first side of an empty active set: z = P^-1 n_p, the step reaches it (no factor yet),
+            // and L = (sqrt(g_p P^-1 g_p))
+            ++steps;
+            const double sp = cand[POL_SGN];
+            double nw = 0.0, gy = 0.0;
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) {
+                nw = fma(cand[j], cand[POL_W + j], nw);
+                gy = fma(cand[j], y[j], gy);
+            }
+            if (!(nw > 0.0)) return 0;
+            const double t = sp * (gy - cand[POL_B]) * rcp(nw);
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-t * sp, cand[POL_W + j], y[j]);
+            wave_lds_sync();
+            pol[gl] = cand[gl];
+            const double rz = rsqrt(nw);
+            L[S6::idx(0, 0)] = nw * rz;
+            dl[0] = rz;
+            u[0] = t;
+            k = 1;
+            wave_lds_sync();
+            GSTAMP(6, outer == 0);
+            continue;
+        }
         double up = 0.0;  // the candidate's multiplier
         for (;;) {
             if (++steps > maxstep) return 0;
@@ -638,7 +664,10 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             yu[o] = -fma(a, q[o], b * q[o + 1]);
             yu[o + 1] = -fma(b, q[o], c * q[o + 1]);
         }
-        bool bad = false;
+        // with the dual active-set solve on, its first scan is the fast-start test (an empty
+        // active set it returns unchanged): no separate row check
+        const bool das = !SLACK && cfg.dual_as > 0 && pol != nullptr;
+        bool bad = das;
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
@@ -646,7 +675,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 const double t = rw.bg[d][k][0] * yu[2 * d] + rw.bg[d][k][1] * yu[2 * d + 1];
                 bad = bad || !(t >= rw.blo[d][k] && t <= rw.bhi[d][k]);  // NaN-safe
             }
-        if (has_cbf) {
+        if (has_cbf && !das) {
 #pragma unroll
             for (int c = 0; c < CB; c++) {
                 double t = 0.0;
@@ -655,7 +684,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 bad = bad || !(t <= rw.chi[c]);
             }
         }
-        if (cfg.fast_start && grp_ballot<G>(bad) == 0ull) {
+        if (cfg.fast_start && !das && grp_ballot<G>(bad) == 0ull) {
 #pragma unroll
             for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
             if (v_out) *v_out = 0.0;
@@ -683,7 +712,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         // (no warm-start duals: the caller's PDIP attempts run cold when it is on)
         GSTAMP(13, true);
         if constexpr (!SLACK) {
-            if (cfg.dual_as > 0 && pol != nullptr) {
+            if (das) {
                 double yg[SEP_NZ], rpg = 0.0, rdg = 0.0;
                 const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, Pinv, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
                                                      rdg, as_steps, nullptr, cfg.want_rd, dbg);
