@@ -56,12 +56,13 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
 }
 
 // Returns 1: optimal (sc.y, rp_out, rd_out); -1: no step reaches the candidate (no feasible
-// point: phase 1 decides); 0: gave up (step limit, breakdown, dual residual) — the PDIP solves.
+// point; tlow = the certificate's lower bound on phase 1's t*); 0: gave up (step limit,
+// breakdown, dual residual) — the PDIP solves.
 // Pinv: P^-1 padded to 16 x 16 (global); P for the dual residual (want_rd).
 __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, WaveScratch& sc,
                               WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
                               double tol, int maxstep, bool want_rd, int lane, double& rp_out,
-                              double& rd_out, int& steps) {
+                              double& rd_out, int& steps, double& tlow) {
     const int i = lane & 15;
     steps = 0;
     for (int e = lane; e < WNZ * WNZ; e += 64) ws.Pi[(e >> 4) * 17 + (e & 15)] = Pinv[e];
@@ -138,7 +139,11 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
             const int l = t1 < 1e300 ? __ffsll((long long)grp_ballot<16>(ratio == t1)) - 1 : -1;
             const bool full = zn > 1e-10 * nw;  // else n_p lies in the span of the active sides
             const double t2 = full ? vp * rcp(zn) : 1e300;
-            if (l < 0 && !full) return -1;
+            if (l < 0 && !full) {
+                // certificate lam = (1, -r) >= 0 (every r <= 0): t* >= vp / (1 - sum r)
+                tlow = vp * rcp(1.0 + grp_sum<16>((i < k && r_i < 0.0) ? -r_i : 0.0));
+                return -1;
+            }
             const double t = fmin(t1, t2);
             if (full) {
                 double zi = sp * wi;

@@ -321,11 +321,11 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             // first attempt (no slack variables): the dual active-set solve; a QP it finds
             // without a feasible point goes to phase 1 directly, one it gives up on to the PDIP
             int das = 0, dsteps = 0;
-            double drp = 0.0, drd = 0.0;
+            double drp = 0.0, drd = 0.0, dtlow = 0.0;
             if constexpr (!SLACK) {
                 if (op.dual_as > 0)
                     das = das_solve_wave(rw, Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16), op.tol,
-                                         2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps);
+                                         2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps, dtlow);
             }
             bool settled = false;
             if (das == 1) {
@@ -333,6 +333,12 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 nit = dsteps;
                 prs = drp;
                 drs = drd;
+                settled = true;
+            } else if (das < 0 && dtlow > 10.0 * op.feas_tol) {
+                // the active set's infeasibility certificate bounds t* from below: no phase 1
+                st = ST_INFEASIBLE;
+                nit = dsteps;
+                prs = dtlow;
                 settled = true;
             } else if (das < 0) {
                 const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);

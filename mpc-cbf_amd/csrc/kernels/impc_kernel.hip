@@ -497,6 +497,13 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 total += po.iters;
                 ((attempt == 0 && warm_try) ? tr_warm : tr_cold) += po.iters;
                 if (po.status == ST_OPTIMAL) break;
+                if (!certified && po.tlow > 10.0 * op.feas_tol) {
+                    // the dual active set's infeasibility certificate bounds t* from below: no
+                    // phase 1 needed (a bound within 10x of the tolerance still goes to phase 1)
+                    tstar = po.tlow;
+                    infeas = true;
+                    certified = true;
+                }
                 if (!certified) {
                     SepRows<SB, CB> rp1 = rw;
                     if constexpr (SLACK) {  // slack rows are always satisfiable: certify the box rows

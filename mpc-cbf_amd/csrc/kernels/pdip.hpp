@@ -141,6 +141,9 @@ struct PdipOut {
     // iterate (mpccbf_batch.primal_res / dual_res); NaN otherwise
     double rp = __builtin_nan("");
     double rd = __builtin_nan("");
+    // stopped by the dual active set without a feasible point: a lower bound on phase 1's t*
+    // from the certificate sum_i lam_i n_i = 0, lam >= 0 (t* >= -sum lam b / sum lam)
+    double tlow = 0.0;
 };
 
 // step-to-boundary of s + a ds >= 0 (or z): returns the limiting a, or `big` if ds >= 0

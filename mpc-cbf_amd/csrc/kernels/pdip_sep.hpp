@@ -352,7 +352,8 @@ template <int G, int SB, int CB>
 __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                            const double* __restrict__ Pinv, const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
                            double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
-                           int& steps, SepWarm<SB>* warm, bool want_rd, long long* dbg = nullptr) {
+                           int& steps, SepWarm<SB>* warm, bool want_rd, double& tlow,
+                           long long* dbg = nullptr) {
     static_assert(G == 16, "rows of pol are copied one column per lane");
     (void)dbg;
     GSTAMP(0, true);
@@ -516,6 +517,15 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             const bool full = zn > 1e-10 * nw;  // else n_p lies in the span of the active sides
             const double t2 = full ? vp * rcp(zn) : 1e300;
             if (l < 0 && !full) {
+                // n_p = N_A r with every r <= 0: lam = (1, -r) >= 0 combines the sides to zero, and
+                // t* >= -sum lam b / sum lam = (n_p y - b_p) / (1 - sum r) (active sides exact at y)
+                double lsum = 1.0;
+#pragma unroll
+                for (int i = 0; i < POL_K; i++) {
+                    const double r = sgn[i] * rho[i];
+                    lsum += (i < k && r < 0.0) ? -r : 0.0;
+                }
+                tlow = vp * rcp(lsum);
 #pragma unroll
                 for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
                 wave_lds_sync();
@@ -713,9 +723,9 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
         GSTAMP(13, true);
         if constexpr (!SLACK) {
             if (das) {
-                double yg[SEP_NZ], rpg = 0.0, rdg = 0.0;
+                double yg[SEP_NZ], rpg = 0.0, rdg = 0.0, tlg = 0.0;
                 const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, Pinv, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
-                                                     rdg, as_steps, nullptr, cfg.want_rd, dbg);
+                                                     rdg, as_steps, nullptr, cfg.want_rd, tlg, dbg);
                 if (r != 0) {
                     PdipOut fo{r > 0 ? ST_OPTIMAL : ST_UNKNOWN, as_steps};
 #pragma unroll
@@ -726,6 +736,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                         fo.polished = true;
                     } else {
                         fo.early = true;  // no feasible point in sight: phase 1 decides
+                        fo.tlow = tlg;
                     }
                     return fo;
                 }
