@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(REPO, "mpc-cbf_amd"))
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (= matrix) peak, vendor spec
 HBM_PEAK_GBS = 8000.0
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions / s: 1024 SIMDs, one per 4 cycles at 2.4 GHz
 
 
 def parse():
@@ -320,7 +321,12 @@ def main():
         # average launch time (HIP events on the launch stream, every step of the replay)
         flops_per_launch = flops_rank0 / nsteps
         achieved_tf = flops_per_launch / (kern_avg * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic(kname, ("fovs" if args.slack else "fov") if fov else "collision")
+        wl = ("fovs" if args.slack else "fov") if fov else "collision"
+        traffic, traffic_src = pmc_traffic(kname, wl)
+        # VALU issue: the kernel is bound by dependent-instruction latency at one wave per SIMD;
+        # wave-level VALU instructions per launch (PMC SQ_INSTS_VALU) / launch time against the
+        # issue peak (every SIMD one wave64 VALU op per 4 cycles: 1024 SIMDs x 2.4 GHz / 4)
+        valu_insts, valu_src = pmc_lookup(kname, wl, "SQ_INSTS_VALU")
         abytes = algorithmic_bytes_per_agent(ctx.n, args.knn, cfg["impc_iter"], cov is not None) * per
         bound = "mfma" if kname.startswith("impc_fov") else "valu"
         res = {
@@ -390,6 +396,12 @@ def main():
                 "flops_model": "executed solver steps (dual active-set + PDIP Newton) x the FP64 flops "
                                "of an active-set step (bench.py flops_per_qp_sep, a lower bound); QPs "
                                "solved by the fast start count 0",
+                "valu_issue": (None if valu_insts is None else {
+                    "insts_per_launch": valu_insts,
+                    "achieved_per_s": valu_insts / (kern_avg * 1e-3),
+                    "peak_per_s": VALU_ISSUE_PEAK,
+                    "frac": valu_insts / (kern_avg * 1e-3) / VALU_ISSUE_PEAK,
+                    "source": valu_src}),
                 "hbm": {"algorithmic_bytes_per_launch": abytes,
                         "achieved_gbs": abytes / (kern_avg * 1e-3) / 1e9,
                         "peak_gbs": HBM_PEAK_GBS,
@@ -406,17 +418,21 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kname: str, workload: str):
-    """HBM bytes per launch of kernel `kname` under `workload` ("collision", "fov", "fovs") from
-    the newest committed PMC summary (profiles/r*_pmc_summary.json: rocprofv3 --pmc FETCH_SIZE /
-    WRITE_SIZE passes of this bench, gfx950-corrected by tools/pmc_summary.py). The counters
-    cannot be read inside a timed run, so the value comes from the separate counter passes of
-    the same command; None if absent."""
+def pmc_lookup(kname: str, workload: str, field: str):
+    """Counter-derived `field` of kernel `kname` under `workload` ("collision", "fov", "fovs") from
+    the newest committed PMC summary (profiles/r*_pmc_summary.json: rocprofv3 --pmc passes of
+    this bench, gfx950-corrected by tools/pmc_summary.py). The counters cannot be read inside a
+    timed run, so the value comes from the separate counter passes of the same command; the
+    kernel's own name may carry defaulted template arguments (", false>"). (None, None) if absent."""
     import glob
     key = kname.replace(" ", "")
 
     def norm(n):
         return n.replace(" ", "").replace("void", "").replace("mpccbf::dev::", "")
+
+    def match(name):
+        n = norm(name)
+        return n == key or (n.startswith(key[:-1] + ",") and n.endswith(">") and key.endswith(">"))
 
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
         try:
@@ -426,9 +442,14 @@ def pmc_traffic(kname: str, workload: str):
         tables = [d[workload]] if isinstance(d.get(workload), dict) else [d]
         for t in tables:
             for name, v in t.items():
-                if isinstance(v, dict) and norm(name) == key and "hbm_bytes_per_launch_corrected" in v:
-                    return float(v["hbm_bytes_per_launch_corrected"]), os.path.relpath(f, REPO)
+                if isinstance(v, dict) and match(name) and field in v:
+                    return float(v[field]), os.path.relpath(f, REPO)
     return None, None
+
+
+def pmc_traffic(kname: str, workload: str):
+    """HBM bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, KiB -> bytes) from the PMC summary."""
+    return pmc_lookup(kname, workload, "hbm_bytes_per_launch_corrected")
 
 
 def cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h=None):

@@ -33,6 +33,21 @@ struct FovSlackLds {
     int32_t order[WSL_NB];
 };
 
+// Position of observed neighbour i: from the neighbour query's LDS copy in grid mode, else the
+// state table.
+__device__ __forceinline__ void nb_position(const ImpcArgs& args, const NbScratch& sc, bool grid_mode, int nb0,
+                                            int i, double& px, double& py) {
+    if (grid_mode) {
+        const int c = sc.src[i];
+        px = sc.cst[0][c];
+        py = sc.cst[1][c];
+    } else {
+        const int nbi = args.nb_col[nb0 + i];
+        px = args.states[(size_t)nbi * 6];
+        py = args.states[(size_t)nbi * 6 + 1];
+    }
+}
+
 template <bool SLACK>
 __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const double* __restrict__ buf,
                                                        const ImpcArgs args) {
@@ -148,8 +163,8 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         const int nvor = nnb * C;
         for (int v = lane; v < nvor; v += 64) {
             const int i = v / C, j = v % C;
-            const int nbi = grid_mode ? nb_scratch.idx[i] : args.nb_col[nb0 + i];
-            const double ox = args.states[(size_t)nbi * 6], oy = args.states[(size_t)nbi * 6 + 1];
+            double ox, oy;
+            nb_position(args, nb_scratch, grid_mode, nb0, i, ox, oy);
             double nx = ox - s0[0], ny = oy - s0[1];
             const double nrm = sqrt(nx * nx + ny * ny);
             if (nrm > 0.0) {
@@ -198,14 +213,13 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 i = task / (4 * nk);
                 kind = (task / nk) % 4;
                 k = task % nk;
-                const int nbi = grid_mode ? nb_scratch.idx[i] : args.nb_col[nb0 + i];
-                double e[6], yk[NZ];
+                double e[6], yk[NZ], npx, npy;
+                nb_position(args, nb_scratch, grid_mode, nb0, i, npx, npy);
 #pragma unroll
                 for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
                 cbf_ego_state<NZ>(op, buf, it, k, s0, yk, e);
                 bool present;
-                fov_cbf_row(kind, e, args.states[(size_t)nbi * 6], args.states[(size_t)nbi * 6 + 1],
-                            op.fov_beta, op.fov_Ds, op.fov_Rs, a, bb, present);
+                fov_cbf_row(kind, e, npx, npy, op.fov_beta, op.fov_Ds, op.fov_Rs, a, bb, present);
                 double bmax = 0.0, bmin = 0.0;
 #pragma unroll
                 for (int d = 0; d < 3; d++) {
