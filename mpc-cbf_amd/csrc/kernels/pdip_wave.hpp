@@ -344,6 +344,13 @@ __device__ __forceinline__ double solve_rows(const double (&L)[WNZ], const doubl
     return xl;
 }
 
+// a load the compiler may not hoist out of the enclosing loop (keeps a loop-invariant row out of
+// the registers: the "memory" clobber orders it after every earlier store)
+__device__ __forceinline__ double ldg_nohoist(const double* p) {
+    asm volatile("" ::: "memory");
+    return *p;
+}
+
 // publish a row-layout vector as a wave-uniform LDS copy
 __device__ __forceinline__ void publish16(double* __restrict__ dst, double v, int lane) {
     if (lane < WNZ) dst[lane] = v;
@@ -417,9 +424,9 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
     }
     const double inv_ns = rcp(wave_reduce<Op::Sum>(nloc));
     const double inv_qn = rcp(1.0 + grp_max<16>(fabs(qi)));
-    double Prow[WNZ];  // row i of P
-#pragma unroll
-    for (int k = 0; k < WNZ; k++) Prow[k] = P[i * WNZ + k];
+    // row i of P is re-read where it is used (L2-resident, 2 KB for the whole launch) instead of
+    // held in 32 registers across the Newton loop
+    const double* __restrict__ Prow = P + i * WNZ;
 
     PdipOut out{ST_UNKNOWN, 0};
     double mu0 = 1.0, rd_track = 1e300;
@@ -488,10 +495,12 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
         const double rhs_i = Mr[WNZ - 1];  // G^T w (column 15)
         PSTAMP(2);
 #pragma unroll
-        for (int k = 0; k < WNZ; k++) Mr[k] = (k == WNZ - 1 && i != WNZ - 1 ? 0.0 : Mr[k]) + Prow[k];
+        for (int k = 0; k < WNZ; k++) Mr[k] = (k == WNZ - 1 && i != WNZ - 1 ? 0.0 : Mr[k]) + ldg_nohoist(Prow + k);
         wave_reduce2<Op::Sum, Op::Max>(mloc, rp);
         const double mu = mloc * inv_ns;
-        const double py_i = dotr(Prow, sc.y) + qi;  // (P y + q)_i
+        double py_i = qi;  // (P y + q)_i
+#pragma unroll
+        for (int k = 0; k < WNZ; k++) py_i = fma(ldg_nohoist(Prow + k), sc.y[k], py_i);
         // exact relative dual residual; slack mode adds the slack rows (original g, weights z) and
         // the v equations w - sum_a z_a - zb (relative to 1 + w)
         auto dual_res = [&]() {
