@@ -27,8 +27,9 @@ struct WaveAS {
     double Pi[WNZ * 17];     // P^-1, rows padded to 17 doubles (lane i reads row i: spread banks)
     double w[WNZ];           // the candidate's P^-1 g
     double b[WNZ], sg[WNZ];  // active rows' bound and side sign (+1 upper, -1 lower)
-    double u[WNZ];           // multipliers (shift scratch)
+    double u[WNZ];           // multipliers (shift scratch; at the optimum: the active rows')
     int32_t row[WNZ];        // active rows' image row
+    int32_t k;               // at the optimum: the number of active rows
 };
 
 // first half of solve_rows: v = L^-1 b on the row layout
@@ -55,7 +56,7 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
     return xl;
 }
 
-// Returns 1: optimal (sc.y, rp_out, rd_out); -1: no step reaches the candidate (no feasible
+// Returns 1: optimal (sc.y, rp_out, rd_out; the active rows' multipliers in ws.u[0 .. ws.k)); -1: no step reaches the candidate (no feasible
 // point; tlow = the certificate's lower bound on phase 1's t*); 0: gave up (step limit,
 // breakdown, dual residual) — the PDIP solves.
 // Pinv: P^-1 padded to 16 x 16 (global); P for the dual residual (want_rd).
@@ -63,9 +64,9 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
                               WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
                               double tol, int maxstep, bool want_rd, int lane, double& rp_out,
                               double& rd_out, int& steps, double& tlow) {
-    const int i = lane & 15;
+    const int i = lane16_opaque(lane);
     steps = 0;
-    for (int e = lane; e < WNZ * WNZ; e += 64) ws.Pi[(e >> 4) * 17 + (e & 15)] = Pinv[e];
+    for (int e = lane; e < WNZ * WNZ; e += 64) ws.Pi[(e >> 4) * 17 + (e & 15)] = ldg_nohoist(Pinv + e);
     // per-slot violation scales, the factor of the empty active set (identity)
     double pl[WR], pu[WR];
 #pragma unroll
@@ -78,7 +79,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
     for (int k = 0; k < WNZ; k++) L[k] = k == i ? 1.0 : 0.0;
     if (lane < WNZ) {
 #pragma unroll
-        for (int k = 0; k < WNZ; k++) sc.M[lane * WNZ + k] = k == lane ? 1.0 : 0.0;
+        for (int k = 0; k < WNZ; k++) sc.M[i * WNZ + k] = k == i ? 1.0 : 0.0;
     }
     wave_lds_sync();
     // y = -P^-1 q
@@ -213,7 +214,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
     if (want_rd) {
         double r = sc.q[i];
 #pragma unroll
-        for (int j = 0; j < WNZ; j++) r = fma(P[i * WNZ + j], sc.y[j], r);
+        for (int j = 0; j < WNZ; j++) r = fma(ldg_nohoist(P + i * WNZ + j), sc.y[j], r);
 #pragma unroll
         for (int a = 0; a < WNZ - 1; a++) {
             const double la = bcast16v(a, ui * (i < k ? ws.sg[i < k ? i : 0] : 0.0));
@@ -223,6 +224,8 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         rd = grp_max<16>(fabs(r)) * rcp(1.0 + grp_max<16>(qn));
         if (!(rd <= tol)) return 0;
     }
+    if (lane < WNZ) ws.u[lane] = i < k ? ui : 0.0;
+    if (lane == 0) ws.k = k;
     rp_out = fmax(m, 0.0);
     rd_out = rd;
     return 1;

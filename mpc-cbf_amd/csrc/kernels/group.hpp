@@ -17,6 +17,16 @@
 namespace mpccbf {
 namespace dev {
 
+// threadIdx.x & M as a value the compiler cannot see through: lane masks derived from it are
+// formed inside each solve instead of hoisted out of the callers' loops, where they stay live
+// across everything and spill
+template <int M>
+__device__ __forceinline__ int lane_bits_opaque() {
+    int r;
+    asm volatile("v_and_b32 %0, %1, %2" : "=v"(r) : "i"(M), "v"((int)threadIdx.x));
+    return r;
+}
+
 constexpr int DPP_XOR1 = 0xB1;         // quad_perm(1,0,3,2)
 constexpr int DPP_XOR2 = 0x4E;         // quad_perm(2,3,0,1)
 constexpr int DPP_HALF_MIRROR = 0x141; // row_half_mirror

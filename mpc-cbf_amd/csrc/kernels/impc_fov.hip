@@ -31,6 +31,7 @@ struct FovSlackLds {
     double h[WSL_ROWS], live[WSL_ROWS];
     double Tn[WSL_NB], w[WSL_NB], dist[WSL_NB];
     int32_t order[WSL_NB];
+    int32_t rown[WSL_ROWS];  // FoV row compacted after the ordinary image -> its neighbour
 };
 
 // Position of observed neighbour i: from the neighbour query's LDS copy in grid mode, else the
@@ -154,6 +155,9 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     const int C = op.C;
 
     for (int it = 0; it < op.impc_iter; it++) {
+        // (keeps the operator tables' loads inside the iteration: hoisted out of it they stay live
+        // across the solves and spill)
+        asm volatile("" ::: "memory");
         const size_t oi = (size_t)ai * op.impc_iter + it;
         if (!success) {
             write_iteration(args, oi, lane, ST_UNKNOWN, __builtin_nan(""), 0);
@@ -292,16 +296,22 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
         } else {
-            WaveRows rw;
+            // the row slots of the first mr image rows
+            // (re-read at every use: the compiler would otherwise keep the slots live across solves)
+            auto image_rows = [&](int mr) {
+                asm volatile("" ::: "memory");
+                WaveRows rw;
 #pragma unroll
-            for (int s = 0; s < WR; s++) {
-                const int r = wave_owner_row(lane, s);
-                const bool on = r < mtot;
-                rw.g[s] = on ? &Gimg[r * WNZ] : zero_row;
-                rw.lo[s] = on ? rlo[r] : -1.0;
-                rw.hi[s] = on ? rhi[r] : 1.0;
-                rw.ml[s] = on ? rml[r] : 1.0;
-            }
+                for (int s = 0; s < WR; s++) {
+                    const int r = wave_owner_row(lane, s);
+                    const bool on = r < mr;
+                    rw.g[s] = on ? &Gimg[r * WNZ] : zero_row;
+                    rw.lo[s] = on ? rlo[r] : -1.0;
+                    rw.hi[s] = on ? rhi[r] : 1.0;
+                    rw.ml[s] = on ? rml[r] : 1.0;
+                }
+                return rw;
+            };
 #ifdef MPCCBF_PDIP_STAMPS
             long long* dbg = (args.stamps && it == 0)
                                  ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 16
@@ -313,6 +323,55 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
 #else
             long long* dbg = nullptr;
 #endif
+            // first attempt: the dual active-set solve; a QP it finds without a feasible point goes
+            // to phase 1 directly, one it gives up on to the PDIP
+            int das = 0, dsteps = 0;
+            double drp = 0.0, drd = 0.0, dtlow = 0.0;
+            if constexpr (!SLACK) {
+                if (op.dual_as > 0)
+                    das = das_solve_wave(image_rows(mtot), Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16),
+                                         op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps,
+                                         dtlow);
+            } else {
+                // slack mode: the QP with every v = 0 (its FoV rows hard, compacted after the ordinary
+                // image) by the dual active set. Its optimum is the slack QP's when each neighbour's
+                // FoV multipliers sum to at most its slack cost (stationarity in v_i: w_i - sum lam =
+                // mu_i >= 0); otherwise, and when that QP has no feasible point, the slack PDIP solves.
+                const bool lv = slk->live[lane] != 0.0;
+                const unsigned long long lm = __ballot(lv);
+                const int ncbf = __popcll(lm);
+                if (op.dual_as > 0 && mtot + ncbf <= WROWS) {
+                    if (lv) {
+                        const int c = __popcll(lm & ((1ull << lane) - 1ull)), r = mtot + c;
+#pragma unroll
+                        for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = slk->Go[lane * WNZ + j];
+                        rlo[r] = 0.0;
+                        rml[r] = 0.0;
+                        rhi[r] = slk->h[lane];
+                        slk->rown[c] = lane >> 3;
+                    }
+                    wave_lds_sync();
+                    das = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
+                                         opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane,
+                                         drp, drd, dsteps, dtlow);
+                    if (das == 1) {
+                        wave_lds_sync();
+                        double lam = 0.0;
+                        if (lane < nnb) {
+                            for (int a = 0; a < was.k; a++) {
+                                const int r = was.row[a];
+                                if (r >= mtot && slk->rown[r - mtot] == lane) lam += was.u[a];
+                            }
+                        }
+                        if (__ballot(lane < nnb && !(lam <= slk->w[lane])) != 0ull) das = 0;
+                    }
+                    if (das != 1) {
+                        das = 0;
+                        for (int e = lane; e < ncbf * WNZ; e += 64) Gimg[mtot * WNZ + e] = 0.0;
+                        wave_lds_sync();
+                    }
+                }
+            }
             WaveSlack sk{};
             if constexpr (SLACK) {
                 wave_lds_sync();  // the slack rows written above
@@ -332,15 +391,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 sk.live = slk->live[lane];
                 sk.w = (lane >> 3) < nnb ? slk->w[lane >> 3] : 0.0;
             }
-            // first attempt (no slack variables): the dual active-set solve; a QP it finds
-            // without a feasible point goes to phase 1 directly, one it gives up on to the PDIP
-            int das = 0, dsteps = 0;
-            double drp = 0.0, drd = 0.0, dtlow = 0.0;
-            if constexpr (!SLACK) {
-                if (op.dual_as > 0)
-                    das = das_solve_wave(rw, Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16), op.tol,
-                                         2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps, dtlow);
-            }
             bool settled = false;
             if (das == 1) {
                 st = ST_OPTIMAL;
@@ -355,7 +405,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 prs = dtlow;
                 settled = true;
             } else if (das < 0) {
-                const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);
+                const double tstar = pdip_phase1_wave(image_rows(mtot), Gimg, nchunk, sc, NZ, cfg, lane);
                 if (tstar > op.feas_tol && tstar < 1e300) {  // (1e300: phase 1 failed, the PDIP decides)
                     st = ST_INFEASIBLE;
                     nit = dsteps;
@@ -364,7 +414,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 }
             }
             if (!settled) {
-                const PdipOut po = pdip_solve_wave<SLACK>(rw, Gimg, nchunk, sc, opp(buf, op.o_P16),
+                const PdipOut po = pdip_solve_wave<SLACK>(image_rows(mtot), Gimg, nchunk, sc, opp(buf, op.o_P16),
                                                           opp(buf, op.o_LP16), cfg, lane, dbg, &sk, &vobj);
                 st = po.status;
                 nit = dsteps + po.iters;
@@ -373,7 +423,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 // slack mode: the slack rows are always satisfiable, phase 1 certifies the box and
                 // Voronoi rows (the ordinary image)
                 if (st != ST_OPTIMAL) {
-                    const double tstar = pdip_phase1_wave(rw, Gimg, nchunk, sc, NZ, cfg, lane);
+                    const double tstar = pdip_phase1_wave(image_rows(mtot), Gimg, nchunk, sc, NZ, cfg, lane);
                     if (tstar > op.feas_tol) {
                         st = ST_INFEASIBLE;
                         prs = tstar;

@@ -147,7 +147,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
                                const double* __restrict__ pol, const double (&sc)[2 * SEP_D * SB + CB],
                                double tol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
                                SepWarm<SB>* warm) {
-    const int gl = threadIdx.x & (G - 1);
+    const int gl = lane_bits_opaque<G - 1>();
     using S6 = Sym<POL_K>;
     double K[S6::P], rhs[POL_K], dk[POL_K], lam[POL_K];
 #pragma unroll
@@ -254,7 +254,7 @@ __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double
                            const double (&pl)[SEP_D][SB], const double (&pu)[SEP_D][SB],
                            const double (&pc)[CB], double tol, double* __restrict__ pol,
                            double (&yo)[SEP_NZ], double& rp_out, double& rd_out, SepWarm<SB>* warm) {
-    const int gl = threadIdx.x & (G - 1);
+    const int gl = lane_bits_opaque<G - 1>();
     double pi[SEP_D][3], yu[SEP_NZ];
     sep_pinv(Pinv, pi);
 #pragma unroll
@@ -360,7 +360,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #ifdef MPCCBF_PDIP_STAMPS
     if (dbg) dbg[15] = 1;
 #endif
-    const int gl = threadIdx.x & (G - 1);
+    const int gl = lane_bits_opaque<G - 1>();
     double pi[SEP_D][3];
     sep_pinv(Pinv, pi);
     constexpr int NS = 2 * SEP_D * SB + CB;
@@ -1365,7 +1365,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
     }
 #ifdef MPCCBF_DEBUG_EXIT
     if (dbg) {  // per-lane exit iteration (all lanes of a group must agree)
-        const int gl = threadIdx.x & (G - 1);
+        const int gl = lane_bits_opaque<G - 1>();
         dbg[16 * 64 + gl] = out.iters;  // caller's buffer: + num_agents * 16 slots (see dbg_slack.py)
     }
 #endif
@@ -1442,7 +1442,7 @@ __device__ double pdip_phase1_sep(const SepRows<SB, CB>& rw, const PdipCfg cfg, 
     }
     double zt = rcp(t);
     const double inv_ns = 1.0 / (double)(G * (2 * SEP_D * SB + CB) + 1);
-    const int gl = threadIdx.x & (G - 1);
+    const int gl = lane_bits_opaque<G - 1>();
     int it = 0;
     for (; it < 2 * cfg.maxit; it++) {
         double acc[P_N];

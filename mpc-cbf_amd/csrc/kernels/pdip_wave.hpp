@@ -294,12 +294,21 @@ __device__ __forceinline__ void gram_rows(const wd4 acc, double* __restrict__ Mb
     wave_lds_sync();
 }
 
+// lane & 15 as a value the compiler cannot see through: the lane masks derived from it (i == k
+// for every k) are then formed inside each solve instead of hoisted out of the caller's loops,
+// where 16 of them stay live across everything and spill
+__device__ __forceinline__ int lane16_opaque(int lane) {
+    int i;
+    asm volatile("v_and_b32 %0, 15, %1" : "=v"(i) : "v"(lane));
+    return i;
+}
+
 // Left-looking Cholesky on the row layout: lane i holds row i of M (k <= i used) and gets row i
 // of L and inv_i = 1 / L_ii; L's rows are then stored to Mbuf (row-major) for the backward
 // solves. Returns false if a pivot is not positive.
 __device__ __forceinline__ bool chol_rows(const double (&M)[WNZ], double (&L)[WNZ], double& inv_i,
                                           double* __restrict__ Mbuf, int lane) {
-    const int i = lane & 15;
+    const int i = lane16_opaque(lane);
     bool ok = true;
     inv_i = 0.0;
 #pragma unroll
@@ -369,7 +378,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
     (void)dbg;
     (void)skp;
     (void)v_obj;
-    const int i = lane & 15;
+    const int i = lane16_opaque(lane);
     const double qi = sc.q[i];
     double L[WNZ], inv_i;
     // ---- start: y0 = -P^{-1} q with the factor of P
@@ -731,7 +740,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
 __device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
                                    WaveScratch& sc, int nz, const PdipCfg cfg, int lane) {
     constexpr double eps = 1e-10;
-    const int i = lane & 15;
+    const int i = lane16_opaque(lane);
     double vi = 0.0;  // y_i (i < 15) on the row layout
     publish16(sc.y, 0.0, lane);
     double viol = 0.0, nloc = 0.0;

@@ -5,6 +5,9 @@ for an offline oracle check (--check).
 
     python tools/fov_status_check.py [steps] [out.npz]          (GPU)
     python tools/fov_status_check.py --check out.npz            (CPU: oracle on the mismatches)
+
+MPCCBF_CHECK_SLACK=1 runs the FoV slack setting (slack_cost 1000, decay 0.9, covariances 0.1 I)
+instead; the objectives of agents solved by both are compared too.
 """
 import os
 import sys
@@ -16,10 +19,18 @@ sys.path.insert(0, os.path.join(REPO, "mpc-cbf_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 
+SLACK = os.environ.get("MPCCBF_CHECK_SLACK") == "1"
+
+
+def fov_cfg(swarm):
+    over = dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.9) if SLACK else {}
+    return swarm.fov_config(20, **over)
+
+
 def run(steps, out):
     import torch
     from mpccbf import Context, swarm
-    cfg = swarm.fov_config(20)
+    cfg = fov_cfg(swarm)
     states, targets = swarm.heading_swarm(512)
     dev = torch.device("cuda", 0)
     os.environ["MPCCBF_DUAL_AS"] = "0"
@@ -33,6 +44,9 @@ def run(steps, out):
     traj_t = torch.full((512,), -1.0, dtype=torch.float64, device=dev)
     o["x"].fill_(float("nan"))
     common = dict(targets=tg, knn_k=8, knn_radius=cfg["fov_Rs"])
+    if SLACK:
+        common["cov"] = torch.tensor(np.tile([0.1, 0.0, 0.1], (512, 1)), dtype=torch.float64, device=dev)
+    objdiff = 0.0
     saved = {}
     nmis = 0
     for s in range(steps):
@@ -42,7 +56,19 @@ def run(steps, out):
                        vel_std=0.01, noise_seed=20251015, **common)
         torch.cuda.synchronize()
         a, b = o["status"].cpu().numpy(), op["status"].cpu().numpy()
-        mis = np.nonzero(np.any(a != b, axis=1))[0]
+        both = (a == 0) & (b == 0)
+        if both.any():
+            oa, ob = o["obj"].cpu().numpy(), op["obj"].cpu().numpy()
+            rel = np.where(both, np.abs(oa - ob) / (1.0 + np.abs(ob)), 0.0)
+            w = np.unravel_index(np.argmax(rel), rel.shape)
+            if rel[w] > objdiff:  # keep the worst agent's inputs for the oracle (--check)
+                objdiff = float(rel[w])
+                saved["worst_states"] = cur.cpu().numpy()
+                saved["worst_agent"] = np.array([w[0], w[1]])
+                saved["worst_obj"] = np.array([oa[w], ob[w]])
+        # (failed solves of the default context count too: UNKNOWN where an attempt was made)
+        failed = (a[:, 0] == 5) | ((a[:, 0] == 0) & (a[:, 1] == 5))
+        mis = np.nonzero(np.any(a != b, axis=1) | failed)[0]
         if len(mis):
             nmis += len(mis)
             saved[f"states_{s}"] = cur.cpu().numpy()
@@ -53,17 +79,19 @@ def run(steps, out):
                 f"{i}: das {a[i].tolist()} pdip {b[i].tolist()}" for i in mis[:6]), flush=True)
         cur = o["next_states"].clone()
         if s % 100 == 0:
-            print(f"step {s}: das hist {np.bincount(a.ravel(), minlength=6).tolist()}", flush=True)
+            print(f"step {s}: das hist {np.bincount(a.ravel(), minlength=6).tolist()} "
+                  f"max rel objective difference {objdiff:.3g}", flush=True)
     np.savez_compressed(out, targets=targets, **saved)
-    print("mismatching agent-steps", nmis, "saved", out)
+    print("mismatching agent-steps", nmis, "max rel objective difference", objdiff, "saved", out)
 
 
 def check(path):
     import oracle_lib as O
     from mpccbf import swarm
     d = np.load(path)
-    cfg = swarm.fov_config(20)
+    cfg = fov_cfg(swarm)
     p = O.make_params(cfg)
+    covs = np.tile([0.1, 0.0, 0.1], (512, 1)) if SLACK else None
     refs = swarm.refs_from_targets(d["targets"], cfg["k_hor"])
     tally = {}
     for key in d.files:
@@ -73,11 +101,18 @@ def check(path):
         states = d[f"states_{s}"]
         rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
         for a in d[key]:
-            r = O.impc_optimize(p, states, int(a), col[rp[a]:rp[a + 1]], refs[a])
+            r = O.impc_optimize(p, states, int(a), col[rp[a]:rp[a + 1]], refs[a], covs)
             k = (tuple(d[f"das_{s}"][a]), tuple(d[f"pdip_{s}"][a]), tuple(r["status"]))
             tally[k] = tally.get(k, 0) + 1
     for k, v in sorted(tally.items(), key=lambda kv: -kv[1]):
         print(f"das {k[0]} pdip {k[1]} oracle {k[2]}: {v}")
+    if "worst_agent" in d.files:  # the largest objective difference: which solve is the oracle's
+        states = d["worst_states"]
+        a, it = (int(v) for v in d["worst_agent"])
+        rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+        r = O.impc_optimize(p, states, a, col[rp[a]:rp[a + 1]], refs[a], covs)
+        print(f"largest objective difference: agent {a} iteration {it}: das-first {d['worst_obj'][0]!r} "
+              f"pdip {d['worst_obj'][1]!r} oracle {r['obj'][it]!r} (status {r['status'].tolist()})")
 
 
 if __name__ == "__main__":
