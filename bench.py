@@ -41,9 +41,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--workload", choices=["collision", "fov"], default="collision",
+    ap.add_argument("--workload", choices=["collision", "fov", "dense"], default="collision",
                     help="collision: BASELINE config 3/4 (ConnectivityIMPCCBF); fov: config 5 "
-                         "(FovBezierIMPCCBF, horizon 20, 4 Bezier pieces)")
+                         "(FovBezierIMPCCBF, horizon 20, 4 Bezier pieces); dense: the generic "
+                         "qpcpp::Solver path (mpccbf_qp_solve_dense_batch) on the golden QPs")
     ap.add_argument("--agents-per-gpu", type=int, default=0,
                     help="default 4096 (collision), 512 (fov: config 5 = 4096 agents on 8 GPUs)")
     ap.add_argument("--agents-total", type=int, default=0, help="strong scaling: fixed total")
@@ -118,9 +119,73 @@ def algorithmic_bytes_per_agent(n: int, knn: int, impc_iter: int, cov: bool) -> 
     return 48 + 24 + 32 * knn + 8 * n + 16 * impc_iter + 48 + 16 + (24 * knn if cov else 0)
 
 
+def run_dense(args) -> None:
+    """--workload dense: the generic path a qpcpp::Solver<double> adapter calls in place of
+    CPLEXSolver::solve (qpcpp/src/solvers/CPLEX.cpp:35-177) — mpccbf_qp_solve_dense_batch on the
+    42 golden MPC-CBF QPs in their full CPLEX form (36 variables, 30 equalities, box + CBF rows),
+    replicated to --agents-per-gpu QPs per call (default 4096). The boundary takes host arrays, so
+    the rate includes the transfers both ways and the host-side packing. Also reported: the
+    single-QP latency (mpccbf_qp_solve_dense, one synchronous call) and the CPU oracle's dense
+    solve of the same QPs. Replicas only: no multi-GPU form."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        sys.exit("bench.py --workload dense: single GPU only")
+    import torch
+    from mpccbf import _lib as L
+    torch.cuda.set_device(0)
+    g = np.load(os.path.join(REPO, "tests", "golden", "golden_qps.npz"))
+    count = int(g["count"])
+    qps = [dict(H=g[f"c{i}_H"], c=g[f"c{i}_c"], A=g[f"c{i}_A"], lo=g[f"c{i}_lo"], hi=g[f"c{i}_hi"])
+           for i in range(count)]
+    ref = np.array([float(g[f"c{i}_obj"]) for i in range(count)])
+    batch = args.agents_per_gpu if args.agents_per_gpu > 0 else 4096
+    big = [qps[i % count] for i in range(batch)]
+    for _ in range(args.warmup):
+        L.dense_qp_solve_batch(big)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st, xs, obj = L.dense_qp_solve_batch(big)
+    dt = time.perf_counter() - t0
+    refb = ref[np.arange(batch) % count]
+    rel = np.abs(obj - refb) / np.maximum(1.0, np.abs(refb))
+    single = []
+    for q in qps:
+        t1 = time.perf_counter()
+        s1, _, o1 = L.dense_qp_solve(**q)
+        single.append(time.perf_counter() - t1)
+    hist = {STATUS_NAMES.get(int(k), str(int(k))): int(v) for k, v in zip(*np.unique(st, return_counts=True))}
+    line = {"metric": "dense_qps_per_sec", "value": batch * args.steps / dt, "unit": "QP/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": 1e3 * dt / args.steps, "higher_is_better": True, "scaling": "replicas",
+            "vs_baseline": None, "dtype": "f64", "data": "golden QPs (tests/golden/golden_qps.npz)",
+            "config": {"workload": f"generic dense path: {batch} QPs per call ({count} golden MPC-CBF QPs "
+                                   "replicated), n=36, 30 equalities, host arrays in/out"},
+            "status_hist": hist, "max_rel_obj_err_vs_golden": float(rel.max()),
+            "single_qp_latency_ms": {"median": 1e3 * float(np.median(single)),
+                                     "max": 1e3 * float(np.max(single))}}
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import oracle_lib as O
+        big_ = np.finfo(np.float64).max
+        oqs = [dict(n=q["c"].shape[0], H=q["H"], c=q["c"], A=q["A"], lo=q["lo"], hi=q["hi"],
+                    vlo=np.full(q["c"].shape[0], -big_), vhi=np.full(q["c"].shape[0], big_)) for q in qps]
+        n_cpu, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < 5.0:
+            for q in oqs:
+                O.solve_dense_qp(q)
+            n_cpu += len(oqs)
+        tc = time.perf_counter() - t1
+        line["cpu_baseline"] = {"value": n_cpu / tc, "unit": "QP/s", "cores": 1, "kind": "port",
+                                "sample": f"{n_cpu} solves of the {count} golden QPs (oracle dense "
+                                          "Mehrotra PDIP + active-set polish)"}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     spawn_ranks(args)
+    if args.workload == "dense":
+        run_dense(args)
+        return
     import torch
     import torch.distributed as dist
     from mpccbf import swarm, Context, Comm, comm_unique_id

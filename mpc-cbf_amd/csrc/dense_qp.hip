@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mpccbf.h"
@@ -127,13 +128,32 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
                                 double* obj_out, int32_t* status_out) {
     if (count < 0 || (count > 0 && (!qps || !status_out)))
         return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "dense QP batch: null argument");
+    // exact equality elimination on the host, QPs split over up to 16 threads (independent)
     std::vector<ReducedQP> red(count);
-    for (int k = 0; k < count; k++) {
-        try {
-            red[k] = reduce_dense_qp(qps[k]);
-        } catch (const std::exception& e) {
-            return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + e.what());
+    std::vector<std::string> err(count);
+    auto reduce_range = [&](int k0, int k1) {
+        for (int k = k0; k < k1; k++) {
+            try {
+                red[k] = reduce_dense_qp(qps[k]);
+            } catch (const std::exception& e) {
+                err[k] = e.what();
+            }
         }
+    };
+    const int nthr = count >= 64 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    if (nthr > 1) {
+        std::vector<std::thread> pool;
+        const int chunk = (count + nthr - 1) / nthr;
+        for (int t = 0; t < nthr; t++) {
+            const int k0 = t * chunk, k1 = std::min(count, k0 + chunk);
+            if (k0 < k1) pool.emplace_back(reduce_range, k0, k1);
+        }
+        for (auto& th : pool) th.join();
+    } else {
+        reduce_range(0, count);
+    }
+    for (int k = 0; k < count; k++) {  // the first bad QP's error, as a serial pass would report
+        if (!err[k].empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + err[k]);
         if (red[k].status < 0 && (red[k].nz > DENSE_NZ || red[k].m > DENSE_ROWS))
             return set_error(MPCCBF_ERR_CAPACITY,
                              "QP " + std::to_string(k) + ": reduced dimension " + std::to_string(red[k].nz) +

@@ -5,7 +5,9 @@
 #   rocprofv3 --kernel-trace --stats of the same commands; PMC passes (one counter group per run,
 #   never combined with traces): HBM bytes (FETCH_SIZE, WRITE_SIZE), SQ issue / wait counters,
 #   FP64 instruction mix, and the FoV kernels' FP64 MFMA counters.
-# Usage: bash tools/profile_round.sh <tag> [quick]
+# Order: PMC passes first (their summary goes to profiles/<tag>_pmc_summary.json, which the bench
+# lines read), then the bench lines and kernel traces, then the GPU tests and the stamp profile.
+# Usage: bash tools/profile_round.sh <tag> [nopmc]
 set -e -o pipefail
 TAG=${1:-rNN}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -14,22 +16,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 B="python3 $ROOT/bench.py"
 step() { echo "[$(date +%T)] $*"; }
-step bench driver; timeout -k 10 200 $B --steps 20 --warmup 5 > $OUT/${TAG}_bench_driver.json 2> $OUT/${TAG}_bench_driver.err
-step bench 1000; timeout -k 10 300 $B > $OUT/${TAG}_bench_collision.json 2> $OUT/${TAG}_bench_collision.err
-step bench 8192; timeout -k 10 300 $B --agents-per-gpu 8192 --no-cpu-baseline > $OUT/${TAG}_bench_8192.json 2> $OUT/${TAG}_bench_8192.err
-step bench fov; timeout -k 10 300 $B --workload fov > $OUT/${TAG}_bench_fov.json 2> $OUT/${TAG}_bench_fov.err
-step bench fov slack; timeout -k 10 300 $B --workload fov --slack > $OUT/${TAG}_bench_fov_slack.json 2> $OUT/${TAG}_bench_fov_slack.err
-prof() {  # name, bench args
-  step prof $1
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof_$1 -o run \
-    -- python3 $ROOT/bench.py --no-cpu-baseline ${@:2} > $OUT/${TAG}_prof_$1.json 2> $OUT/${TAG}_prof_$1.err
-}
-prof driver --steps 20 --warmup 5
-prof collision
-prof 8192 --agents-per-gpu 8192
-prof fov --workload fov
-prof fov_slack --workload fov --slack
-[ "$2" = "quick" ] && { echo done; exit 0; }
+[ "$2" = "nopmc" ] || {
 pmc() {  # dir, bench args..., -- counters
   local d=$1; shift
   local args=()
@@ -51,7 +38,31 @@ pmc fov_sqa --workload fov -- $SQA
 pmc fov_mfma --workload fov -- $SQM
 pmc fovs_fetch --workload fov --slack -- FETCH_SIZE
 pmc fovs_write --workload fov --slack -- WRITE_SIZE
+pmc fovs_sqa --workload fov --slack -- $SQA
 pmc fovs_mfma --workload fov --slack -- $SQM
 pmc collision_cache -- SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES
+# the bench lines below read their traffic / VALU figures from this round's summary
+python3 $ROOT/tools/pmc_summary.py $OUT/${TAG}_pmc > $ROOT/profiles/${TAG}_pmc_summary.json
+cp $ROOT/profiles/${TAG}_pmc_summary.json $OUT/${TAG}_pmc_summary.json
+}
+step bench driver; timeout -k 10 200 $B --steps 20 --warmup 5 > $OUT/${TAG}_bench_driver.json 2> $OUT/${TAG}_bench_driver.err
+step bench 1000; timeout -k 10 300 $B > $OUT/${TAG}_bench_collision.json 2> $OUT/${TAG}_bench_collision.err
+step bench 8192; timeout -k 10 300 $B --agents-per-gpu 8192 --no-cpu-baseline > $OUT/${TAG}_bench_8192.json 2> $OUT/${TAG}_bench_8192.err
+step bench fov; timeout -k 10 300 $B --workload fov > $OUT/${TAG}_bench_fov.json 2> $OUT/${TAG}_bench_fov.err
+step bench fov slack; timeout -k 10 300 $B --workload fov --slack > $OUT/${TAG}_bench_fov_slack.json 2> $OUT/${TAG}_bench_fov_slack.err
+prof() {  # name, bench args
+  step prof $1
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof_$1 -o run \
+    -- python3 $ROOT/bench.py --no-cpu-baseline ${@:2} > $OUT/${TAG}_prof_$1.json 2> $OUT/${TAG}_prof_$1.err
+}
+prof driver --steps 20 --warmup 5
+prof collision
+prof 8192 --agents-per-gpu 8192
+prof fov --workload fov
+prof fov_slack --workload fov --slack
+step bench dense; timeout -k 10 300 $B --workload dense --steps 10 --warmup 2 > $OUT/${TAG}_bench_dense.json 2> $OUT/${TAG}_bench_dense.err
+prof dense --workload dense --steps 10 --warmup 2
+step pytest; (cd $ROOT && timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/${TAG}_pytest_gpu.log 2>&1)
+step fovs status; MPCCBF_CHECK_SLACK=1 timeout -k 10 300 python3 $ROOT/tools/fov_status_check.py 1000 $OUT/${TAG}_fovs_status.npz > $OUT/${TAG}_fovs_status.log 2>&1
 step stamps; MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 $ROOT/tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1
 echo done
