@@ -73,9 +73,11 @@ for v in VARIANTS:
     if PDIP and v == 0 and not FOV:  # dual active-set stamps (solve 0, first steps)
         ps = allst[N * 8:].reshape(N, 16).astype(np.float64)
         its0 = out["iters"].cpu().numpy()[:, 0]
-        names = [("fast-start test", 12, 13), ("call", 13, 0), ("init", 0, 1), ("scan 1", 1, 2),
-                 ("stage", 2, 3), ("substitutions", 3, 4), ("step+update", 4, 5), ("add", 5, 6),
-                 ("scan 2", 6, 8), ("dual residual", 8, 9), ("warm+exit", 9, 10)]
+        # (the first scan is the fast-start test; the first side joins an empty active set
+        # without substitutions, so stamps 4 and 5 belong to later steps only)
+        names = [("solver entry", 12, 13), ("call", 13, 0), ("init", 0, 1),
+                 ("scan 1/fast start", 1, 2), ("stage", 2, 3), ("first side", 3, 6),
+                 ("scan 2", 6, 8), ("dual residual", 8, 9), ("exit", 9, 10)]
         for nstep in (1, 2):
             m = (ps[:, 15] == 1) & (its0 == nstep) & (ps[:, 10] > 0)
             if m.sum() == 0:
