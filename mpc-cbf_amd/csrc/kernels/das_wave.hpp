@@ -208,6 +208,8 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
             if (!chol_rows(Kr, L, inv_i, sc.M, lane)) return 0;
         }
     }
+    // a non-finite iterate fails every violation test, so it would pass as converged: give up
+    if (__ballot(!isfinite(yi)) != 0ull) return 0;
     // converged: primal residual = the last scan's worst violation; dual residual of the iterate
     // P y + q + G_A^T lam (lam_a = sign_a u_a) when reported
     double rd = 0.0;

@@ -31,7 +31,8 @@ struct FovSlackLds {
     double h[WSL_ROWS], live[WSL_ROWS];
     double Tn[WSL_NB], w[WSL_NB], dist[WSL_NB];
     int32_t order[WSL_NB];
-    int32_t rown[WSL_ROWS];  // FoV row compacted after the ordinary image -> its neighbour
+    int32_t rowl[WSL_ROWS];  // FoV row compacted after the ordinary image -> its slack-image row
+    int32_t lead[WSL_NB];    // per neighbour: its leader row (slack-image row), -1 = v_i at 0
 };
 
 // Position of observed neighbour i: from the neighbour query's LDS copy in grid mode, else the
@@ -333,41 +334,100 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                                          op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps,
                                          dtlow);
             } else {
-                // slack mode: the QP with every v = 0 (its FoV rows hard, compacted after the ordinary
-                // image) by the dual active set. Its optimum is the slack QP's when each neighbour's
-                // FoV multipliers sum to at most its slack cost (stationarity in v_i: w_i - sum lam =
-                // mu_i >= 0); otherwise, and when that QP has no feasible point, the slack PDIP solves.
+                // slack mode: the dual active set on a hard-row QP per slack pattern. Neighbour i is
+                // either at v_i = 0 (its FoV rows hard: g_a y <= h_a) or, with a leader row l, at
+                // v_i = g_l y - h_l >= 0: w_i g_l joins the linear term, its other rows become
+                // (g_a - g_l) y <= h_a - h_l and row l the bound g_l y >= h_l. A solve is the slack
+                // QP's optimum when every neighbour's multipliers are consistent (stationarity in
+                // v_i: at v_i = 0 the FoV multipliers sum to at most w_i; with a leader, its own
+                // multiplier w_i - sum(others) - mu_i is >= 0). All start at v = 0; a neighbour
+                // over its cost takes its largest-multiplier row as leader, one with a negative
+                // leader multiplier the next-largest; after SLK_PATTERNS patterns, or when a pattern
+                // has no feasible point, the slack PDIP solves.
+                constexpr int SLK_PATTERNS = 4;
                 const bool lv = slk->live[lane] != 0.0;
                 const unsigned long long lm = __ballot(lv);
                 const int ncbf = __popcll(lm);
+                const int c_me = __popcll(lm & ((1ull << lane) - 1ull));
+                if (lane < WSL_NB) slk->lead[lane] = -1;
                 if (op.dual_as > 0 && mtot + ncbf <= WROWS) {
-                    if (lv) {
-                        const int c = __popcll(lm & ((1ull << lane) - 1ull)), r = mtot + c;
-#pragma unroll
-                        for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = slk->Go[lane * WNZ + j];
-                        rlo[r] = 0.0;
-                        rml[r] = 0.0;
-                        rhi[r] = slk->h[lane];
-                        slk->rown[c] = lane >> 3;
-                    }
-                    wave_lds_sync();
-                    das = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
-                                         opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane,
-                                         drp, drd, dsteps, dtlow);
-                    if (das == 1) {
+                    if (lv) slk->rowl[c_me] = lane;
+                    int tot_steps = 0;
+                    for (int pat = 0; pat < SLK_PATTERNS; pat++) {
                         wave_lds_sync();
-                        double lam = 0.0;
+                        const int ld = slk->lead[lane >> 3];
+                        if (lv) {
+                            const int r = mtot + c_me;
+                            const double* go = slk->Go + lane * WNZ;
+                            const double* gl_ = slk->Go + (ld < 0 ? lane : ld) * WNZ;
+                            const bool diff = ld >= 0 && ld != lane;
+#pragma unroll
+                            for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = diff ? go[j] - gl_[j] : go[j];
+                            const bool lead_row = ld == lane;
+                            rlo[r] = lead_row ? slk->h[lane] : 0.0;
+                            rml[r] = lead_row ? 1.0 : 0.0;
+                            rhi[r] = lead_row ? 1e300 : (diff ? slk->h[lane] - slk->h[ld] : slk->h[lane]);
+                        }
+                        if (lane < WNZ) {  // q + sum over led neighbours of w_i g_l
+                            double qv = q_s[lane];
+                            for (int g = 0; g < nnb; g++) {
+                                const int l = slk->lead[g];
+                                if (l >= 0) qv = fma(slk->w[g], slk->Go[l * WNZ + lane], qv);
+                            }
+                            sc.q[lane] = qv;
+                        }
+                        wave_lds_sync();
+                        int st_ = 0;
+                        das = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
+                                             opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as, args.dual_res != nullptr,
+                                             lane, drp, drd, st_, dtlow);
+                        tot_steps += st_;
+                        if (das != 1) break;
+                        wave_lds_sync();
+                        // per neighbour (lane g < nnb): multipliers of its upper sides, of its leader's
+                        // bound, and its largest-multiplier active rows other than the leader
+                        bool bad = false;
+                        int pick = -1;
                         if (lane < nnb) {
+                            const int l = slk->lead[lane];
+                            double lam = 0.0, mu = 0.0, best = -1.0;
                             for (int a = 0; a < was.k; a++) {
                                 const int r = was.row[a];
-                                if (r >= mtot && slk->rown[r - mtot] == lane) lam += was.u[a];
+                                if (r < mtot) continue;
+                                const int sl = slk->rowl[r - mtot];
+                                if ((sl >> 3) != lane) continue;
+                                const double ua = was.u[a];
+                                if (was.sg[a] < 0.0) {
+                                    mu += ua;  // the leader's bound v_i >= 0
+                                } else {
+                                    lam += ua;
+                                    if (sl != l && ua > best) best = ua, pick = sl;
+                                }
                             }
+                            bad = l < 0 ? !(lam <= slk->w[lane]) : !(slk->w[lane] - lam - mu >= 0.0);
                         }
-                        if (__ballot(lane < nnb && !(lam <= slk->w[lane])) != 0ull) das = 0;
+                        const unsigned long long badm = __ballot(bad);
+                        if (badm == 0ull) {
+                            // consistent: v_i = g_l y - h_l for led neighbours, the cost into the objective
+                            double vw = 0.0;
+                            if (lane < nnb) {
+                                const int l = slk->lead[lane];
+                                if (l >= 0) vw = slk->w[lane] * (dotl(slk->Go + l * WNZ, sc.y) - slk->h[l]);
+                            }
+                            vobj = wave_reduce<Op::Sum>(vw);
+                            break;
+                        }
+                        das = 0;
+                        if (__ballot(bad && pick < 0) != 0ull) break;  // no row to lead: the PDIP
+                        wave_lds_sync();
+                        if (bad) slk->lead[lane] = pick;
                     }
+                    dsteps = tot_steps;
                     if (das != 1) {
                         das = 0;
+                        vobj = 0.0;
                         for (int e = lane; e < ncbf * WNZ; e += 64) Gimg[mtot * WNZ + e] = 0.0;
+                        if (lane < WNZ) sc.q[lane] = q_s[lane];
                         wave_lds_sync();
                     }
                 }

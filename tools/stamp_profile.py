@@ -35,6 +35,9 @@ tg = torch.tensor(targets_h, device=dev)
 radius = cfg["fov_Rs"] if FOV else 3.0 * cfg["d_min"]
 ctx = Context(cfg)
 out = ctx.alloc_outputs(N)
+if os.environ.get("RESIDUALS", "") != "1":  # as the bench: no residual outputs (no dual-residual check)
+    out.pop("primal_res", None)
+    out.pop("dual_res", None)
 if FOV and SLACK:
     COV = torch.tensor(np.tile([0.1, 0.0, 0.1], (N, 1)), device=dev)
 for _ in range(WARM):
@@ -78,13 +81,15 @@ for v in VARIANTS:
         names = [("solver entry", 12, 13), ("call", 13, 0), ("init", 0, 1),
                  ("scan 1/fast start", 1, 2), ("stage", 2, 3), ("first side", 3, 6),
                  ("scan 2", 6, 8), ("dual residual", 8, 9), ("exit", 9, 10)]
-        for nstep in (1, 2):
+        names0 = [("solver entry", 12, 13), ("call", 13, 0), ("init", 0, 1),
+                  ("scan/fast start", 1, 2), ("converged", 2, 9), ("exit", 9, 10)]
+        for nstep in (0, 1, 2):
             m = (ps[:, 15] == 1) & (its0 == nstep) & (ps[:, 10] > 0)
             if m.sum() == 0:
                 continue
             print(f"variant {v}: dual active-set solves with {nstep} step(s): {m.sum()} agents, "
                   f"cycles entry->exit mean {np.mean(ps[m, 10] - ps[m, 12]):.0f}")
-            for name, a, b in names:
+            for name, a, b in (names0 if nstep == 0 else names):
                 d = ps[m, b] - ps[m, a]
                 print(f"   {name:15s} mean {d.mean():7.0f}  p50 {np.median(d):7.0f} cycles")
     status = out["status"].cpu().numpy()
