@@ -344,7 +344,10 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 // over its cost takes its largest-multiplier row as leader, one with a negative
                 // leader multiplier the next-largest; after SLK_PATTERNS patterns, or when a pattern
                 // has no feasible point, the slack PDIP solves.
-                constexpr int SLK_PATTERNS = 4;
+#ifndef MPCCBF_SLK_PATTERNS
+#define MPCCBF_SLK_PATTERNS 4
+#endif
+                constexpr int SLK_PATTERNS = MPCCBF_SLK_PATTERNS;
                 const bool lv = slk->live[lane] != 0.0;
                 const unsigned long long lm = __ballot(lv);
                 const int ncbf = __popcll(lm);
