@@ -467,28 +467,44 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #pragma unroll
             for (int j = 0; j < SEP_NZ; j++) gp[j] = cand[j];
             const double sp = cand[POL_SGN];
+            // rows at or beyond the wave's largest active count kw are identity rows of L with zero
+            // right-hand side (v = rho = 0 there): skipped by scalar branches (kw is wave-uniform)
+#ifndef MPCCBF_NO_KW
+            int kw = 0;
+#pragma unroll
+            for (int i = 1; i <= POL_K; i++) kw += __ballot(k >= i) != 0ull ? 1 : 0;
+#else  // comparison build: every row
+            constexpr int kw = POL_K;
+#endif
             // v = L^-1 (sp c), c_i = g_i P^-1 g_p: the forward substitution fused with the dots
             double v[POL_K], sgn[POL_K];
 #pragma unroll
             for (int i = 0; i < POL_K; i++) {
-                const double* ri = pol + (i < k ? i : 0) * 16;
-                double t = 0.0;
+                v[i] = 0.0;
+                sgn[i] = 0.0;
+                if (i < kw) {
+                    const double* ri = pol + (i < k ? i : 0) * 16;
+                    double t = 0.0;
 #pragma unroll
-                for (int j = 0; j < SEP_NZ; j++) t = fma(ri[POL_W + j], gp[j], t);
-                sgn[i] = ri[POL_SGN];
-                double s = i < k ? sp * t : 0.0;
+                    for (int j = 0; j < SEP_NZ; j++) t = fma(ri[POL_W + j], gp[j], t);
+                    sgn[i] = ri[POL_SGN];
+                    double s = i < k ? sp * t : 0.0;
 #pragma unroll
-                for (int mm = 0; mm < i; mm++) s = fma(-L[S6::idx(mm, i)], v[mm], s);
-                v[i] = s * dl[i];
+                    for (int mm = 0; mm < i; mm++) s = fma(-L[S6::idx(mm, i)], v[mm], s);
+                    v[i] = s * dl[i];
+                }
             }
             // rho = L^-T v = K^-1 G_A P^-1 n_p: the active multipliers' change per unit step
             double rho[POL_K];
 #pragma unroll
             for (int i = POL_K - 1; i >= 0; i--) {
-                double s = v[i];
+                rho[i] = 0.0;
+                if (i < kw) {
+                    double s = v[i];
 #pragma unroll
-                for (int mm = i + 1; mm < POL_K; mm++) s = fma(-L[S6::idx(i, mm)], rho[mm], s);
-                rho[i] = s * dl[i];
+                    for (int mm = i + 1; mm < POL_K; mm++) s = fma(-L[S6::idx(i, mm)], rho[mm], s);
+                    rho[i] = s * dl[i];
+                }
             }
             GSTAMP(4, outer == 0);
             double nw = 0.0, vv = 0.0, vp = 0.0;
@@ -542,10 +558,12 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 for (int j = 0; j < SEP_NZ; j++) z[j] = sp * cand[POL_W + j];
 #pragma unroll
                 for (int i = 0; i < POL_K; i++) {
-                    const double* wi = pol + (i < k ? i : 0) * 16 + POL_W;
-                    const double ri = i < k ? rho[i] : 0.0;
+                    if (i < kw) {
+                        const double* wi = pol + (i < k ? i : 0) * 16 + POL_W;
+                        const double ri = i < k ? rho[i] : 0.0;
 #pragma unroll
-                    for (int j = 0; j < SEP_NZ; j++) z[j] = fma(-ri, wi[j], z[j]);
+                        for (int j = 0; j < SEP_NZ; j++) z[j] = fma(-ri, wi[j], z[j]);
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-t, z[j], y[j]);
