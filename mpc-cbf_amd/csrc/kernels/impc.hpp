@@ -86,28 +86,11 @@ __host__ __device__ inline uint32_t cell_hash(long long cx, long long cy, uint32
     return (uint32_t)(h ^ (h >> 29)) & mask;
 }
 
-// Each slot also holds its row's (px, py, vx, vy), slot-major after the GRID_CAP x T row words, so
-// the neighbour query reads a candidate's position and velocity from the slot it already reads
-// instead of a further dependent load of the state table.
-__host__ __device__ inline double* grid_slot_states(uint32_t* slots, uint32_t T) {
-    return (double*)(slots + (size_t)GRID_CAP * T);
-}
-__host__ __device__ inline const double* grid_slot_states(const uint32_t* slots, uint32_t T) {
-    return (const double*)(slots + (size_t)GRID_CAP * T);
-}
-
-// insert state row `row` at planar position (x, y), velocity (vx, vy) into the table (ins_cnt,
-// ins_slots and the slot states)
-__device__ inline void grid_insert(const GridArgs& g, double x, double y, double vx, double vy, uint32_t row) {
+// insert state row `row` at planar position (x, y) into the table (ins_cnt, ins_slots)
+__device__ inline void grid_insert(const GridArgs& g, double x, double y, uint32_t row) {
     const uint32_t h = cell_hash((long long)floor(x * g.inv_cell), (long long)floor(y * g.inv_cell), g.mask);
     const uint32_t j = atomicAdd(&g.ins_cnt[h], 1u);
-    if (j < (uint32_t)GRID_CAP) {
-        const size_t e = (size_t)j * (g.mask + 1u) + h;
-        g.ins_slots[e] = row;
-        double2* ss = (double2*)(grid_slot_states(g.ins_slots, g.mask + 1u) + e * 4);
-        ss[0] = make_double2(x, y);
-        ss[1] = make_double2(vx, vy);
-    }
+    if (j < (uint32_t)GRID_CAP) g.ins_slots[(size_t)j * (g.mask + 1u) + h] = row;
 }
 
 // hash table size for n agents: power of two >= n (>= 1024)

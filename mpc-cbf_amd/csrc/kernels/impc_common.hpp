@@ -100,24 +100,17 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         if (t < total) {
             if (full) {
                 j = (int)t;
-                nx = args.states[(size_t)j * 6];
-                ny = args.states[(size_t)j * 6 + 1];
-                nvx = args.states[(size_t)j * 6 + 3];
-                nvy = args.states[(size_t)j * 6 + 4];
             } else {
                 uint32_t e = 0;
 #pragma unroll
                 for (int c = 0; c < 9; c++)  // the cell whose range holds t
                     if (off[c] <= t && t - off[c] < nc[c]) e = (t - off[c]) * (gr.mask + 1u) + hs[c];
                 j = (int)gr.slots[e];
-                // the row's state from the slot itself (written with it), not the state table
-                const double2* ss = (const double2*)(grid_slot_states(gr.slots, gr.mask + 1u) + (size_t)e * 4);
-                const double2 p = ss[0], w = ss[1];
-                nx = p.x;
-                ny = p.y;
-                nvx = w.x;
-                nvy = w.y;
             }
+            nx = args.states[(size_t)j * 6];
+            ny = args.states[(size_t)j * 6 + 1];
+            nvx = args.states[(size_t)j * 6 + 3];
+            nvy = args.states[(size_t)j * 6 + 4];
             const double ex = nx - px;
             const double ey = ny - py;
             d2 = ex * ex + ey * ey;
@@ -555,8 +548,7 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
     if (args.grid.ins_cnt) {  // the next step's neighbour table gets this row (lane 0: x, lane 1: y)
         const int base = (int)(threadIdx.x & 63u) & ~(G - 1);
         const double y = __shfl(v, base + 1, 64);
-        const double vx = __shfl(v, base + 3, 64), vy = __shfl(v, base + 4, 64);
-        if (gl == 0) grid_insert(args.grid, v, y, vx, vy, (uint32_t)(args.agent_first + ai));
+        if (gl == 0) grid_insert(args.grid, v, y, (uint32_t)(args.agent_first + ai));
     }
 }
 

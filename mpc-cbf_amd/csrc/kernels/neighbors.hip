@@ -255,19 +255,17 @@ __global__ void __launch_bounds__(256) grid_insert_kernel(const double* __restri
     const int gap = skip1 - skip0;
     if (i >= n - gap) return;
     const int r = i < skip0 ? i : i + gap;
-    const double* s = st + (size_t)r * 6;
-    grid_insert(g, s[0], s[1], s[3], s[4], (uint32_t)r);
+    grid_insert(g, st[(size_t)r * 6], st[(size_t)r * 6 + 1], (uint32_t)r);
 }
 
 }  // namespace dev
 
 static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
-// one table: bucket counts (T) | slots (GRID_CAP x T, slot-major) | slot states (GRID_CAP x T x 4
-// doubles, same order)
+// one table: bucket counts (T) | slots (GRID_CAP x T, slot-major)
 size_t grid_table_bytes(int num_states) {
     const uint32_t T = grid_table_size(num_states);
-    return al256((size_t)T * 4) + (size_t)T * GRID_CAP * 4 + (size_t)T * GRID_CAP * 32;
+    return al256((size_t)T * 4) + (size_t)T * GRID_CAP * 4;
 }
 
 void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots) {
