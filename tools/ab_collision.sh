@@ -1,5 +1,6 @@
 # A/B of the collision kernel (default build vs build/${1:-nokw}): GPU tests first, then bench lines
-# on the driver command and at 300 steps, 2 rounds interleaved
+# on the driver command and at 300 steps, 2 rounds interleaved. The alternative library is built
+# beforehand, e.g. from a stashed tree: make -C mpc-cbf_amd BUILD=build/base build/base/libmpccbf.so
 set -e -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out

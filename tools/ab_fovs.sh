@@ -1,4 +1,6 @@
-# A/B of the FoV slack pattern limit (4: default build; 8 / 16: build/pat*): bench lines, 2 rounds
+# A/B of the FoV slack pattern limit (4: default build; 8 / 16: build/pat*): bench lines, 2 rounds.
+# Build the alternatives first (CPU side), e.g.
+#   make -C mpc-cbf_amd BUILD=build/pat8 HIPFLAGS="<default HIPFLAGS> -DMPCCBF_SLK_PATTERNS=8" build/pat8/libmpccbf.so
 set -e -o pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
