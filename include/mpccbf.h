@@ -260,6 +260,17 @@ int mpccbf_build_neighbors(mpccbf_ctx* ctx, const double* states, int32_t num_st
                            int32_t agent_first, int32_t num_agents, int32_t k, double radius,
                            int32_t* row_ptr, int32_t* col, void* hip_stream);
 
+/* The FoV controller's per-neighbour rows on the device, by the same device functions the IMPC
+ * kernel evaluates (for parity checks of the rows themselves): for count (ego, neighbour) pairs
+ * (ego: count x 6, nb_xy: count x 2, device) the box-shifted Voronoi hyperplane
+ * (separating_hyperplanes::voronoi, Voronoi.cpp:10-29, math::shiftHyperplane, Helpers.cpp:20-36;
+ * bbox: host, 3 half extents, NULL = 0) as voronoi[i] = (nx, ny, 0, offset), n . p + offset = 0,
+ * and the four FoV HOCBF rows (FovCBF::get{Safety,LB,RB,Range}{Constraints,Bound},
+ * FovCBF.cpp:622-810) as fov_rows[i][kind] = (a0, a1, a2, b), kind = safety, left, right, range
+ * (b = DBL_MAX for the border rows of a 360-degree field of view). Either output may be NULL. */
+int mpccbf_fov_rows_eval(int32_t count, const double* ego, const double* nb_xy, double fov, double Ds,
+                         double Rs, const double* bbox, double* voronoi, double* fov_rows, void* hip_stream);
+
 /* ---- Batched CBF-only controller (FovControl::optimize, cbf/src/controller/FovControl.cpp:17-86)
  * Per agent: min ||u - u_des||^2 over the control input u (3) subject to the 4 FoV HOCBF rows of
  * every observed neighbour (FovQPGenerator.cpp:12-115), the velocity CBF rows

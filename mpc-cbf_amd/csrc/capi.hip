@@ -27,6 +27,8 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
                        hipStream_t s);
 const char* impc_kernel_name(const DevOps& op, int variant);
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
+hipError_t launch_fov_rows_eval(int count, const double* ego, const double* nb, double fov, double Ds, double Rs,
+                                double bbx, double bby, double* vor, double* rows, hipStream_t s);
 hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
 bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k);
 int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
@@ -194,6 +196,9 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
         f.defer = nullptr;
         f.queue = c->defer;
         e = launch_impc_fallback(c->dev, c->dbuf, f, stream);
+        // the fallback's last block empties the queue; if it never ran, the agents the main
+        // launch appended are dropped here, so the next main launch starts from an empty queue
+        if (e != hipSuccess) (void)hipMemsetAsync(c->defer, 0, 2 * sizeof(int32_t), stream);
     }
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, stream);
     if (e == hipErrorInvalidValue)
@@ -502,16 +507,35 @@ struct LocalGroup {
     std::vector<hipEvent_t> ev[2];     // [step & 1][rank]: that rank's IMPC kernel of the step done
     // (double-buffered by step parity: a rank rewrites slot s & 1 only after the barrier of step
     // s + 1, which every peer reaches after enqueueing its step-s copies)
-    void barrier() {
+    std::vector<int> nsteps;           // [rank]: num_steps of the current mpccbf_run_steps call
+    bool aborted = false;              // a rank left early: every barrier fails from then on
+    // false: a rank aborted (the group cannot be used again; destroy and recreate it)
+    bool barrier() {
         std::unique_lock<std::mutex> lk(m);
+        if (aborted) return false;
         const long long g = gen;
         if (++arrived == nranks) {
             arrived = 0;
             gen++;
             cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return gen != g; });
+            return true;
         }
+        cv.wait(lk, [&] { return gen != g || aborted; });
+        return gen != g;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(m);
+        aborted = true;
+        cv.notify_all();
+    }
+};
+
+// Aborts the rank's in-process group when mpccbf_run_steps leaves before its last barrier, so the
+// peers' barriers return an error instead of waiting forever.
+struct GroupAbortGuard {
+    LocalGroup* g = nullptr;
+    ~GroupAbortGuard() {
+        if (g) g->abort();
     }
 };
 
@@ -564,6 +588,7 @@ int mpccbf_comm_create_local(int32_t nranks, int32_t device, mpccbf_comm** out) 
         g->ev[p].assign(nranks, nullptr);
         for (int r = 0; r < nranks; r++) HIP_TRY(hipEventCreateWithFlags(&g->ev[p][r], hipEventDisableTiming));
     }
+    g->nsteps.assign(nranks, 0);
     for (int r = 0; r < nranks; r++) {
         out[r] = new mpccbf_comm();
         out[r]->nranks = nranks;
@@ -585,6 +610,30 @@ void mpccbf_comm_destroy(mpccbf_comm* cm) {
 
 int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* stream_) {
     if (!c || !b || !r) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
+    // in-process group: any return before the last step's barrier aborts the group (the peers
+    // get an error), and every rank must run the same number of steps
+    LocalGroup* lg = (r->comm && r->comm->nranks > 1 && r->comm->local) ? r->comm->local.get() : nullptr;
+    GroupAbortGuard guard{lg};
+    if (lg) {
+        {
+            std::lock_guard<std::mutex> lk(lg->m);
+            lg->nsteps[r->comm->rank] = r->num_steps;
+        }
+        if (!lg->barrier()) return fail(MPCCBF_ERR_HIP, "run: a rank of the in-process group aborted");
+        bool same = true;
+        {
+            std::lock_guard<std::mutex> lk(lg->m);
+            for (int v : lg->nsteps) same = same && v == r->num_steps;
+        }
+        // (every rank reads the counts before any rank can overwrite them at its next call's
+        // entry: that write follows this call's step barriers, or the abort below)
+        if (!same) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "run: ranks of the in-process group differ in num_steps");
+        if (r->num_steps == 0) {
+            if (!lg->barrier()) return fail(MPCCBF_ERR_HIP, "run: a rank of the in-process group aborted");
+            guard.g = nullptr;
+            return MPCCBF_OK;
+        }
+    }
     if (r->num_steps < 0 || !r->states_alt || !b->states)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "run: num_steps < 0 or missing state tables");
     const int first = b->agent_first, count = b->num_agents, ns = b->num_states;
@@ -645,7 +694,7 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
             const int me = r->comm->rank;
             g.table[s & 1][me] = nxt;
             HIP_TRY(hipEventRecord(g.ev[s & 1][me], stream));
-            g.barrier();
+            if (!g.barrier()) return fail(MPCCBF_ERR_HIP, "run: a rank of the in-process group aborted");
             for (int p = 0; p < g.nranks; p++) {
                 if (p == me) continue;
                 HIP_TRY(hipStreamWaitEvent(stream, g.ev[s & 1][p], 0));
@@ -664,6 +713,7 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
                                        gslots[(s + 1) % 3], stream));
         if (r->step_ms || (timing && s == r->num_steps - 1)) HIP_TRY(hipEventRecord(ev[3 * s + 3], stream));
     }
+    guard.g = nullptr;  // every barrier of the call passed: the peers no longer wait on this rank
     r->final_table = r->num_steps & 1;
     if (timing && r->num_steps > 0) {
         HIP_TRY(hipEventSynchronize(ev[3 * (r->num_steps - 1) + 3]));
@@ -734,6 +784,18 @@ int mpccbf_connectivity_control_solve(const mpccbf_connectivity_control_params* 
     a.slack_cost = p->slack_cost;
     a.slack_decay = p->slack_decay_rate;
     HIP_TRY(launch_connectivity_control(a, (hipStream_t)stream));
+    return MPCCBF_OK;
+}
+
+int mpccbf_fov_rows_eval(int32_t count, const double* ego, const double* nb_xy, double fov, double Ds,
+                         double Rs, const double* bbox, double* voronoi, double* fov_rows, void* stream) {
+    if (count < 0 || (count > 0 && (!ego || !nb_xy))) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "bad arguments");
+    if (count == 0) return MPCCBF_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+        return fail(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
+    const double bbx = bbox ? bbox[0] : 0.0, bby = bbox ? bbox[1] : 0.0;
+    HIP_TRY(launch_fov_rows_eval(count, ego, nb_xy, fov, Ds, Rs, bbx, bby, voronoi, fov_rows, (hipStream_t)stream));
     return MPCCBF_OK;
 }
 

@@ -99,15 +99,18 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         double vb = -1.0;
         int rb = 0, sdb = 1;
         double bb = 0.0;
+        bool nf = false;  // a NaN row or iterate fails every comparison: give up instead
 #pragma unroll
         for (int s = 0; s < WR; s++) {
             const double t = dotl(rw.g[s], sc.y);
             const double vl = rw.ml[s] > 0.0 ? (rw.lo[s] - t) * pl[s] : -1.0;
             const double vu = (t - rw.hi[s]) * pu[s];
             const int r = wave_owner_row(lane, s);
+            nf = nf || vl != vl || vu != vu;
             if (vl > vb) vb = vl, rb = r, sdb = 0, bb = rw.lo[s];
             if (vu > vb) vb = vu, rb = r, sdb = 1, bb = rw.hi[s];
         }
+        if (__ballot(nf) != 0ull) return 0;
         m = wave_reduce<Op::Max>(vb);
         if (!(m > add_tol)) break;
         if (steps >= maxstep) return 0;
@@ -211,9 +214,10 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
     // a non-finite iterate fails every violation test, so it would pass as converged: give up
     if (__ballot(!isfinite(yi)) != 0ull) return 0;
     // converged: primal residual = the last scan's worst violation; dual residual of the iterate
-    // P y + q + G_A^T lam (lam_a = sign_a u_a) when reported
+    // P y + q + G_A^T lam (lam_a = sign_a u_a), checked whether or not the caller stores it
+    (void)want_rd;
     double rd = 0.0;
-    if (want_rd) {
+    {
         double r = sc.q[i];
 #pragma unroll
         for (int j = 0; j < WNZ; j++) r = fma(ldg_nohoist(P + i * WNZ + j), sc.y[j], r);

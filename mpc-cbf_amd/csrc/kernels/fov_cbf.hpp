@@ -60,6 +60,23 @@ __device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double 
     b = lf2 + 5.0 * gamma * b4 * lf + gamma * p2 * p2 * psi;
 }
 
+// Voronoi row of the FoV controller: separating_hyperplanes::voronoi of the planar positions
+// (Voronoi.cpp:10-29: unit normal from self to other, the plane through the midpoint; Eigen's
+// normalize() leaves a zero vector unchanged), shifted by the robot box (math::shiftHyperplane,
+// Helpers.cpp:20-36: the offset's maximum over the box corners; the yaw component of the normal is
+// zeroed, FovBezierIMPCCBF.cpp:135-141): n . p + off = 0, (nx, ny, 0).
+__host__ __device__ inline void voronoi_row(double sx, double sy, double ox, double oy, double bbx,
+                                            double bby, double& nx, double& ny, double& off) {
+    nx = ox - sx;
+    ny = oy - sy;
+    const double nrm = sqrt(nx * nx + ny * ny);
+    if (nrm > 0.0) {
+        nx /= nrm;
+        ny /= nrm;
+    }
+    off = -(nx * 0.5 * (sx + ox) + ny * 0.5 * (sy + oy)) + bbx * fabs(nx) + bby * fabs(ny);
+}
+
 // FovBezierIMPCCBF::distanceToEllipse (FovBezierIMPCCBF.cpp:226-280; FovControl.cpp:90-148 is the
 // same function): signed distance from the
 // robot to the point of the target's 90 % confidence ellipse (s = 4.605) at parametric angle

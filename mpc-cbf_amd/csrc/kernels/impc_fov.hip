@@ -168,16 +168,9 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         const int nvor = nnb * C;
         for (int v = lane; v < nvor; v += 64) {
             const int i = v / C, j = v % C;
-            double ox, oy;
+            double ox, oy, nx, ny, off;
             nb_position(args, nb_scratch, grid_mode, nb0, i, ox, oy);
-            double nx = ox - s0[0], ny = oy - s0[1];
-            const double nrm = sqrt(nx * nx + ny * ny);
-            if (nrm > 0.0) {
-                nx /= nrm;
-                ny /= nrm;
-            }
-            const double off = -(nx * 0.5 * (s0[0] + ox) + ny * 0.5 * (s0[1] + oy)) +
-                               op.bbox[0] * fabs(nx) + op.bbox[1] * fabs(ny);
+            voronoi_row(s0[0], s0[1], ox, oy, op.bbox[0], op.bbox[1], nx, ny, off);
             const double* VZ = opp(buf, op.o_VZ) + (size_t)j * 2 * NZ;
             const double* VS = opp(buf, op.o_VS) + (size_t)j * 12;
             const int r = mb + v;
@@ -522,7 +515,50 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     stamp(args, ai, lane, 7);
 }
 
+// The FoV controller's per-neighbour rows for `count` (ego, neighbour) pairs, evaluated by the same
+// device functions the IMPC kernel uses (mpccbf_fov_rows_eval): Voronoi (nx, ny, 0, off) and the
+// four FoV HOCBF rows (a0, a1, a2, b; safety, left, right, range; b = DBL_MAX when absent).
+__global__ void __launch_bounds__(64) fov_rows_eval_kernel(int count, const double* __restrict__ ego,
+                                                           const double* __restrict__ nb, double fov, double Ds,
+                                                           double Rs, double bbx, double bby,
+                                                           double* __restrict__ vor, double* __restrict__ rows) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= count) return;
+    double e[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) e[k] = ego[(size_t)i * 6 + k];
+    const double ox = nb[(size_t)i * 2], oy = nb[(size_t)i * 2 + 1];
+    if (vor) {
+        double nx, ny, off;
+        voronoi_row(e[0], e[1], ox, oy, bbx, bby, nx, ny, off);
+        vor[(size_t)i * 4 + 0] = nx;
+        vor[(size_t)i * 4 + 1] = ny;
+        vor[(size_t)i * 4 + 2] = 0.0;
+        vor[(size_t)i * 4 + 3] = off;
+    }
+    if (rows) {
+        for (int kind = 0; kind < 4; kind++) {
+            double a[3], b;
+            bool present;
+            fov_cbf_row(kind, e, ox, oy, fov, Ds, Rs, a, b, present);
+            double* r = rows + ((size_t)i * 4 + kind) * 4;
+            r[0] = a[0];
+            r[1] = a[1];
+            r[2] = a[2];
+            r[3] = b;
+        }
+    }
+}
+
 }  // namespace dev
+
+hipError_t launch_fov_rows_eval(int count, const double* ego, const double* nb, double fov, double Ds, double Rs,
+                                double bbx, double bby, double* vor, double* rows, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(dev::fov_rows_eval_kernel, dim3((count + 63) / 64), dim3(64), 0, s, count, ego, nb, fov, Ds,
+                       Rs, bbx, bby, vor, rows);
+    return hipGetLastError();
+}
 
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
     if (a.num_agents <= 0) return hipSuccess;

@@ -384,6 +384,25 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     for (int i = 0; i < POL_K; i++) u[i] = 0.0;
     int k = 0;
     steps = 0;
+    {
+        // a non-finite start or row (NaN / Inf state, target or neighbour state) fails every
+        // violation comparison below, so the scan would pass it as converged: give up and let the
+        // PDIP's finiteness checks decide
+        bool nf = false;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) nf = nf || !isfinite(yu[j]);
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int kk = 0; kk < SB; kk++)
+                nf = nf || !isfinite(rw.bg[d][kk][0] + rw.bg[d][kk][1] + rw.blo[d][kk] + rw.bhi[d][kk]);
+        if (has_cbf) {
+#pragma unroll
+            for (int c = 0; c < CB; c++)
+                nf = nf || !isfinite(rw.cg[c][0] + rw.cg[c][1] + rw.cg[c][2] + rw.cg[c][3] + rw.chi[c]);
+        }
+        if (grp_ballot<G>(nf) != 0ull) return 0;
+    }
     const double add_tol = 0.1 * tol;
     double* cand = pol + POL_K * 16;
     using S6 = Sym<POL_K>;
@@ -604,11 +623,19 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         }
     }
     // converged: primal residual = the last scan's worst violation; the iterate's dual residual
-    // P y + q + G_A^T lam (lam = sign * u) when it is reported (want_rd): the updates hold
-    // stationarity by construction, so the check only guards against rounding
+    // P y + q + G_A^T lam (lam = sign * u), checked whether or not the caller stores it (the
+    // updates hold stationarity by construction, so the check only guards against rounding); a
+    // non-finite iterate gives up
+    (void)want_rd;
+    {
+        bool nf = false;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) nf = nf || !isfinite(y[j]);
+        if (grp_ballot<G>(nf) != 0ull) return 0;
+    }
     double rd = 0.0, qn = 0.0;
 #pragma unroll
-    for (int d = 0; d < (want_rd ? SEP_D : 0); d++) {
+    for (int d = 0; d < SEP_D; d++) {
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int o = 2 * d + h;

@@ -22,7 +22,7 @@ EXPORTED = [
     "mpccbf_status_string", "mpccbf_abi_version", "mpccbf_run_steps", "mpccbf_comm_unique_id",
     "mpccbf_comm_create", "mpccbf_comm_destroy", "mpccbf_kernel_name", "mpccbf_fov_control_solve",
     "mpccbf_connectivity_control_solve", "mpccbf_host_operators", "mpccbf_host_last_error",
-    "mpccbf_comm_create_local",
+    "mpccbf_comm_create_local", "mpccbf_fov_rows_eval",
 ]
 
 
@@ -142,6 +142,7 @@ def load():
     L.mpccbf_kernel_name.argtypes = [vp]
     L.mpccbf_kernel_name.restype = C.c_char_p
     L.mpccbf_last_error.restype = C.c_char_p
+    L.mpccbf_fov_rows_eval.argtypes = [C.c_int32, vp, vp, C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]
     L.mpccbf_status_string.restype = C.c_char_p
     L.mpccbf_status_string.argtypes = [C.c_int32]
     _lib = L
@@ -422,6 +423,20 @@ def fov_control_solve(cfg: dict, states, desired_u, nb_row_ptr, nb_xy, u, status
                         status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters), nb_cov=_ptr(nb_cov))
     p = fov_control_params(cfg)
     _check(load().mpccbf_fov_control_solve(C.byref(p), C.byref(b), device, _stream(stream)))
+
+
+def fov_rows_eval(ego, nb_xy, fov: float, Ds: float, Rs: float, bbox=(0.0, 0.0, 0.0), stream=None):
+    """The FoV controller's per-neighbour rows on the device (mpccbf_fov_rows_eval): ego (n x 6)
+    and nb_xy (n x 2) device tensors -> (voronoi n x 4 = (nx, ny, 0, offset), fov rows n x 4 x 4 =
+    (a0, a1, a2, b) per kind: safety, left, right, range)."""
+    import torch
+    n = ego.shape[0]
+    vor = torch.empty((n, 4), dtype=torch.float64, device=ego.device)
+    rows = torch.empty((n, 4, 4), dtype=torch.float64, device=ego.device)
+    bb = (C.c_double * 3)(*bbox)
+    _check(load().mpccbf_fov_rows_eval(n, _ptr(ego), _ptr(nb_xy), fov, Ds, Rs, C.cast(bb, C.c_void_p),
+                                       _ptr(vor), _ptr(rows), _stream(stream)))
+    return vor, rows
 
 
 class ConnControlParams(C.Structure):

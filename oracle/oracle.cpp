@@ -1478,6 +1478,11 @@ int orc_impc_optimize_cov(const orc_params* p, int32_t N, const double* states, 
     }
 }
 
+void orc_voronoi(const double* self2, const double* other2, const double* bbox3, double* normal3,
+                 double* offset) {
+    orc::voronoi_shifted(self2, other2, bbox3, normal3, offset);
+}
+
 double orc_distance_to_ellipse(const double* robot2, const double* mean2, const double* cov3) {
     return orc::distance_to_ellipse(robot2, mean2, cov3);
 }

@@ -121,6 +121,11 @@ int orc_impc_optimize_cov(const orc_params* p, int32_t num_agents, const double*
                           double* x, int32_t* qp_iters);
 /* FovBezierIMPCCBF::distanceToEllipse (FovBezierIMPCCBF.cpp:226-280); cov3 = (cxx, cxy, cyy) */
 double orc_distance_to_ellipse(const double* robot2, const double* mean2, const double* cov3);
+/* separating_hyperplanes::voronoi (Voronoi.cpp:10-29) of two planar points, shifted by the robot
+ * box bbox3 (math::shiftHyperplane, Helpers.cpp:20-36; bbox3 = 0: the plain Voronoi hyperplane):
+ * normal3 . x + *offset = 0, as the FoV controller uses it (FovBezierIMPCCBF.cpp:130-147) */
+void orc_voronoi(const double* self2, const double* other2, const double* bbox3, double* normal3,
+                 double* offset);
 
 /* Batched CPU baseline: agents [first, first+count) with neighbor CSR (row_ptr, col).
  * nthreads worker threads, one agent per task (CPLEX Threads=1 per solve, CPLEX.cpp:158).

@@ -6,6 +6,8 @@ Sources (paths under workspace/lib of ywang760/mpc-cbf @ 2025-08-29):
   qpcpp/tests/CPLEXTest.cpp:28-56          min x^2 + y^2 s.t. x + y >= 1 -> x = y = 0.5
   model/tests/DoubleIntegratorXYYawTest.cpp:19-47  applyInput with ts = 0.1
   math/tests/CombinatoricsTest.cpp:17-63   fac / comb / perm
+  separating_hyperplanes/tests/VoronoiTest.cpp:10-73  voronoi(p1, p2): normal direction, midpoint
+      on the plane, sides, equidistance (the test's own points and sample parameters)
   cbf/tests/TestInitConnectivity.cpp:103-153  connectivity (lambda2) CBF Ac/Bc, d_max 3.0;
       the intermediate values (lambda2, grad h, Hessian, Lf h, Lf^2 h) are the ones the same
       test run printed, cbf/tests/results.log:7-128 (a data file the reference's tests hold)
@@ -15,6 +17,20 @@ import json
 import os
 
 KATS = {
+    "voronoi": {
+        "source": "separating_hyperplanes/tests/VoronoiTest.cpp:10-73",
+        "tolerance": 1e-10,
+        "cases": [
+            # ComputeVoronoiHyperplane2D (:10-44): normal = (p2 - p1) / |p2 - p1|; the midpoint on
+            # the plane; p1 on the negative side, p2 on the positive side; equal distances
+            {"name": "ComputeVoronoiHyperplane2D", "p1": [1.0, 1.0], "p2": [4.0, 5.0],
+             "expected_normal": [0.6, 0.8], "midpoint": [2.5, 3.0], "p1_side": "<0", "p2_side": ">0"},
+            # EquidistanceProperty (:46-70): points n_perp t - n offset / |n|^2, t = -5 + 10 i / 10,
+            # i = 0..9, lie on the plane and are equidistant from p1 and p2
+            {"name": "EquidistanceProperty", "p1": [2.5, -1.0], "p2": [-3.0, 4.0],
+             "t": [-5.0 + 10.0 * i / 10 for i in range(10)]},
+        ],
+    },
     "connectivity_cbf": {
         "source": "cbf/tests/TestInitConnectivity.cpp:103-153, cbf/tests/results.log:7-128",
         "d_min": 0.8, "d_max": 3.0, "lambda2_min": 0.1,

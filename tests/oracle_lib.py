@@ -103,6 +103,7 @@ def lib():
                                             C.c_int32, ip, dp, dp, ip, dp, dp, ip]
         L.orc_distance_to_ellipse.restype = C.c_double
         L.orc_distance_to_ellipse.argtypes = [dp, dp, dp]
+        L.orc_voronoi.argtypes = [dp, dp, dp, dp, dp]
         L.orc_impc_batch.restype = C.c_int64
         L.orc_impc_batch.argtypes = [C.POINTER(OrcParams), C.c_int32, dp, dp, ip, ip, C.c_int32,
                                      C.c_int32, C.c_int32, ip, dp, dp, dp]
@@ -201,6 +202,15 @@ def solve_dense_qp(qp):
 def distance_to_ellipse(robot, mean, cov3):
     """FovBezierIMPCCBF::distanceToEllipse; cov3 = (cxx, cxy, cyy)."""
     return lib().orc_distance_to_ellipse(_d(robot), _d(mean), _d(cov3))
+
+
+def voronoi(self_xy, other_xy, bbox=(0.0, 0.0, 0.0)):
+    """(normal (3), offset) of the Voronoi hyperplane of two planar points, box-shifted."""
+    n = np.zeros(3)
+    off = np.zeros(1)
+    lib().orc_voronoi(_d(np.asarray(self_xy, dtype=np.float64)), _d(np.asarray(other_xy, dtype=np.float64)),
+                      _d(np.asarray(bbox, dtype=np.float64)), _d(n), _d(off))
+    return n, float(off[0])
 
 
 def impc_optimize(p: OrcParams, states, self_idx, neighbor_idx, ref, covs=None):

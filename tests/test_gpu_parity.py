@@ -687,3 +687,46 @@ def _live_cbf_rows(cfg, states, rp, col):
             bmax = np.sum(np.maximum(-a * amin, -a * amax))
             out[i] += int(b < bmax)
     return out
+
+
+@pytest.mark.parametrize("what", ["neighbour", "target", "state"])
+def test_non_finite_inputs_are_never_optimal(mpclib, what):
+    """A NaN neighbour state, target or own state must not come back OPTIMAL (the dual
+    active-set scan treats a NaN row as satisfied; it gives up instead and the PDIP's finiteness
+    checks decide). Agents packed so the affected agent has live CBF rows; the other agents'
+    statuses and optima are unchanged against the oracle on the finite inputs."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(64)
+    states[:, :2] *= 0.5
+    rp, col = swarm.knn_csr(states, 8, 3 * cfg["d_min"])
+    bad = 27
+    nb = int(col[rp[bad]])
+    st, tg = states.copy(), targets.copy()
+    if what == "neighbour":
+        st[nb, 0] = np.nan  # agent `bad` sees it; so does every other agent with nb in its list
+        hit = [a for a in range(64) if nb in col[rp[a]:rp[a + 1]]] + [nb]
+    elif what == "target":
+        tg[bad, 1] = np.nan
+        hit = [bad]
+    else:
+        st[bad, 3] = np.inf
+        hit = [bad]
+    # agents that see the bad state (an infinite velocity may give an infinite, dropped row)
+    skip = set(hit) | {a for a in range(64) if (nb if what == "neighbour" else bad) in col[rp[a]:rp[a + 1]]}
+    ctx = mpclib.Context(cfg)
+    for dual_res in (True, False):  # the solver's acceptance must not depend on dual_res
+        dev = torch.device("cuda", 0)
+        out = ctx.alloc_outputs(64)
+        if not dual_res:
+            out["dual_res"] = None
+        ctx.impc_solve(torch.tensor(st, device=dev), torch.tensor(rp, device=dev), torch.tensor(col, device=dev),
+                       targets=torch.tensor(tg, device=dev), **out)
+        torch.cuda.synchronize()
+        status = out["status"].cpu().numpy()
+        for a in hit:
+            assert status[a, 0] != O.OPTIMAL, (what, a, status[a])
+            assert status[a, 1] != O.OPTIMAL, (what, a, status[a])
+    g = {k: v.cpu().numpy() for k, v in out.items() if v is not None}
+    others = [a for a in range(64) if a not in skip][:24]
+    compare(cfg, g, run_oracle(cfg, states, targets, rp, col, others), others)

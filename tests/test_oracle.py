@@ -124,3 +124,40 @@ def test_knn_and_all_neighbours_agree_on_lattice(oracle):
         r2 = oracle.impc_optimize(p, states, a, cola[rpa[a]:rpa[a + 1]], refs[a])
         assert list(r1["status"]) == list(r2["status"])
         np.testing.assert_allclose(r1["obj"], r2["obj"], rtol=1e-8)
+
+
+def test_slack_mode_all_neighbours_objective_independent_solver(oracle):
+    """The oracle's slack-mode objective with every other robot as a neighbour (the reference's
+    all-(N-1) lists, ConnectivityIMPCCBF.cpp:59-67,73-119: slack weights slack_cost * decay^rank
+    over 11 neighbours, 5e4 down to 5e-6, some slacks positive) against an independent solve of
+    the same assembled QP by scipy's trust-constr. This pins the oracle's slack polish
+    (oracle.cpp, orc_impc_optimize: v_i = max(0, max row excess) after the dense solve) with a
+    solver that shares no code with it or with the GPU."""
+    from scipy.optimize import Bounds, LinearConstraint, minimize
+    cfg = swarm.config(15, slack_mode=1)
+    p = O.make_params(cfg)
+    states, targets = swarm.lattice_swarm(12)
+    states[:, :2] *= 0.45  # packed: CBF rows active, slacks positive for close neighbours
+    refs = swarm.refs_from_targets(targets, 15)
+    big = 1e300
+    for i in (0, 2):
+        nbr = [j for j in range(12) if j != i]
+        r = oracle.impc_optimize(p, states, i, nbr, refs[i])
+        assert r["status"][0] == O.OPTIMAL
+        d = np.hypot(states[nbr, 0] - states[i, 0], states[nbr, 1] - states[i, 1])
+        order = sorted(range(len(nbr)), key=lambda k: (d[k], k))
+        rank = np.empty(len(nbr), int)
+        rank[order] = np.arange(len(nbr))
+        w = cfg["slack_cost"] * cfg["slack_decay_rate"] ** rank
+        q = oracle.assemble_qp(p, states[i], refs[i], states[nbr], it=0, slack_w=w)
+        inf = lambda a, s: np.where(s * a >= big, s * np.inf, a)  # noqa: E731
+        H, c, c0 = q["H"], q["c"], q["c0"]
+        res = minimize(lambda x: x @ H @ x + c @ x + c0, np.zeros(q["n"]), jac=lambda x: 2 * H @ x + c,
+                       hess=lambda x: 2 * H, method="trust-constr",
+                       constraints=[LinearConstraint(q["A"], inf(q["lo"], -1), inf(q["hi"], 1))],
+                       bounds=Bounds(inf(q["vlo"], -1), inf(q["vhi"], 1)),
+                       options=dict(gtol=1e-12, xtol=1e-14, maxiter=20000))
+        assert res.constr_violation <= 1e-9
+        assert abs(res.fun - r["obj"][0]) <= 1e-6 * max(1.0, abs(r["obj"][0])), (i, res.fun, r["obj"][0])
+        if i == 2:  # a case where the slacks carry most of the cost
+            assert r["obj"][0] > 1e6

@@ -193,3 +193,38 @@ def test_fov_slack_qp_structure_and_weights(oracle):
                             slack_w=1000.0 * 0.5 ** np.arange(4))
     r2 = O.impc_optimize(p, states, 0, nb, ref)
     assert abs(r2["obj"][0] - oracle.solve_dense_qp(q2)["obj"]) <= 1e-9 * max(1, abs(r2["obj"][0]))
+
+
+def voronoi_kat_checks(vor_fn, case, tol):
+    """The expectations of separating_hyperplanes/tests/VoronoiTest.cpp:10-73 for one case;
+    vor_fn(p1, p2) -> (normal (2+), offset) with bbox 0."""
+    p1, p2 = np.array(case["p1"]), np.array(case["p2"])
+    n, off = vor_fn(p1, p2)
+    n = np.asarray(n, dtype=np.float64)[:2]
+    ev = lambda p: float(n @ p + off)  # noqa: E731
+    if case["name"] == "ComputeVoronoiHyperplane2D":
+        np.testing.assert_allclose(n, case["expected_normal"], atol=tol)
+        assert abs(ev(np.array(case["midpoint"]))) <= tol
+        assert ev(p1) < 0.0 and ev(p2) > 0.0
+        nn = np.linalg.norm(n)
+        assert abs(abs(ev(p1)) / nn - abs(ev(p2)) / nn) <= tol
+    else:
+        perp = np.array([-n[1], n[0]])
+        for t in case["t"]:
+            pt = perp * t - n * off / (n @ n)
+            assert abs(ev(pt)) <= tol
+            assert abs(np.linalg.norm(pt - p1) - np.linalg.norm(pt - p2)) <= tol
+
+
+def test_voronoi_kats(oracle):
+    """The oracle's Voronoi rows (oracle.cpp voronoi_shifted, zero box) pass the reference's own
+    VoronoiTest known-answer tests (reference_kats.json "voronoi")."""
+    k = json.load(open(os.path.join(os.path.dirname(GOLDEN), "reference_kats.json")))["voronoi"]
+    assert [c["name"] for c in k["cases"]] == ["ComputeVoronoiHyperplane2D", "EquidistanceProperty"]
+    for case in k["cases"]:
+        voronoi_kat_checks(lambda a, b: O.voronoi(a, b), case, k["tolerance"])
+        # the shift by the robot box moves the plane towards self by |n| . box (planar extents)
+        n0, off0 = O.voronoi(case["p1"], case["p2"])
+        n1, off1 = O.voronoi(case["p1"], case["p2"], (0.2, 0.3, 0.1))
+        np.testing.assert_array_equal(n0, n1)
+        assert abs(off1 - (off0 + 0.2 * abs(n0[0]) + 0.3 * abs(n0[1]))) <= 1e-14

@@ -73,3 +73,21 @@ def test_hipsolver_solves_on_gpu(mpclib):
     x, fun = _problem1_reference()
     np.testing.assert_allclose(p1["x"], x, atol=1e-6)
     assert abs(p1["obj"] - fun) <= 1e-6 * max(1.0, abs(fun))
+
+
+def test_problem_mirror_passes_reference_problem_tests(mpclib):
+    """The reference's qpcpp/tests/ProblemTest.cpp:19-137 (all 11 bookkeeping tests: counts,
+    variable limits, hasVariable, solution values, constraint / cost coefficients, symmetric
+    quadratic lookup, clear / reset) restated in hipsolver_check against the qpcpp::Problem
+    mirror that qpcpp::HIPSolver flattens."""
+    if not os.path.exists(EXE):
+        pytest.fail(f"{EXE} not built (make -C mpc-cbf_amd)")
+    out = subprocess.run([EXE, "problemtest"], capture_output=True, text=True, timeout=60)
+    lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")]
+    names = [r["test"] for r in lines]
+    assert names == ["InitialProblemStateIsEmpty", "AddingVariablesIncreasesCount", "VariableMinMaxLimits",
+                     "HasVariableTest", "VariableSolutionValueTest", "AddingConstraintsIncreasesCount",
+                     "ConstraintCoefficients", "ClearingConstraints", "CostFunctionLinearTerms",
+                     "CostFunctionQuadraticTerms", "ResetProblem"]
+    assert all(r["ok"] for r in lines), [r for r in lines if not r["ok"]]
+    assert out.returncode == 0
