@@ -63,6 +63,13 @@ def parse():
                     help="native: mpccbf_run_steps (C++ loop, RCCL); python: one call per step")
     ap.add_argument("--neighbours", choices=["grid", "csr"], default="grid",
                     help="grid: fused in-kernel spatial-hash query; csr: separate KNN kernels")
+    ap.add_argument("--crowded", action="store_true",
+                    help="collision workload on a crowded lattice (0.6 x the spacing: 3 m, jitter +-0.3 m), "
+                         "where the dual active set and the interior-point fallback do the work")
+    ap.add_argument("--no-trace", action="store_true",
+                    help="skip the closed-loop safety metrics pass (collision_check.py on the trace)")
+    ap.add_argument("--dump", default="",
+                    help="write the timed pass's per-step status / solver-step logs (rank 0) to this .npz")
     return ap.parse_args()
 
 
@@ -218,7 +225,7 @@ def main():
     else:
         cfg = swarm.config(args.k_hor, **slack)
         radius = 3.0 * cfg["d_min"]
-        states_h, targets_h = swarm.lattice_swarm(total)
+        states_h, targets_h = swarm.lattice_swarm(total, spacing_scale=0.6 if args.crowded else 1.0)
     # neighbour-estimate covariances (FoV slack weights): the FoV example's 0.1 I for everyone
     cov_h = np.tile([0.1, 0.0, 0.1], (total, 1)) if (fov and args.slack) else None
     cov = None if cov_h is None else torch.tensor(cov_h, dtype=torch.float64, device=dev)
@@ -241,6 +248,7 @@ def main():
         torch.cuda.synchronize()
 
     replay_same = None
+    trace_res = None
     if args.loop == "native" and args.neighbours == "grid":
         # the whole closed loop in libmpccbf (mpccbf_run_steps): per step the fused IMPC kernel
         # (neighbour query, both IMPC QPs, next-step neighbour table) and, across ranks, one
@@ -288,6 +296,29 @@ def main():
         _, rr = closed_loop(logs[1], timing=True)
         step_ms, kern_ms = rr["step_ms"].astype(np.float64), rr["solve_ms"].astype(np.float64)
         replay_same = bool(torch.equal(logs[0][0], logs[1][0]) and torch.equal(logs[0][1], logs[1][1]))
+        if world == 1 and not args.no_trace:
+            # the same closed loop once more, one step per call, every step's state table kept:
+            # the trace the reference's collision_check.py scores (outside the timed region)
+            tables = [full0.clone(), torch.empty_like(full0)]
+            traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
+            out["x"].fill_(float("nan"))
+            nt = args.warmup + nsteps
+            trace_dev = torch.empty((nt + 1, total, 6), dtype=torch.float64, device=dev)
+            trace_dev[0].copy_(tables[0])
+            common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn, knn_radius=radius,
+                          x=out["x"], obj=out["obj"], traj_t=traj_t, pos_std=0.001, vel_std=0.01,
+                          noise_seed=20251015, cov=cov, status=out["status"], iters=out["iters"])
+            last_status = None
+            for s in range(nt):
+                r = ctx.run_steps(tables[0], tables[1], 1, step_index=s, **common)
+                if r["final"] is not tables[0]:
+                    tables.reverse()
+                trace_dev[s + 1].copy_(tables[0])
+                if s == nt - 1:
+                    last_status = out["status"].clone()
+            trace_h = trace_dev.cpu().numpy()
+            trace_res = dict(traj=np.transpose(trace_h, (1, 0, 2)), last_status=last_status.cpu().numpy())
+            del trace_dev
         if comm is not None:
             comm.close()
     else:
@@ -336,6 +367,8 @@ def main():
 
     status = logs[0][0].cpu().numpy()
     iters = logs[0][1].cpu().numpy()
+    if args.dump and rank == 0:
+        np.savez_compressed(args.dump, status=status, iters=iters, kernel_ms=np.asarray(kern_ms))
     attempted = ~((status == 5) & (iters == 0))  # UNKNOWN with 0 steps: iteration not attempted
     hist = {name: int(np.sum((status == code) & attempted)) for code, name in STATUS_NAMES.items()}
     hist["not_attempted"] = int(np.sum(~attempted))
@@ -416,7 +449,8 @@ def main():
                     (f"config5: {total} agents ({per}/GPU), FoV 120 deg + Voronoi CBF, horizon "
                      f"{cfg['k_hor']}, 4 Bezier pieces, {args.knn} nearest observed within {radius:g} m"
                      if fov else
-                     f"config3: {total} agents, horizon {cfg['k_hor']}, pairwise collision CBF, "
+                     f"config3{' crowded (0.6 x spacing)' if args.crowded else ''}: {total} agents, horizon "
+                     f"{cfg['k_hor']}, pairwise collision CBF, "
                      f"knn{args.knn} r={radius:g}m ({args.neighbours})")
                     + (f", slack_mode (cost 1000, decay {args.slack_decay:g})" if args.slack else "")
                     + ", base_config.json; 2 IMPC QPs/agent/step"
@@ -435,7 +469,8 @@ def main():
             "qps_optimal_frac": hist["OPTIMAL"] / max(attempted_n, 1),
             "status_hist": hist,
             "newton_steps_per_qp": ({"mean_by_step": [round(float(v), 3) for v in newton_mean],
-                                     "max_by_step": [int(v) for v in newton_max]}
+                                     "max_by_step": [int(v) for v in newton_max],
+                                     "kernel_us_by_step": [round(float(v) * 1e3, 1) for v in kern_ms]}
                                     if nsteps <= 64 else
                                     {"mean": float(np.mean(newton_mean)), "max": int(np.max(newton_max))}),
             "roofline": {
@@ -476,6 +511,15 @@ def main():
         }
         if replay_same is False:
             res["roofline"]["kernel_timing"] += " (WARNING: replay statuses differ)"
+        occ, occ_src = resource_lookup(kname, "occupancy")
+        sq_wait, _ = pmc_lookup(kname, wl, "SQ_WAIT_ANY")
+        sq_cyc, sq_src = pmc_lookup(kname, wl, "SQ_WAVE_CYCLES")
+        res["roofline"]["occupancy_waves_per_simd"] = occ
+        res["roofline"]["occupancy_source"] = occ_src
+        res["roofline"]["sq_wait_frac"] = (sq_wait / sq_cyc) if (sq_wait is not None and sq_cyc) else None
+        res["roofline"]["sq_wait_source"] = sq_src
+        if trace_res is not None:
+            res["closed_loop"] = closed_loop_metrics(trace_res, targets_h, cfg, fov)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h)
         print(json.dumps(res), flush=True)
@@ -510,6 +554,54 @@ def pmc_lookup(kname: str, workload: str, field: str):
                 if isinstance(v, dict) and match(name) and field in v:
                     return float(v[field]), os.path.relpath(f, REPO)
     return None, None
+
+
+def resource_lookup(kname: str, field: str):
+    """`field` (vgpr, agpr, scratch, lds, occupancy) of kernel `kname` from the newest committed
+    resource table (profiles/r*_resource_usage.txt, tools/resource_usage.py: hipcc
+    -Rpass-analysis=kernel-resource-usage of the same sources). (None, None) if absent."""
+    import glob
+    cols = {"vgpr": 1, "agpr": 2, "scratch": 3, "lds": 4, "occupancy": 5}
+    key = kname.replace(" ", "")
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_resource_usage.txt")), reverse=True):
+        for ln in open(f):
+            parts = ln.split()
+            if len(parts) < 6:
+                continue
+            name = "".join(parts[:-5]).replace(" ", "")
+            rest = name[len(key) - 1:-1].split(",")[1:] if key.endswith(">") and name.startswith(key[:-1] + ",") else None
+            # exact, or the kernel's own name with defaulted template arguments (", false>")
+            if name == key or (rest is not None and all(r == "false" for r in rest)):
+                return int(parts[-6 + cols[field]]), os.path.relpath(f, REPO)
+    return None, None
+
+
+def closed_loop_metrics(tr, targets_h, cfg, fov):
+    """The reference's post-processing checks (collision_check.py:48-80, mpccbf.metrics, shape =
+    base_config.json's aligned_box [0.2, 0.2], goal radius 1 m) on the closed-loop trace (every
+    control step of warm-up + timed steps), the smallest pair distance, and whether the last step's
+    INFEASIBLE QPs are controller semantics: agents that entered the step within d_min of a
+    neighbour (a CBF row no acceleration satisfies, ConnectivityIMPCCBF.cpp:199-211)."""
+    from scipy.spatial import cKDTree
+    from mpccbf import metrics
+    traj = tr["traj"]
+    ok, makespan, hit = metrics.instance_success_sparse(traj, targets_h, 1.0, [0.2, 0.2], "box")
+    last_in = traj[:, -2, :2]  # the states the last step's QPs were built from
+    d1, _ = cKDTree(last_in).query(last_in, k=2)
+    within = d1[:, 1] < cfg["d_min"]
+    infeas = tr["last_status"][:, 0] == 3
+    return {
+        "steps_traced": int(traj.shape[1] - 1),
+        "instance_success": bool(ok),
+        "makespan_steps": (None if makespan == float("inf") else int(makespan)),
+        "first_collision": (None if hit is None else {"step": hit[0], "i": hit[1], "j": hit[2]}),
+        "min_pair_distance_m": metrics.min_pair_distance_sparse(traj),
+        "final_goal_reached_frac": float(np.mean(metrics.reach_goal_area(traj[:, -1, :2], targets_h[:, :2], 1.0))),
+        "last_step_infeasible_agents": int(infeas.sum()),
+        "last_step_infeasible_within_dmin": int((infeas & within).sum()),
+        "last_step_agents_within_dmin": int(within.sum()),
+        "shape": "box [0.2, 0.2] (base_config.json robot_params.collision_shape), goal radius 1 m",
+    }
 
 
 def pmc_traffic(kname: str, workload: str):

@@ -29,8 +29,10 @@ const char* impc_kernel_name(const DevOps& op, int variant);
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
 hipError_t launch_fov_rows_eval(int count, const double* ego, const double* nb, double fov, double Ds, double Rs,
                                 double bbx, double bby, double* vor, double* rows, hipStream_t s);
-hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
+hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide,
+                                hipStream_t s);
 bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k);
+bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k);
 int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
                      double radius, int32_t* row_ptr, int32_t* col, void* scratch,
                      size_t scratch_bytes, hipStream_t s);
@@ -119,6 +121,8 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "states / neighbour CSR missing");
     if (grid && (b->knn_k < 1 || !(b->knn_radius > 0)))
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
+    if (grid && b->knn_k > NB_MAX)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours: knn_k > 16 not supported (give CSR lists)");
     if (!b->targets && !b->refs) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "targets or refs required");
     if (b->traj_t && !b->x)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "traj_t (closed-loop fallback) needs the persistent x buffer");
@@ -176,8 +180,9 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.substeps = b->substeps;
     if (b->substeps && !b->traj_t)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "substeps (closed-loop records) needs traj_t");
-    // capacity fallback: agents beyond the separable kernel's 16 CBF row slots are deferred to a
-    // second launch of the same solver with 128 slots (only when the slots can be exceeded)
+    // fallback launch: agents the main launch defers (the lean launch: QPs that need the PDIP or
+    // phase 1; beyond the separable kernel's 16 CBF row slots) are solved by a second launch of
+    // the full separable pipeline (128 slots when the 16 can be exceeded)
     const bool fb = c->dev.cbf_mode != 1 && impc_may_defer(c->dev, c->variant, !grid, b->knn_k);
     if (fb && c->defer_cap < b->num_agents) {
         if (c->defer) (void)hipFree(c->defer);
@@ -195,7 +200,7 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
         ImpcArgs f = a;
         f.defer = nullptr;
         f.queue = c->defer;
-        e = launch_impc_fallback(c->dev, c->dbuf, f, stream);
+        e = launch_impc_fallback(c->dev, c->dbuf, f, impc_rows_may_exceed(c->dev, !grid, b->knn_k), stream);
         // the fallback's last block empties the queue; if it never ran, the agents the main
         // launch appended are dropped here, so the next main launch starts from an empty queue
         if (e != hipSuccess) (void)hipMemsetAsync(c->defer, 0, 2 * sizeof(int32_t), stream);
@@ -417,6 +422,8 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
         if (f) d.fast_start = atoi(f);
         const char* g = getenv("MPCCBF_DUAL_AS");
         if (g) d.dual_as = atoi(g);
+        const char* l = getenv("MPCCBF_LEAN");
+        d.lean = l ? atoi(l) : 0;  // measured no faster at occupancy 1
     }
     c->variant = 0;
     hipError_t e = hipSetDevice(c->device);

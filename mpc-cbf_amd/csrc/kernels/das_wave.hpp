@@ -56,14 +56,16 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
     return xl;
 }
 
-// Returns 1: optimal (sc.y, rp_out, rd_out; the active rows' multipliers in ws.u[0 .. ws.k)); -1: no step reaches the candidate (no feasible
-// point; tlow = the certificate's lower bound on phase 1's t*); 0: gave up (step limit,
+// Returns 1: optimal (sc.y, rp_out, rd_out; the active rows' multipliers in ws.u[0 .. ws.k)); -1: no
+// step reaches the candidate (no feasible point; tlow = the certificate's lower bound on phase
+// 1's t*; cand = the unreachable candidate's image row, the active rows in ws.row[0 .. ws.k) with
+// their certificate weights in ws.u: candidate + sum_a u_a n_a = 0); 0: gave up (step limit,
 // breakdown, dual residual) — the PDIP solves.
 // Pinv: P^-1 padded to 16 x 16 (global); P for the dual residual (want_rd).
 __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, WaveScratch& sc,
                               WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
                               double tol, int maxstep, bool want_rd, int lane, double& rp_out,
-                              double& rd_out, int& steps, double& tlow) {
+                              double& rd_out, int& steps, double& tlow, int* cand = nullptr) {
     const int i = lane16_opaque(lane);
     steps = 0;
     for (int e = lane; e < WNZ * WNZ; e += 64) ws.Pi[(e >> 4) * 17 + (e & 15)] = ldg_nohoist(Pinv + e);
@@ -146,6 +148,10 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
             if (l < 0 && !full) {
                 // certificate lam = (1, -r) >= 0 (every r <= 0): t* >= vp / (1 - sum r)
                 tlow = vp * rcp(1.0 + grp_sum<16>((i < k && r_i < 0.0) ? -r_i : 0.0));
+                if (lane < WNZ) ws.u[lane] = (i < k && r_i < 0.0) ? -r_i : 0.0;
+                if (lane == 0) ws.k = k;
+                if (cand) *cand = rp;
+                wave_lds_sync();
                 return -1;
             }
             const double t = fmin(t1, t2);

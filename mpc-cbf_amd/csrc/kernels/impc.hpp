@@ -49,6 +49,9 @@ struct DevOps {
     int32_t early_it;
     int32_t fast_start;  // PdipCfg::fast_start
     int32_t dual_as;     // PdipCfg::dual_as (first attempt)
+    // separable layout: the main launch runs the fast start and the dual active set only and
+    // defers agents that need the PDIP or phase 1 to the fallback launch (0: one full launch)
+    int32_t lean;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;
@@ -78,7 +81,8 @@ struct GridArgs {
     double cone;   // > 0: keep only agents whose bearing is within +-cone of the ego yaw (FoV)
 };
 
-constexpr int NB_CAP = 64;  // grid-mode candidate capacity per agent (LDS)
+constexpr int NB_CAP = 64;  // grid mode: candidates ranked at once (more: the streaming query)
+constexpr int NB_MAX = 16;  // grid mode: at most this many nearest neighbours per agent (knn_k)
 
 // bucket of uniform cell (cx, cy) in a power-of-two hash table (mask = size - 1)
 __host__ __device__ inline uint32_t cell_hash(long long cx, long long cy, uint32_t mask) {

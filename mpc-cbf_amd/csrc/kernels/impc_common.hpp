@@ -57,11 +57,131 @@ __device__ __forceinline__ bool nb_before(double da, int ja, double db, int jb) 
     return da < db || (da == db && ja < jb);
 }
 
+// The query of grid_neighbors when more than NB_CAP candidates lie within the radius (crowds, the
+// reference's all-(N-1) semantics at short range): no cap — the candidate list (hs, nc, off,
+// total, full as grid_neighbors built them) is streamed 16 entries at a time through a running
+// k-nearest set: lane l of each 16-lane row holds the l-th nearest so far; a chunk's candidates
+// within the radius and the kept set are ranked against each other by DPP row broadcasts and the
+// first k go back to the lanes by rank (through sc's first NB_MAX entries). Leaves the k nearest
+// in sc.idx / sc.cst[.] positions 0 .. nk-1 sorted by agent index (sc.src[p] = p); returns nk.
+// G = 64: the four rows of the wave run the same query redundantly.
+template <int G>
+__device__ __forceinline__ int grid_neighbors_stream(const ImpcArgs& args, int self, double px, double py,
+                                                  NbScratch& sc, int gl, double yaw, const uint32_t (&hs)[9],
+                                                  const uint32_t (&nc)[9], const uint32_t (&off)[9], uint32_t total,
+                                                  bool full) {
+    static_assert(G == 16 || G == 64, "16-lane rows");
+    const int l = gl & 15;
+    const GridArgs& gr = args.grid;
+    const double r2 = gr.radius * gr.radius;
+    const int k = gr.k < NB_MAX ? gr.k : NB_MAX;
+    // the kept set (lane l: the l-th nearest so far; unused: (1e300, INT_MAX))
+    double kd = 1e300, kx = 0.0, ky = 0.0, kvx = 0.0, kvy = 0.0;
+    int kj = 0x7fffffff, nk = 0;
+    for (uint32_t t0 = 0; t0 < total; t0 += 16) {
+        const uint32_t t = t0 + l;
+        bool keep = false;
+        int j = 0x7fffffff;
+        double d2 = 1e300, nx = 0.0, ny = 0.0, nvx = 0.0, nvy = 0.0;
+        if (t < total) {
+            if (full) {
+                j = (int)t;
+            } else {
+                uint32_t e = 0;
+#pragma unroll
+                for (int c = 0; c < 9; c++)  // the cell whose range holds t
+                    if (off[c] <= t && t - off[c] < nc[c]) e = (t - off[c]) * (gr.mask + 1u) + hs[c];
+                j = (int)gr.slots[e];
+            }
+            nx = args.states[(size_t)j * 6];
+            ny = args.states[(size_t)j * 6 + 1];
+            nvx = args.states[(size_t)j * 6 + 3];
+            nvy = args.states[(size_t)j * 6 + 4];
+            const double ex = nx - px;
+            const double ey = ny - py;
+            const double dd = ex * ex + ey * ey;
+            keep = (j != self) && (dd <= r2);
+            if (keep && gr.cone > 0.0) {  // inside the field of view (strict)
+                double offa = atan2(ey, ex) - yaw;
+                offa -= 6.283185307179586 * rint(offa * 0.15915494309189535);
+                keep = fabs(offa) < gr.cone;
+            }
+            d2 = dd;
+        }
+        const unsigned long long msk = grp_ballot<16>(keep);
+        if (msk == 0ull) continue;
+        const double dn = keep ? d2 : 1e300;
+        const int jn = keep ? j : 0x7fffffff;
+        // ranks in (kept set) U (this chunk's candidates); the kept set is sorted, so a kept entry
+        // is preceded by the l kept entries before it and by the candidates nearer than it
+        int r_old = l, r_new = 0;
+        auto rank_step = [&](double dm, int jm, double dk, int jk) {
+            r_old += nb_before(dm, jm, kd, kj) ? 1 : 0;
+            r_new += (nb_before(dm, jm, dn, jn) ? 1 : 0) + (nb_before(dk, jk, dn, jn) ? 1 : 0);
+        };
+#define MPCCBF_NB_RANK(K) \
+    rank_step(row_bcast_k<K>(dn), row_bcast_i<K>(jn), row_bcast_k<K>(kd), row_bcast_i<K>(kj));
+        // (scheduling barriers every four broadcasts: hoisted together, the 64 broadcast values
+        // would stay live at once)
+        MPCCBF_NB_RANK(0) MPCCBF_NB_RANK(1) MPCCBF_NB_RANK(2) MPCCBF_NB_RANK(3)
+        __builtin_amdgcn_sched_barrier(0);
+        MPCCBF_NB_RANK(4) MPCCBF_NB_RANK(5) MPCCBF_NB_RANK(6) MPCCBF_NB_RANK(7)
+        __builtin_amdgcn_sched_barrier(0);
+        MPCCBF_NB_RANK(8) MPCCBF_NB_RANK(9) MPCCBF_NB_RANK(10) MPCCBF_NB_RANK(11)
+        __builtin_amdgcn_sched_barrier(0);
+        MPCCBF_NB_RANK(12) MPCCBF_NB_RANK(13) MPCCBF_NB_RANK(14) MPCCBF_NB_RANK(15)
+#undef MPCCBF_NB_RANK
+        wave_lds_sync();  // the previous chunk's reads of the buffer are done
+        auto put = [&](int s, int jj, double dd, double x, double y, double vx, double vy) {
+            sc.idx[s] = jj;
+            sc.d2[s] = dd;
+            sc.cst[0][s] = x;
+            sc.cst[1][s] = y;
+            sc.cst[2][s] = vx;
+            sc.cst[3][s] = vy;
+        };
+        if (l < nk && r_old < k) put(r_old, kj, kd, kx, ky, kvx, kvy);
+        if (keep && r_new < k) put(r_new, jn, dn, nx, ny, nvx, nvy);
+        nk += __popcll(msk);
+        nk = nk < k ? nk : k;
+        wave_lds_sync();
+        if (l < nk) {
+            kj = sc.idx[l];
+            kd = sc.d2[l];
+            kx = sc.cst[0][l];
+            ky = sc.cst[1][l];
+            kvx = sc.cst[2][l];
+            kvy = sc.cst[3][l];
+        }
+    }
+    // the kept set ordered by agent index: position = kept entries with a smaller index
+    int pos = 0;
+#define MPCCBF_NB_POS(K) pos += row_bcast_i<K>(kj) < kj ? 1 : 0;
+    MPCCBF_NB_POS(0) MPCCBF_NB_POS(1) MPCCBF_NB_POS(2) MPCCBF_NB_POS(3)
+    MPCCBF_NB_POS(4) MPCCBF_NB_POS(5) MPCCBF_NB_POS(6) MPCCBF_NB_POS(7)
+    MPCCBF_NB_POS(8) MPCCBF_NB_POS(9) MPCCBF_NB_POS(10) MPCCBF_NB_POS(11)
+    MPCCBF_NB_POS(12) MPCCBF_NB_POS(13) MPCCBF_NB_POS(14) MPCCBF_NB_POS(15)
+#undef MPCCBF_NB_POS
+    wave_lds_sync();
+    if (l < nk) {
+        sc.idx[pos] = kj;
+        sc.src[pos] = pos;
+        sc.d2[pos] = kd;
+        sc.cst[0][pos] = kx;
+        sc.cst[1][pos] = ky;
+        sc.cst[2][pos] = kvx;
+        sc.cst[3][pos] = kvy;
+    }
+    wave_lds_sync();
+    return nk;
+}
+
 // k nearest other agents (planar distance, ties by index) within the radius, found through the
-// spatial hash; the result is left in sc.idx sorted by agent index. Returns the count, or -1 if
-// more than NB_CAP candidates lie within the radius. Distance-only test: agents of a colliding
-// cell that share a bucket are still filtered by distance, and a bucket reached from two of the
-// 9 cells is scanned once.
+// spatial hash; the result is left in sc.idx sorted by agent index (sc.src: each one's slot in
+// sc.cst). Returns the count. Up to NB_CAP candidates within the radius are gathered and ranked at
+// once; beyond, grid_neighbors_stream re-runs the query without a cap. Distance-only test: agents
+// of a colliding cell that share a bucket are still filtered by distance, and a bucket reached
+// from two of the 9 cells is scanned once.
 template <int G>
 __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double py, NbScratch& sc,
                               int gl, double yaw = 0.0) {
@@ -133,7 +253,7 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         }
         cnt += __popcll(msk);
     }
-    if (cnt > NB_CAP) return -1;
+    if (cnt > NB_CAP) return grid_neighbors_stream<G>(args, self, px, py, sc, gl, yaw, hs, nc, off, total, full);
     wave_lds_sync();
     // rank by (d2, index): keep the k nearest
     const int k = gr.k;

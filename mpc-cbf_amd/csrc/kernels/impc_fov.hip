@@ -285,8 +285,21 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         int nit = 0;
         double prs = __builtin_nan(""), drs = __builtin_nan("");
         double vobj = 0.0;  // slack mode: sum_i w_i v_i (addSlackCost, MPCCBFQPGeneratorBase.cpp:121-130)
-        if (mtot > WROWS || nb_overflow || (SLACK && 4 * nchunk + WSL_CROWS > WROWS)) {
-            st = ST_ERROR;  // capacity (rows per agent / observed neighbours)
+        // non-finite data (a NaN / Inf state, target or neighbour position): not solved, ERROR
+        bool nfin = lane < WNZ && !isfinite(sc.q[lane]);
+        for (int r = lane; r < mtot && r < WROWS; r += 64) {
+            nfin = nfin || !isfinite(rlo[r]) || !isfinite(rhi[r]);
+            for (int j = 0; j < WNZ; j++) nfin = nfin || !isfinite(Gimg[r * WNZ + j]);
+        }
+        if constexpr (SLACK) {  // the slack rows (lane = row) and the neighbours' slack weights
+            if (slk->live[lane] != 0.0) {
+                nfin = nfin || !isfinite(slk->h[lane]);
+                for (int j = 0; j < WNZ; j++) nfin = nfin || !isfinite(slk->Go[lane * WNZ + j]);
+            }
+            nfin = nfin || ((lane >> 3) < nnb && !isfinite(slk->w[lane >> 3]));
+        }
+        if (mtot > WROWS || nb_overflow || (SLACK && 4 * nchunk + WSL_CROWS > WROWS) || __ballot(nfin) != 0ull) {
+            st = ST_ERROR;  // capacity (rows per agent / observed neighbours) / non-finite data
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
         } else {
@@ -335,10 +348,13 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 // v_i: at v_i = 0 the FoV multipliers sum to at most w_i; with a leader, its own
                 // multiplier w_i - sum(others) - mu_i is >= 0). All start at v = 0; a neighbour
                 // over its cost takes its largest-multiplier row as leader, one with a negative
-                // leader multiplier the next-largest; after SLK_PATTERNS patterns, or when a pattern
-                // has no feasible point, the slack PDIP solves.
+                // leader multiplier the next-largest. A pattern without a feasible point relaxes a
+                // FoV row of its infeasibility certificate: the unreachable candidate when it is a
+                // slack row (it leads its neighbour), else the certificate's active slack row of
+                // largest weight whose neighbour has no leader. After SLK_PATTERNS patterns, or
+                // when no rule applies, the slack PDIP solves.
 #ifndef MPCCBF_SLK_PATTERNS
-#define MPCCBF_SLK_PATTERNS 4
+#define MPCCBF_SLK_PATTERNS 8
 #endif
                 constexpr int SLK_PATTERNS = MPCCBF_SLK_PATTERNS;
                 const bool lv = slk->live[lane] != 0.0;
@@ -373,11 +389,33 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                             sc.q[lane] = qv;
                         }
                         wave_lds_sync();
-                        int st_ = 0;
+                        int st_ = 0, cand = -1;
                         das = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
                                              opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as, args.dual_res != nullptr,
-                                             lane, drp, drd, st_, dtlow);
+                                             lane, drp, drd, st_, dtlow, &cand);
                         tot_steps += st_;
+                        if (das < 0) {
+                            // no feasible point with this pattern: a FoV row of the certificate
+                            // takes the slack (wave-uniform choice, every lane scans the same LDS)
+                            int pick = -1;
+                            if (cand >= mtot) {
+                                const int sl = slk->rowl[cand - mtot];
+                                if (slk->lead[sl >> 3] != sl) pick = sl;  // (not the leader's own bound)
+                            } else {
+                                double best = 0.0;
+                                for (int a = 0; a < was.k; a++) {
+                                    const int r = was.row[a];
+                                    if (r < mtot || was.sg[a] < 0.0) continue;
+                                    const int sl = slk->rowl[r - mtot];
+                                    if (slk->lead[sl >> 3] < 0 && was.u[a] > best) best = was.u[a], pick = sl;
+                                }
+                            }
+                            if (pick < 0) break;
+                            wave_lds_sync();
+                            if (lane == 0) slk->lead[pick >> 3] = pick;
+                            das = 0;
+                            continue;
+                        }
                         if (das != 1) break;
                         wave_lds_sync();
                         // per neighbour (lane g < nnb): multipliers of its upper sides, of its leader's

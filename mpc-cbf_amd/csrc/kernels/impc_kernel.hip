@@ -134,8 +134,17 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
         int st;
         int nit = 0;
         double prs = __builtin_nan(""), drs = __builtin_nan("");
-        if (count > cap || nb_overflow) {
-            st = ST_ERROR;  // capacity (the 64-lane instantiation takes up to 256 rows)
+        bool nfin = false;  // non-finite data: not solved, ERROR (see impc_sep_agent)
+#pragma unroll
+        for (int j = 0; j < NZ; j++) nfin = nfin || !isfinite(q[j]);
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            nfin = nfin || !isfinite(rw.lo[r]) || !isfinite(rw.hi[r]);
+#pragma unroll
+            for (int j = 0; j < NZ; j++) nfin = nfin || !isfinite(rw.g[r][j]);
+        }
+        if (count > cap || nb_overflow || grp_ballot<G>(nfin) != 0ull) {
+            st = ST_ERROR;  // capacity (CBF rows beyond this instantiation's slots) / non-finite data
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
         } else {
@@ -329,7 +338,7 @@ __device__ __forceinline__ void defer_agent(const ImpcArgs& args, int ai, int gl
 
 // One agent's IMPC step on the separable layout (the body of impc_sep_kernel). stage / red / nbs:
 // this group's LDS (CBF-row staging, Newton-sum all-reduce, neighbour query).
-template <int SB, int CB, bool SLACK, bool QUEUE>
+template <int SB, int CB, bool SLACK, bool QUEUE, bool LEAN = false>
 __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
                                const int ai, const int gl, double* stage, double* red, NbScratch& nbs,
                                double* keep) {
@@ -396,7 +405,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     for (int i = 0; i < NZ; i++) y[i] = ykeep[16 * i] = 0.0;
     // the agent's state, kept for the CBF rows and the outputs (group-uniform: LDS broadcast reads
     // instead of further global round trips)
-    double* s0k = keep + 16 * (SEP_NZ + 2 * SEP_D * SB);
+    double* s0k = keep + 16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB));
     {
         double v = s0[0];
 #pragma unroll
@@ -454,10 +463,51 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         int st;
         int nit = 0;
         double prs = __builtin_nan(""), drs = __builtin_nan("");
-        if (count > cap || nb_overflow || slack_overflow) {
+        // non-finite data (a NaN / Inf state, target or neighbour state): such a model is not
+        // solved (CPLEX rejects non-finite coefficients); reported as ERROR
+        bool nfin = false;
+#pragma unroll
+        for (int j = 0; j < NZ; j++) nfin = nfin || !isfinite(q[j]);
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int k = 0; k < SB; k++) nfin = nfin || !isfinite(rw.blo[d][k]) || !isfinite(rw.bhi[d][k]);
+#pragma unroll
+        for (int c = 0; c < CB; c++)
+            nfin = nfin || !isfinite(rw.chi[c]) || !isfinite(rw.cg[c][0]) || !isfinite(rw.cg[c][1]) ||
+                   !isfinite(rw.cg[c][2]) || !isfinite(rw.cg[c][3]);
+        const bool nonfinite = grp_ballot<G>(nfin) != 0ull;
+        if (count > cap || nb_overflow || slack_overflow || nonfinite) {
             st = ST_ERROR;
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
+        } else if constexpr (LEAN) {
+            // lean main launch: the fast start and the dual active set only. A QP that needs more
+            // (the active set gives up, or no feasible point without a certificate well above the
+            // tolerance: phase 1) defers the whole agent to the fallback launch, which runs the
+            // full pipeline (PDIP attempts, phase 1) on the same inputs — so the main kernel's
+            // registers are those of the active-set path, not the interior-point solver's.
+            const double* Pi = opp(buf, op.o_Pinv);
+            double yu[NZ];
+#pragma unroll
+            for (int d = 0; d < SEP_D; d++) {
+                const int o = 2 * d;
+                yu[o] = -fma(Pi[3 * d], q[o], Pi[3 * d + 1] * q[o + 1]);
+                yu[o + 1] = -fma(Pi[3 * d + 1], q[o], Pi[3 * d + 2] * q[o + 1]);
+            }
+            double tl = 0.0;
+            const int r = sep_dual_as<G, SB, CB>(rw, live, opp(buf, op.o_Pr), Pi, q, yu, op.tol, op.dual_as, stage, y,
+                                                 prs, drs, nit, nullptr, true, tl);
+            if (r > 0) {
+                st = ST_OPTIMAL;
+            } else if (r < 0 && tl > 10.0 * op.feas_tol) {
+                st = ST_INFEASIBLE;
+                prs = tl;
+                drs = __builtin_nan("");
+            } else {
+                defer_agent(args, ai, gl);
+                return;
+            }
         } else {
 #ifdef MPCCBF_PDIP_STAMPS
             long long* dbg = (args.stamps && it == 0)
@@ -561,30 +611,33 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     stamp(args, ai, gl, 7);
 }
 
-// QUEUE = false: one agent per 16-lane group. QUEUE = true (capacity fallback): the agents the main
-// launch deferred (args.queue: [count, blocks done, agents...]), grid-stride; the last block to
-// finish empties the queue for the next step.
-template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false>
+// QUEUE = false: one agent per 16-lane group. QUEUE = true (fallback launch): the agents the main
+// launch deferred (args.queue: [count, blocks done, agents...]), one per group (the grid covers
+// every agent of the batch); the last block to finish empties the queue for the next step.
+template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = false>
 __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
                                                        const ImpcArgs args) {
     constexpr int GPB = BS / 16;
     __shared__ double stage_all[GPB][SLACK ? 1 : CB * 16 * (SEP_NZ + 1)];
-    __shared__ double red_all[GPB][16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
+    __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
-    __shared__ double keep_all[GPB][16 * (SEP_NZ + 2 * SEP_D * SB) + 8];
+    // kept solution | warm-start duals (not in the lean launch) | the agent's state
+    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     if constexpr (!QUEUE) {
         grid_clear(args);
         const int ai = blockIdx.x * GPB + gib;
         if (ai >= args.num_agents) return;
-        impc_sep_agent<SB, CB, SLACK, false>(op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib],
-                                      keep_all[gib]);
+        impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
+                                                   nb_scratch[gib], keep_all[gib]);
     } else {
-        const int n = args.queue[0];
-        for (int k = blockIdx.x * GPB + gib; k < n; k += gridDim.x * GPB)
+        // one queue entry per group (no grid-stride loop: carried across iterations the agent's
+        // state spills); groups beyond the queue's length leave at once
+        const int k = blockIdx.x * GPB + gib;
+        if (k < args.queue[0])
             impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
-                                          nb_scratch[gib], keep_all[gib]);
+                                                nb_scratch[gib], keep_all[gib]);
         __syncthreads();
         if (threadIdx.x == 0) {
             __threadfence();
@@ -608,33 +661,48 @@ static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcA
     return hipGetLastError();
 }
 
-template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false>
+template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false, bool LEAN = false>
 static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                     hipStream_t s) {
     constexpr int GPB = BS / 16;
     int blocks = (a.num_agents + GPB - 1) / GPB;
-    if (QUEUE) blocks = blocks < 64 ? blocks : 64;  // grid-stride over the deferred agents
-    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE>), dim3(blocks), dim3(BS), 0, s, op, buf, a);
+    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE, LEAN>), dim3(blocks), dim3(BS), 0, s, op, buf,
+                       a);
     return hipGetLastError();
 }
 
-// Agents beyond the default separable kernel's capacity are deferred to this launch: more than
-// 16 live CBF rows in an IMPC iteration — the same solver with 8 CBF row slots per lane (128
-// rows) in 64-thread blocks; slack mode with more than 16 neighbours — the slack solver, the
-// neighbours with a live row compacted into the lanes. Agents beyond that report ERROR.
-hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
-    if (a.num_agents <= 0 || !a.queue) return hipSuccess;
-    if (op.slack_mode) return launch_impc_sep_t<1, 2, true, 64, true>(op, buf, a, s);
-    return launch_impc_sep_t<1, 8, false, 64, true>(op, buf, a, s);
+// The separable layout's lean main launch (fast start + dual active set; everything else deferred)
+static bool sep_lean(const DevOps& op, int variant) {
+    return variant == 0 && !op.slack_mode && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 &&
+           op.lean && op.dual_as > 0;
 }
 
-// Whether launch_impc defers agents (so launch_impc_fallback must follow): the separable kernel,
-// when its 16 CBF row slots can be exceeded (caller lists, or k nearest x CBF samples > 16).
+// Agents the main launch deferred are solved by this launch (the queue in a.queue):
+//   slack mode, more than 16 neighbours — the slack solver, the neighbours with a live row
+//   compacted into the lanes;
+//   otherwise — the full separable pipeline (dual active set, PDIP attempts, phase 1): with 16 CBF
+//   row slots when no agent can exceed them, else 8 slots per lane (128 rows). Agents beyond
+//   that report ERROR.
+hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide,
+                                hipStream_t s) {
+    if (a.num_agents <= 0 || !a.queue) return hipSuccess;
+    if (op.slack_mode) return launch_impc_sep_t<1, 2, true, 64, true>(op, buf, a, s);
+    if (wide) return launch_impc_sep_t<1, 8, false, 64, true>(op, buf, a, s);
+    return launch_impc_sep_t<1, 1, false, 64, true>(op, buf, a, s);
+}
+
+// Whether some agent can exceed the default separable kernel's 16 CBF row slots (caller lists,
+// or k nearest x CBF samples > 16).
+bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k) { return csr || knn_k * op.cbf_h > 16; }
+
+// Whether launch_impc defers agents (so launch_impc_fallback must follow): the lean main launch
+// always may; the full separable kernel when its 16 CBF row slots can be exceeded.
 bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k) {
     if (op.slack_mode)
         return op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2 && (csr || knn_k > 16);
+    if (sep_lean(op, variant)) return true;
     if (!(variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)) return false;
-    return csr || knn_k * op.cbf_h > 16;
+    return impc_rows_may_exceed(op, csr, knn_k);
 }
 
 // Instantiation launch_impc picks for (operators, variant); nullptr if none fits.
@@ -642,6 +710,7 @@ const char* impc_kernel_name(const DevOps& op, int variant) {
     if (op.slack_mode)  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2
         return (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
                    ? "impc_sep_kernel<1,2,true,256>" : nullptr;
+    if (sep_lean(op, variant)) return "impc_sep_kernel<1,1,false,256,false,true>";
     if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false,256>";
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
@@ -651,11 +720,6 @@ const char* impc_kernel_name(const DevOps& op, int variant) {
     return nullptr;
 }
 
-// Returns hipErrorInvalidValue if no instantiation fits (nz, m).
-//   variant 0: separable layout when the operators allow it (16 lanes, 16 box rows per channel,
-//              16 CBF rows), else 16 lanes x 4 dense slots
-//   variant 1: dense, 64 lanes x 1 slot;  variant 2: dense, 64 lanes x 4 slots (wide rows)
-//   variant 3: dense, 16 lanes x 4 slots (the pre-separable default)
 hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
                        hipStream_t s) {
     if (a.num_agents <= 0) return hipSuccess;
@@ -664,6 +728,7 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
             return launch_impc_sep_t<1, 2, true>(op, buf, a, s);
         return hipErrorInvalidValue;
     }
+    if (sep_lean(op, variant)) return launch_impc_sep_t<1, 1, false, 256, false, true>(op, buf, a, s);
     if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)
         return launch_impc_sep_t<1, 1, false>(op, buf, a, s);
     if (op.nz == 6) {

@@ -51,6 +51,47 @@ def instance_success(traj, goals, radius, collision_shape, shape_type):
     return True, ts, None
 
 
+def instance_success_sparse(traj, goals, radius, collision_shape, shape_type):
+    """instance_success for large swarms: the same walk and the same result, with each step's
+    colliding pairs found among the pairs a k-d tree returns within the largest distance at which
+    the shape test can hold (circle: 2 r; box: centre offsets below 2 x half on both axes, so
+    within 2 |half|), so a step costs
+    O(n log n) instead of the script's O(n^2)."""
+    from scipy.spatial import cKDTree
+    traj = np.asarray(traj, dtype=np.float64)
+    goals = np.asarray(goals, dtype=np.float64)
+    n, ts = traj.shape[0], traj.shape[1]
+    if shape_type == "circle":
+        reach = 2.0 * float(collision_shape) * (1.0 + 1e-12)
+    else:
+        reach = 2.0 * float(np.hypot(collision_shape[0], collision_shape[1])) * (1.0 + 1e-12)
+    reached = np.zeros(n, dtype=bool)
+    for t in range(ts):
+        if reached.all():
+            return True, max(0, t - 1), None
+        p = traj[:, t, :2]
+        reached |= reach_goal_area(p, goals[:, :2], radius)
+        pairs = cKDTree(p).query_pairs(reach, output_type="ndarray")
+        if len(pairs):
+            i, j = pairs.min(axis=1), pairs.max(axis=1)
+            hit = collision_check(p[i, 0], p[i, 1], p[j, 0], p[j, 1], collision_shape, shape_type)
+            if np.any(hit):
+                k = np.lexsort((j[hit], i[hit]))[0]  # first pair in the script's (i, j) order
+                return False, float("inf"), (t, int(i[hit][k]), int(j[hit][k]))
+    return True, ts, None
+
+
+def min_pair_distance_sparse(traj):
+    """min_pair_distance through a k-d tree per step (large swarms)."""
+    from scipy.spatial import cKDTree
+    traj = np.asarray(traj, dtype=np.float64)
+    best = np.inf
+    for t in range(traj.shape[1]):
+        d, _ = cKDTree(traj[:, t, :2]).query(traj[:, t, :2], k=2)
+        best = min(best, float(d[:, 1].min()))
+    return best
+
+
 def min_pair_distance(traj):
     """Smallest planar distance between two robots over the run (a safety margin summary)."""
     traj = np.asarray(traj, dtype=np.float64)

@@ -71,15 +71,16 @@ def validate(cfg: dict) -> None:
 
 
 def lattice_swarm(n_agents: int, d_min: float = 2.0, seed: int = SEED, v_range: float = 0.5,
-                  target_radius: float = 3.0):
-    """Returns states (N, 6) = [px, py, yaw, vx, vy, vyaw] and targets (N, 3)."""
+                  target_radius: float = 3.0, spacing_scale: float = 1.0):
+    """Returns states (N, 6) = [px, py, yaw, vx, vy, vyaw] and targets (N, 3). Lattice spacing
+    2.5 d_min and jitter +-0.25 d_min, both times spacing_scale (< 1: a crowded swarm)."""
     rng = np.random.default_rng(seed)
     side = int(math.ceil(math.sqrt(n_agents)))
-    spacing = 2.5 * d_min
+    spacing = 2.5 * d_min * spacing_scale
     idx = np.arange(n_agents)
     gx = (idx % side).astype(np.float64) * spacing
     gy = (idx // side).astype(np.float64) * spacing
-    jit = rng.uniform(-0.25 * d_min, 0.25 * d_min, size=(n_agents, 2))
+    jit = rng.uniform(-0.25 * d_min * spacing_scale, 0.25 * d_min * spacing_scale, size=(n_agents, 2))
     states = np.zeros((n_agents, 6))
     states[:, 0] = gx + jit[:, 0]
     states[:, 1] = gy + jit[:, 1]

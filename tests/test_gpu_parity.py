@@ -730,3 +730,41 @@ def test_non_finite_inputs_are_never_optimal(mpclib, what):
     g = {k: v.cpu().numpy() for k, v in out.items() if v is not None}
     others = [a for a in range(64) if a not in skip][:24]
     compare(cfg, g, run_oracle(cfg, states, targets, rp, col, others), others)
+
+
+@pytest.mark.parametrize("fov", [False, True])
+def test_grid_neighbours_crowd_beyond_candidate_capacity(mpclib, fov):
+    """More than 64 agents within the query radius of every agent (a 12 x 12 block at 0.45 m
+    spacing, radius 6 m: up to 143 candidates): the query switches to its uncapped streaming form
+    (grid_neighbors_stream) instead of reporting ERROR, and the k nearest it keeps equal the CPU
+    lists: grid path == CSR path (statuses, objectives), collision and FoV controllers."""
+    torch = _torch()
+    n = 144
+    g = np.arange(n)
+    states = np.zeros((n, 6))
+    states[:, 0], states[:, 1] = 0.45 * (g % 12), 0.45 * (g // 12)
+    states[:, 2] = 0.3 * np.sin(g)  # yaw (FoV cones differ per agent)
+    targets = states[:, :3].copy()
+    targets[:, 0] += 1.5
+    if fov:
+        cfg = swarm.fov_config(20)
+        radius = cfg["fov_Rs"]
+        rp, col = swarm.fov_csr(states, 8, radius, cfg["fov_beta"])
+    else:
+        cfg = swarm.config(15)
+        radius = 6.0
+        rp, col = swarm.knn_csr(states, 8, radius)
+    d2 = np.sum((states[:, None, :2] - states[None, :, :2]) ** 2, axis=-1)
+    assert np.all(np.sum(d2 <= radius * radius, axis=1) - 1 > 64)  # every agent: > 64 in range
+    dev = torch.device("cuda", 0)
+    ctx = mpclib.Context(cfg)
+    st, tg = torch.tensor(states, device=dev), torch.tensor(targets, device=dev)
+    o_csr, o_grid = ctx.alloc_outputs(n), ctx.alloc_outputs(n)
+    ctx.impc_solve(st, torch.tensor(rp, device=dev), torch.tensor(col, device=dev), targets=tg, **o_csr)
+    ctx.impc_solve(st, targets=tg, knn_k=8, knn_radius=radius, **o_grid)
+    torch.cuda.synchronize()
+    s_csr, s_grid = o_csr["status"].cpu().numpy(), o_grid["status"].cpu().numpy()
+    assert not np.any(s_grid[:, 0] == O.ERROR)
+    np.testing.assert_array_equal(s_grid, s_csr)
+    ok = s_csr == 0
+    np.testing.assert_allclose(o_grid["obj"].cpu().numpy()[ok], o_csr["obj"].cpu().numpy()[ok], rtol=1e-10, atol=1e-9)

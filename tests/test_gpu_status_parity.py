@@ -31,12 +31,14 @@ def _torch():
     return torch
 
 
-def _check_agents(cfg, states, targets, agents, g_status, g_obj, g_x=None):
+def _check_agents(cfg, states, targets, agents, g_status, g_obj, g_x=None, cov=None, lists=None):
+    """lists: per agent its neighbour list (default: the 8 nearest within 3 d_min)."""
     p = O.make_params(cfg)
     refs = swarm.refs_from_targets(targets, cfg["k_hor"])
     rp, col = swarm.knn_csr(states, 8, 3.0 * cfg["d_min"])
     for a in agents:
-        r = O.impc_optimize(p, states, a, col[rp[a]:rp[a + 1]], refs[a])
+        nb = lists[a] if lists is not None else col[rp[a]:rp[a + 1]]
+        r = O.impc_optimize(p, states, a, nb, refs[a], covs=cov)
         assert list(g_status[a]) == list(r["status"]), (a, g_status[a], r["status"])
         for it in range(cfg["impc_iter"]):
             if r["status"][it] == O.OPTIMAL:
@@ -55,10 +57,17 @@ def test_regression_cases_match_oracle(mpclib):
     torch = _torch()
     cases = json.load(open(os.path.join(HERE, "golden", "regress_cases.json")))["cases"]
     dev = torch.device("cuda", 0)
+    assert any(c.get("controller") == "fov_slack" for c in cases)
     for case in cases:
-        cfg = swarm.config(case["k_hor"])
         states = np.array(case["states"])
         n = len(states)
+        cov = None
+        if case.get("controller") == "fov_slack":  # FovBezierIMPCCBF in slack mode (config 5)
+            cfg = swarm.fov_config(case["k_hor"], slack_mode=1, slack_cost=case["slack_cost"],
+                                   slack_decay_rate=case["slack_decay_rate"])
+            cov = np.tile(np.array(case["cov"]), (n, 1))
+        else:
+            cfg = swarm.config(case["k_hor"])
         targets = np.tile(np.array(case["target"]), (n, 1))
         rp = np.array([0, n - 1] + [n - 1] * (n - 1), np.int32)
         col = np.arange(1, n, dtype=np.int32)
@@ -66,10 +75,11 @@ def test_regression_cases_match_oracle(mpclib):
         out = ctx.alloc_outputs(1)
         ctx.impc_solve(torch.tensor(states, device=dev), torch.tensor(rp, device=dev),
                        torch.tensor(col, device=dev), targets=torch.tensor(targets[:1], device=dev),
-                       num_agents=1, **out)
+                       num_agents=1, cov=None if cov is None else torch.tensor(cov, device=dev), **out)
         torch.cuda.synchronize()
         g = {k: v.cpu().numpy() for k, v in out.items()}
-        _check_agents(cfg, states, targets, [0], g["status"], g["obj"], g["x"])
+        _check_agents(cfg, states, targets, [0], g["status"], g["obj"], g["x"], cov=cov,
+                      lists={0: np.arange(1, n, dtype=np.int32)})
 
 
 @pytest.mark.parametrize("snaps", [(16, 20, 27)])

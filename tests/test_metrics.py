@@ -49,3 +49,22 @@ def test_goal_not_reached_runs_to_the_end():
     r0 = np.stack([t, 0 * t, 0 * t], axis=1)
     ok, makespan, _ = metrics.instance_success(_traj([r0]), [[9, 9, 0]], 1.0, 0.2, "circle")
     assert ok and makespan == 5
+
+
+def test_sparse_metrics_equal_the_script_form():
+    """instance_success_sparse / min_pair_distance_sparse (k-d tree pairs, used on bench-size
+    swarms) return exactly what the script-form O(n^2) walk returns, for both shapes, on random
+    crowded trajectories with and without collisions."""
+    rng = np.random.default_rng(3)
+    for trial in range(12):
+        n, ts = 40, 15
+        start = rng.uniform(0, 6, (n, 2))
+        goal = rng.uniform(0, 6, (n, 2))
+        w = np.linspace(0.0, 1.0, ts)[None, :, None]
+        traj = np.concatenate([start[:, None, :] * (1 - w) + goal[:, None, :] * w, np.zeros((n, ts, 1))], axis=2)
+        goals = np.concatenate([goal, np.zeros((n, 1))], axis=1)
+        for shape, kind in ((0.2, "circle"), ([0.2, 0.2], "box"), ([0.05, 0.3], "box")):
+            a = metrics.instance_success(traj, goals, 1.0, shape, kind)
+            b = metrics.instance_success_sparse(traj, goals, 1.0, shape, kind)
+            assert a == b, (trial, kind, a, b)
+        assert metrics.min_pair_distance(traj) == metrics.min_pair_distance_sparse(traj)
