@@ -48,6 +48,10 @@ def parse():
     ap.add_argument("--agents-per-gpu", type=int, default=0,
                     help="default 4096 (collision), 512 (fov: config 5 = 4096 agents on 8 GPUs)")
     ap.add_argument("--agents-total", type=int, default=0, help="strong scaling: fixed total")
+    ap.add_argument("--rank-share", type=int, default=0,
+                    help="one GPU times rank 0's share of an N-rank run: agents-total / N agents of "
+                         "the agents-total table, the other rows carried over and inserted into the "
+                         "next step's neighbour table every step (the all-gather itself excluded)")
     ap.add_argument("--k-hor", type=int, default=0, help="default 15 (collision), 20 (fov)")
     ap.add_argument("--knn", type=int, default=8)
     ap.add_argument("--slack", action="store_true",
@@ -213,8 +217,12 @@ def main():
     if args.k_hor <= 0:
         args.k_hor = 20 if fov else 15
     total = args.agents_total if args.agents_total > 0 else args.agents_per_gpu * world
-    per = total // world
-    assert per * world == total, "agents must divide evenly over ranks"
+    shares = world
+    if args.rank_share > 0:
+        assert world == 1, "--rank-share runs on one GPU"
+        shares = args.rank_share
+    per = total // shares
+    assert per * shares == total, "agents must divide evenly over ranks"
     first = rank * per
     slack = dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=args.slack_decay) if args.slack else {}
     if fov:
@@ -296,7 +304,7 @@ def main():
         _, rr = closed_loop(logs[1], timing=True)
         step_ms, kern_ms = rr["step_ms"].astype(np.float64), rr["solve_ms"].astype(np.float64)
         replay_same = bool(torch.equal(logs[0][0], logs[1][0]) and torch.equal(logs[0][1], logs[1][1]))
-        if world == 1 and not args.no_trace:
+        if world == 1 and not args.no_trace and args.rank_share <= 0:
             # the same closed loop once more, one step per call, every step's state table kept:
             # the trace the reference's collision_check.py scores (outside the timed region)
             tables = [full0.clone(), torch.empty_like(full0)]
@@ -368,7 +376,10 @@ def main():
     status = logs[0][0].cpu().numpy()
     iters = logs[0][1].cpu().numpy()
     if args.dump and rank == 0:
-        np.savez_compressed(args.dump, status=status, iters=iters, kernel_ms=np.asarray(kern_ms))
+        extra = {}
+        if trace_res is not None:  # every step's state table (warm-up steps first)
+            extra = dict(traj=trace_res["traj"], warmup=args.warmup)
+        np.savez_compressed(args.dump, status=status, iters=iters, kernel_ms=np.asarray(kern_ms), **extra)
     attempted = ~((status == 5) & (iters == 0))  # UNKNOWN with 0 steps: iteration not attempted
     hist = {name: int(np.sum((status == code) & attempted)) for code, name in STATUS_NAMES.items()}
     hist["not_attempted"] = int(np.sum(~attempted))
@@ -407,7 +418,7 @@ def main():
     # launch when its slots can be exceeded), so the timed region's events divided by the steps
     # are the kernel's average duration without the dispatch gap that per-launch events add
     fallback = kname.startswith("impc_sep_kernel") and not args.slack and args.knn * cfg["cbf_horizon"] > 16
-    kernel_only = world == 1 and region_ms is not None and not fallback
+    kernel_only = world == 1 and region_ms is not None and not fallback and args.rank_share <= 0
     if kernel_only:
         kern_avg = region_ms / nsteps
 
@@ -454,7 +465,10 @@ def main():
                      f"knn{args.knn} r={radius:g}m ({args.neighbours})")
                     + (f", slack_mode (cost 1000, decay {args.slack_decay:g})" if args.slack else "")
                     + ", base_config.json; 2 IMPC QPs/agent/step"
-                    + ("" if world == 1 else f"; {per}/GPU, RCCL all-gather of states")),
+                    + ("" if world == 1 else f"; {per}/GPU, RCCL all-gather of states")
+                    + (f"; rank 0's share of {shares} ranks ({per} of {total} agents; the other rows carried "
+                       "over and inserted into the neighbour table every step, the all-gather excluded)"
+                       if args.rank_share > 0 else "")),
                 "agents_total": total,
                 "agents_per_gpu": per,
                 "k_hor": cfg["k_hor"],

@@ -95,12 +95,13 @@ typedef struct mpccbf_options {
     int32_t no_cbf_filter;     /* 1: keep every CBF row (no exact in-kernel redundancy filter) */
     int32_t max_pdip_iters;    /* default 60 */
     double tolerance;          /* PDIP relative tolerance, default 1e-9 */
-    /* IMPC iteration 1 starts from iteration 0's primal-dual point (same box rows and cost),
-     * slacks and duals floored at warm_delta: 0 = default (0.3), < 0 = cold start. A warm start
-     * that does not converge is certified by phase 1 and, when the QP is feasible, re-solved
-     * cold, so statuses do not depend on it; optima agree within the solver tolerance (a warm
-     * start may converge where a cold one would not). Environment variable MPCCBF_WARM_DELTA
-     * (read here, a number) overrides it for tuning. */
+    /* Interior-point warm start of IMPC iteration 1 — used only when the dual active-set solve
+     * is off (environment MPCCBF_DUAL_AS=0; by default the active set solves first, IMPC
+     * iteration 1 starting from iteration 0's active box sides, and the PDIP runs cold):
+     * iteration 0's primal-dual point, slacks and duals floored at warm_delta: 0 = default
+     * (0.3), < 0 = cold start. A warm start that does not converge is certified by phase 1 and,
+     * when the QP is feasible, re-solved cold, so statuses do not depend on it. Environment
+     * variable MPCCBF_WARM_DELTA (read here, a number) overrides it for tuning. */
     double warm_delta;
 } mpccbf_options;
 
@@ -130,10 +131,14 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *               knn_k nearest others (planar) within knn_radius, found on the device in the same
  *               launch sequence (spatial hash of `states` + in-kernel 3x3-cell query; in
  *               mpccbf_run_steps the IMPC kernel itself fills the next step's hash table);
- *               at most 64 agents within the radius (more: that agent's QP reports ERROR)
+ *               knn_k <= 16; any number of agents within the radius (beyond 64 candidates the
+ *               query streams them through a running k-nearest set)
  *               Capacity: the default separable kernel keeps up to 16 live (unfiltered) CBF rows
  *               per IMPC iteration and agent (slack mode: 16 neighbours); an agent beyond it is
- *               re-solved in the same call by the 64-lane dense instantiation (up to 256 rows)
+ *               re-solved in the same call by the fallback launch of the same separable solver
+ *               with 8 CBF row slots per lane (128 rows; slack mode: the neighbours with a live
+ *               row compacted into the 16 lanes); beyond that its QPs report ERROR. A QP whose
+ *               data is not finite (NaN / Inf state, target or neighbour state) reports ERROR
  * Outputs (device, any may be NULL):
  *   x           num_agents x n: control points of the last OPTIMAL iteration (the curve the
  *               driver keeps, example :160-164); NaN if no iteration was OPTIMAL
@@ -349,8 +354,11 @@ int mpccbf_connectivity_control_solve(const mpccbf_connectivity_control_params* 
  *   minimise  x^T H x + c^T x + c0        (H symmetric: sum_{i<=j} q_ij x_i x_j, CPLEX.cpp:122-147)
  *   s.t.      lo_r <= A_r x <= hi_r       (rows; lo == hi is an equality)
  *             vlo_i <= x_i <= vhi_i
- * Equalities are eliminated on the host (null space), the reduced problem is solved by the GPU
- * interior-point kernel. x_out is written only if *status_out is OPTIMAL (Solver.h:33-35). */
+ * The host validates and packs the nonzeros; the device eliminates the equalities (Householder QR
+ * with column pivoting: null space + minimum-norm particular solution) and solves the reduced
+ * problem with the interior-point kernel. n <= 64, at most 64 equality rows, reduced dimension
+ * <= 8 and 256 reduced rows (MPCCBF_ERR_CAPACITY beyond). x_out is written only if *status_out is
+ * OPTIMAL (Solver.h:33-35). */
 typedef struct mpccbf_dense_qp {
     int32_t n, m;
     const double* H;  /* n x n row-major */

@@ -424,6 +424,8 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
         if (g) d.dual_as = atoi(g);
         const char* l = getenv("MPCCBF_LEAN");
         d.lean = l ? atoi(l) : 0;  // measured no faster at occupancy 1
+        const char* w = getenv("MPCCBF_DAS_WARM");
+        d.das_warm = w ? atoi(w) : 3;  // iteration-0 steps that enable the warm start (0: never)
     }
     c->variant = 0;
     hipError_t e = hipSetDevice(c->device);

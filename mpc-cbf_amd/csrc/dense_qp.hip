@@ -2,9 +2,22 @@
 //
 // This is the path a qpcpp::Solver<double> subclass uses (csrc/qpcpp/HIPSolver.h): it replaces
 // one CPLEXSolver<double>::solve(Problem&) call (qpcpp/src/solvers/CPLEX.cpp:35-177) for any
-// Problem, not only the MPC-CBF one. Host: exact equality elimination (host/dense_qp.cpp).
-// Device: one 64-lane wavefront per QP running the same Mehrotra PDIP + phase-1 certificate
-// as the structured IMPC kernel (kernels/pdip.hpp), reduced dimension padded to 8.
+// Problem, not only the MPC-CBF one.
+//
+// Host: validation (the reference's invalid_argument cases) and a streaming sparse pack of each
+// QP — nonzeros of H, c, c0, and the rows classified as equalities (lo == hi, fixed variables)
+// or inequalities (a finite side; variable bounds as unit rows) in CSR — one host-to-device copy.
+// Device, one 64-lane wavefront per QP, three launches:
+//   dense_reduce_kernel  exact equality elimination: Householder QR with column pivoting of E^T
+//                        (lane = equality row; rank by |R_tt| <= 1e-12 |R_00|), x = xp + Z y with
+//                        xp the minimum-norm solution and Z the orthonormal null-space basis
+//                        (reflections applied to unit vectors), inconsistent equalities ->
+//                        INFEASIBLE; reduced objective 1/2 y^T (2 Z^T Hs Z) y + ..., Cholesky of P;
+//                        inequality rows g = Z^T a with bounds shifted by a^T xp (constant rows
+//                        decided here), compacted;
+//   dense_qp_kernel      the Mehrotra PDIP + phase-1 certificate of the structured kernel
+//                        (kernels/pdip.hpp), reduced dimension padded to 8;
+//   dense_expand_kernel  x = xp + Z y and the full-space objective x^T H x + c^T x + c0.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -15,38 +28,320 @@
 #include <vector>
 
 #include "../../include/mpccbf.h"
-#include "host/dense_qp.hpp"
 #include "host/errors.hpp"
+#include "kernels/group.hpp"
 #include "kernels/pdip.hpp"
 
 namespace mpccbf {
 
-constexpr int DQ_R = DENSE_ROWS / 64;               // row slots per lane
+constexpr int DENSE_NZ = 8;        // reduced dimension (padded)
+constexpr int DENSE_ROWS = 256;    // reduced inequality rows: 64 lanes x 4 slots
+constexpr int DENSE_NMAX = 64;     // variables per QP (lane = variable)
+constexpr int DENSE_EMAX = 64;     // equalities per QP (lane = equality)
+constexpr int DQ_R = DENSE_ROWS / 64;
 constexpr int DQ_HDR = 2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 2;  // P, LP, q, reg, pad
-constexpr int DQ_ROW = DENSE_NZ + 2;                // g, lo, hi
+constexpr int DQ_ROW = DENSE_NZ + 2;                            // g, lo, hi
+constexpr int DQ_STRIDE = DQ_HDR + DENSE_ROWS * DQ_ROW;        // reduced QP, doubles
+constexpr double kInf = 1e300;     // |bound| >= 1e300 means "absent" (numeric_limits lowest/max)
+constexpr double kFeasTol = 1e-6;  // CPLEX default feasibility tolerance (CPLEX.cpp:8 default ctor)
+// reduce-kernel statuses beyond qpcpp::SolveStatus: -1 = the PDIP solves it; capacity errors
+constexpr int RS_SOLVE = -1, RS_CAP_NZ = -2, RS_CAP_ROWS = -3;
 
-struct DenseArgs {
-    const double* buf;     // per QP: [P | LP | q | reg, 0 | rows (g, lo, hi) x m]
-    const int32_t* off;    // offset of each QP in buf (doubles)
-    const int32_t* m;      // rows per QP
-    const int32_t* pd;     // 1: LP holds the Cholesky factor of P
+// Packed QP (host -> device). Integers: [n, me, mi, nh | H index (i n + j) x nh | eq row ptr
+// (me + 1) | eq cols | in row ptr (mi + 1) | in cols]. Doubles: [c (n) | c0 | H values (nh) | eq rhs
+// (me) | eq values | in lo (mi) | in hi (mi) | in values]. Row pointers are relative to the QP.
+struct DenseBatch {
+    const double* dbl;
+    const int32_t* ints;
+    const int64_t* off_d;  // per QP
+    const int64_t* off_i;
     int32_t count;
+    double* red;      // count x DQ_STRIDE reduced QPs (the PDIP's input)
+    double* zx;       // count x (DENSE_NMAX x DENSE_NZ + DENSE_NMAX): Z row-major, then xp
+    int32_t* status;  // count: decided status or RS_*
+    int32_t* m;       // count: reduced rows
+    int32_t* pd;      // count: 1 if P is positive definite (LP its factor)
+    double* y;        // count x DENSE_NZ
+    int32_t* iters;
+    double* x;        // count x DENSE_NMAX
+    double* obj;      // count
     int32_t maxit;
     double tol;
     double feas_tol;
-    double* y;             // count x DENSE_NZ
-    int32_t* status;
-    int32_t* iters;
 };
 
 namespace dev {
 
+constexpr int LDS_S = DENSE_EMAX + 1;  // row stride of the E^T image (odd: spread banks)
+
+struct ReduceLds {
+    double et[DENSE_NMAX * LDS_S];   // E^T: row i = variable, column c = equality (lane c)
+    double z[DENSE_NMAX * DENSE_NZ]; // Z row-major
+    double xp[DENSE_NMAX];
+    double hz[DENSE_NMAX * DENSE_NZ];
+    double hx[DENSE_NMAX];
+    double rdiag[DENSE_EMAX], beta[DENSE_EMAX], u[DENSE_EMAX], bp[DENSE_EMAX];
+    double P[DENSE_NZ * DENSE_NZ];
+    double L[DENSE_NZ * DENSE_NZ];
+    int32_t perm[DENSE_EMAX];
+};
+
+__device__ __forceinline__ bool fin_bound(double v) { return isfinite(v) && fabs(v) < kInf; }
+
+__global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
+    const int qi = blockIdx.x;
+    const int l = threadIdx.x;
+    if (qi >= a.count) return;
+    __shared__ ReduceLds s;
+    const int32_t* ib = a.ints + a.off_i[qi];
+    const double* db = a.dbl + a.off_d[qi];
+    const int n = ib[0], me = ib[1], mi = ib[2], nh = ib[3];
+    const int32_t* hidx = ib + 4;
+    const int32_t* eptr = hidx + nh;
+    const int32_t* ecol = eptr + me + 1;
+    const int32_t* iptr = ecol + eptr[me];
+    const int32_t* icol = iptr + mi + 1;
+    const double* c = db;
+    const double* hval = db + n + 1;
+    const double* erhs = hval + nh;
+    const double* eval = erhs + me;
+    const double* ilo = eval + eptr[me];
+    const double* ihi = ilo + mi;
+    const double* ival = ihi + mi;
+    double* red = a.red + (size_t)qi * DQ_STRIDE;
+    bool infeasible = false;
+
+    // ---- E^T into LDS (lane c: equality c's row as column c), zero elsewhere
+    for (int e = l; e < DENSE_NMAX * LDS_S; e += 64) s.et[e] = 0.0;
+    __syncthreads();
+    if (l < me) {
+        for (int k = eptr[l]; k < eptr[l + 1]; k++) s.et[ecol[k] * LDS_S + l] = eval[k];
+        s.perm[l] = l;
+    }
+    __syncthreads();
+    // ---- Householder QR with column pivoting: E^T Pi = Q R (reflection t stored in column t,
+    // rows t .. n-1; R's diagonal in rdiag)
+    const int tmax = n < me ? n : me;
+    int rank = 0;
+    double r00 = 0.0;
+    for (int t = 0; t < tmax; t++) {
+        double nrm = -1.0;
+        if (l >= t && l < me) {
+            nrm = 0.0;
+            for (int i = t; i < n; i++) nrm = fma(s.et[i * LDS_S + l], s.et[i * LDS_S + l], nrm);
+        }
+        const double best = grp_max<64>(nrm);
+        const int p = __ffsll((long long)__ballot(nrm == best && l >= t && l < me)) - 1;
+        const double sig = sqrt(best);
+        if (t == 0) r00 = sig;
+        if (!(sig > 1e-12 * r00) || p < 0) break;  // the remaining columns are dependent
+        // swap columns t and p (lane i: row i)
+        if (p != t && l < n) {
+            const double v = s.et[l * LDS_S + t];
+            s.et[l * LDS_S + t] = s.et[l * LDS_S + p];
+            s.et[l * LDS_S + p] = v;
+        }
+        if (p != t && l == 0) {
+            const int q = s.perm[t];
+            s.perm[t] = s.perm[p];
+            s.perm[p] = q;
+        }
+        __syncthreads();
+        const double xt = s.et[t * LDS_S + t];
+        const double alpha = xt >= 0.0 ? -sig : sig;
+        const double vt = xt - alpha;
+        const double vn2 = best - xt * xt + vt * vt;  // |v|^2
+        const double bt = vn2 > 0.0 ? 2.0 / vn2 : 0.0;
+        __syncthreads();
+        if (l == 0) {
+            s.et[t * LDS_S + t] = vt;  // v = (vt, x_{t+1}, ...)
+            s.rdiag[t] = alpha;
+            s.beta[t] = bt;
+        }
+        __syncthreads();
+        // apply to columns t+1 .. me-1 (lane c)
+        if (l > t && l < me) {
+            double w = 0.0;
+            for (int i = t; i < n; i++) w = fma(s.et[i * LDS_S + t], s.et[i * LDS_S + l], w);
+            w *= bt;
+            for (int i = t; i < n; i++) s.et[i * LDS_S + l] = fma(-w, s.et[i * LDS_S + t], s.et[i * LDS_S + l]);
+        }
+        __syncthreads();
+        rank = t + 1;
+    }
+    const int nz = n - rank;
+    // ---- particular solution: R11^T u = (Pi^T b)_{1..r}, xp = Q [u; 0]  (minimum norm)
+    if (l < me) s.bp[l] = erhs[s.perm[l]];
+    __syncthreads();
+    for (int t = 0; t < rank; t++) {
+        const double part = (l < t) ? s.et[l * LDS_S + t] * s.u[l] : 0.0;  // R[l][t] u_l, l < t
+        const double sum = grp_sum<64>(part);
+        if (l == 0) s.u[t] = (s.bp[t] - sum) / s.rdiag[t];
+        __syncthreads();
+    }
+    // reflections applied to the vectors [u; 0] and e_{r+j} (lane i: component i)
+    double w = (l < rank) ? s.u[l] : 0.0;
+    double zc[DENSE_NZ];
+#pragma unroll
+    for (int j = 0; j < DENSE_NZ; j++) zc[j] = (l == rank + j && j < nz) ? 1.0 : 0.0;
+    for (int t = rank - 1; t >= 0; t--) {
+        const double vi = (l >= t && l < n) ? s.et[l * LDS_S + t] : 0.0;
+        const double bt = s.beta[t];
+        double d = grp_sum<64>(vi * w);
+        w = fma(-bt * d, vi, w);
+#pragma unroll
+        for (int j = 0; j < DENSE_NZ; j++) {
+            d = grp_sum<64>(vi * zc[j]);
+            zc[j] = fma(-bt * d, vi, zc[j]);
+        }
+    }
+    if (l < DENSE_NMAX) {
+        s.xp[l] = l < n ? w : 0.0;
+#pragma unroll
+        for (int j = 0; j < DENSE_NZ; j++) s.z[l * DENSE_NZ + j] = (l < n && j < nz) ? zc[j] : 0.0;
+        s.hx[l] = 0.0;
+#pragma unroll
+        for (int j = 0; j < DENSE_NZ; j++) s.hz[l * DENSE_NZ + j] = 0.0;
+    }
+    __syncthreads();
+    // inconsistent equalities (redundant rows with a different right-hand side)
+    if (l < me) {
+        double v = 0.0;
+        for (int k = eptr[l]; k < eptr[l + 1]; k++) v = fma(eval[k], s.xp[ecol[k]], v);
+        if (fabs(v - erhs[l]) > kFeasTol) infeasible = true;
+    }
+    // ---- Hs Z and Hs xp from H's nonzeros (Hs = (H + H^T) / 2; LDS atomics)
+    for (int e = l; e < nh; e += 64) {
+        const int i = hidx[e] / n, j = hidx[e] % n;
+        const double hv = 0.5 * hval[e];
+        atomicAdd(&s.hx[i], hv * s.xp[j]);
+        atomicAdd(&s.hx[j], hv * s.xp[i]);
+        for (int b = 0; b < nz && b < DENSE_NZ; b++) {
+            atomicAdd(&s.hz[i * DENSE_NZ + b], hv * s.z[j * DENSE_NZ + b]);
+            atomicAdd(&s.hz[j * DENSE_NZ + b], hv * s.z[i * DENSE_NZ + b]);
+        }
+    }
+    __syncthreads();
+    // P = 2 Z^T Hs Z (lane a * 8 + b), q = Z^T (2 Hs xp + c), k0 (objective constant: unused,
+    // the expansion evaluates the full-space objective)
+    if (nz <= DENSE_NZ) {
+        const int pa = l >> 3, pb = l & 7;
+        double v = 0.0;
+        for (int i = 0; i < n; i++) v = fma(s.z[i * DENSE_NZ + pa], s.hz[i * DENSE_NZ + pb], v);
+        s.P[pa * DENSE_NZ + pb] = 2.0 * v;
+    }
+    __syncthreads();
+    double pmax = 0.0;
+    if (l < DENSE_NZ * DENSE_NZ && nz <= DENSE_NZ) {
+        const int pa = l >> 3, pb = l & 7;
+        const bool in = pa < nz && pb < nz;
+        const double v = in ? 0.5 * (s.P[pa * DENSE_NZ + pb] + s.P[pb * DENSE_NZ + pa]) : (pa == pb ? 1.0 : 0.0);
+        red[l] = v;  // P (padding: identity)
+        pmax = in ? fabs(v) : 0.0;
+    }
+    pmax = grp_max<64>(pmax);
+    __syncthreads();
+    if (l < DENSE_NZ && nz <= DENSE_NZ) {
+        double v = 0.0;
+        if (l < nz)
+            for (int i = 0; i < n; i++) v = fma(s.z[i * DENSE_NZ + l], 2.0 * s.hx[i] + c[i], v);
+        red[2 * DENSE_NZ * DENSE_NZ + l] = v;  // q
+    }
+    // Cholesky of P (lane 0, in LDS; nz <= 8): the PDIP's start factor when P is positive definite
+    int pd = 0;
+    if (l == 0 && nz <= DENSE_NZ) {
+        double* L = s.L;
+        bool ok = nz > 0;
+        for (int j = 0; j < DENSE_NZ * DENSE_NZ; j++) L[j] = 0.0;
+        for (int j = 0; j < nz && ok; j++) {
+            double d = red[j * DENSE_NZ + j];
+            for (int k = 0; k < j; k++) d -= L[j * DENSE_NZ + k] * L[j * DENSE_NZ + k];
+            if (!(d > 0.0)) {
+                ok = false;
+                break;
+            }
+            const double ljj = sqrt(d);
+            L[j * DENSE_NZ + j] = ljj;
+            for (int i = j + 1; i < nz; i++) {
+                double v = red[i * DENSE_NZ + j];
+                for (int k = 0; k < j; k++) v -= L[i * DENSE_NZ + k] * L[j * DENSE_NZ + k];
+                L[i * DENSE_NZ + j] = v / ljj;
+            }
+        }
+        for (int j = 0; j < DENSE_NZ * DENSE_NZ; j++) {
+            const int r = j / DENSE_NZ, cc = j % DENSE_NZ;
+            red[DENSE_NZ * DENSE_NZ + j] = (ok && r < nz) ? L[j] : (r == cc ? 1.0 : 0.0);  // padding: identity
+        }
+        red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ] = ok ? 0.0 : 1e-10 * fmax(1.0, pmax);  // Newton ridge if PSD
+        red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 1] = 0.0;
+        pd = ok ? 1 : 0;
+    }
+    // ---- inequality rows in y: g = Z^T a, bounds shifted by a^T xp; constant rows decided here
+    int cnt = 0;
+    double* rows = red + DQ_HDR;
+    for (int r0 = 0; r0 < mi; r0 += 64) {
+        const int r = r0 + l;
+        bool keep = false;
+        double g[DENSE_NZ], lo = 0.0, hi = 0.0;
+#pragma unroll
+        for (int b = 0; b < DENSE_NZ; b++) g[b] = 0.0;
+        if (r < mi && nz <= DENSE_NZ) {
+            double amax = 0.0, shift = 0.0, gmax = 0.0;
+            for (int k = iptr[r]; k < iptr[r + 1]; k++) {
+                const double av = ival[k];
+                const int j = icol[k];
+                amax = fmax(amax, fabs(av));
+                shift = fma(av, s.xp[j], shift);
+#pragma unroll
+                for (int b = 0; b < DENSE_NZ; b++) g[b] = fma(av, s.z[j * DENSE_NZ + b], g[b]);
+            }
+#pragma unroll
+            for (int b = 0; b < DENSE_NZ; b++) gmax = fmax(gmax, fabs(g[b]));
+            const double rl = ilo[r], rh = ihi[r];
+            const bool hl = fin_bound(rl), hu = fin_bound(rh);
+            if (gmax <= 1e-13 * fmax(1.0, amax)) {  // constant row: a feasibility check of xp
+                if ((hl && shift < rl - kFeasTol) || (hu && shift > rh + kFeasTol)) infeasible = true;
+            } else {
+                keep = true;
+                lo = hl ? rl - shift : -kInf;
+                hi = hu ? rh - shift : kInf;
+            }
+        }
+        const unsigned long long msk = __ballot(keep);
+        const int slot = cnt + __popcll(msk & ((1ull << l) - 1ull));
+        if (keep && slot < DENSE_ROWS) {
+            double* dst = rows + (size_t)slot * DQ_ROW;
+#pragma unroll
+            for (int b = 0; b < DENSE_NZ; b++) dst[b] = g[b];
+            dst[DENSE_NZ] = lo;
+            dst[DENSE_NZ + 1] = hi;
+        }
+        cnt += __popcll(msk);
+    }
+    infeasible = __ballot(infeasible) != 0ull;
+    // ---- expansion data and the decision
+    double* zx = a.zx + (size_t)qi * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX);
+    for (int e = l; e < DENSE_NMAX * DENSE_NZ; e += 64) zx[e] = s.z[e];
+    zx[DENSE_NMAX * DENSE_NZ + l] = s.xp[l];
+    if (l < DENSE_NZ) a.y[(size_t)qi * DENSE_NZ + l] = 0.0;  // (the PDIP overwrites it when it solves)
+    if (l == 0) {
+        int st = RS_SOLVE;
+        if (nz > DENSE_NZ) st = RS_CAP_NZ;
+        else if (cnt > DENSE_ROWS) st = RS_CAP_ROWS;
+        else if (infeasible) st = ST_INFEASIBLE;
+        else if (nz == 0) st = ST_OPTIMAL;  // x = xp is the only point
+        a.status[qi] = st;
+        a.m[qi] = cnt < DENSE_ROWS ? cnt : DENSE_ROWS;
+        a.pd[qi] = pd;
+    }
+}
+
 template <int NZ, int R>
-__global__ void __launch_bounds__(64) dense_qp_kernel(const DenseArgs a) {
+__global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int gl = threadIdx.x;
-    if (qi >= a.count) return;
-    const double* base = a.buf + a.off[qi];
+    if (qi >= a.count || a.status[qi] != RS_SOLVE) return;  // decided by the reduction
+    const double* base = a.red + (size_t)qi * DQ_STRIDE;
     const double* P = base;
     const double* LP = base + NZ * NZ;
     const double* qv = base + 2 * NZ * NZ;
@@ -92,6 +387,31 @@ __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseArgs a) {
     }
 }
 
+// x = xp + Z y (y = 0 when the equalities decided x) and x^T H x + c^T x + c0 for OPTIMAL QPs.
+__global__ void __launch_bounds__(64) dense_expand_kernel(const DenseBatch a) {
+    const int qi = blockIdx.x;
+    const int l = threadIdx.x;
+    if (qi >= a.count || a.status[qi] != ST_OPTIMAL) return;
+    __shared__ double xs[DENSE_NMAX];
+    const int32_t* ib = a.ints + a.off_i[qi];
+    const double* db = a.dbl + a.off_d[qi];
+    const int n = ib[0], nh = ib[3];
+    const int32_t* hidx = ib + 4;
+    const double* c = db;
+    const double* hval = db + n + 1;
+    const double* zx = a.zx + (size_t)qi * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX);
+    double xv = zx[DENSE_NMAX * DENSE_NZ + l];
+#pragma unroll
+    for (int b = 0; b < DENSE_NZ; b++) xv = fma(zx[l * DENSE_NZ + b], a.y[(size_t)qi * DENSE_NZ + b], xv);
+    xs[l] = l < n ? xv : 0.0;
+    __syncthreads();
+    double f = l < n ? c[l] * xv : 0.0;
+    for (int e = l; e < nh; e += 64) f = fma(hval[e] * xs[hidx[e] / n], xs[hidx[e] % n], f);
+    f = grp_sum<64>(f);
+    if (l < n) a.x[(size_t)qi * DENSE_NMAX + l] = xv;
+    if (l == 0) a.obj[qi] = f + db[n];
+}
+
 }  // namespace dev
 
 namespace {
@@ -113,9 +433,164 @@ struct DevBuf {
         return e;
     }
 };
+struct HostBuf {  // pinned staging of the packed QPs
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t reserve(size_t need) {
+        if (p && bytes >= need) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipHostMalloc(&p, need);
+        if (e == hipSuccess) bytes = need;
+        return e;
+    }
+};
 thread_local DevBuf g_dense_buf;
+thread_local HostBuf g_dense_host;
 
-size_t align8(size_t v) { return (v + 7) & ~size_t(7); }
+size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
+
+bool finite_bound(double v) { return std::isfinite(v) && std::fabs(v) < kInf; }
+
+// Host half: validation (the reference's invalid_argument cases: NULL pointers, n < 1, m < 0,
+// non-finite H / c, NaN bounds) and the row classification; sizes of the packed form.
+struct PackPlan {
+    int n = 0, me = 0, mi = 0, nh = 0, enz = 0, inz = 0;
+    size_t nd = 0, ni = 0;  // doubles / ints of the packed QP
+    std::string err;
+    bool cap = false;
+};
+
+PackPlan plan_qp(const mpccbf_dense_qp& qp) {
+    PackPlan pl;
+    auto fail = [&](const char* m) {
+        pl.err = m;
+        return pl;
+    };
+    if (qp.n < 1) return fail("dense QP: n must be >= 1");
+    if (qp.m < 0) return fail("dense QP: m must be >= 0");
+    if (!qp.H || !qp.c) return fail("dense QP: H and c are required");
+    if (qp.m > 0 && !(qp.A && qp.lo && qp.hi)) return fail("dense QP: A, lo, hi are required when m > 0");
+    const int n = qp.n, m = qp.m;
+    pl.n = n;
+    for (size_t k = 0; k < (size_t)n * n; k++) {
+        const double v = qp.H[k];
+        if (!std::isfinite(v)) return fail("dense QP: H has a non-finite entry");
+        pl.nh += v != 0.0;
+    }
+    for (int i = 0; i < n; i++)
+        if (!std::isfinite(qp.c[i])) return fail("dense QP: c has a non-finite entry");
+    for (int k = 0; k < m; k++) {
+        const double lo = qp.lo[k], hi = qp.hi[k];
+        if (std::isnan(lo) || std::isnan(hi)) return fail("dense QP: NaN row bound");
+        const double* a = qp.A + (size_t)k * n;
+        int nnz = 0;
+        for (int j = 0; j < n; j++) nnz += a[j] != 0.0;
+        if (finite_bound(lo) && lo == hi) {
+            pl.me++;
+            pl.enz += nnz;
+        } else if (finite_bound(lo) || finite_bound(hi)) {
+            pl.mi++;
+            pl.inz += nnz;
+        }
+    }
+    for (int i = 0; i < n; i++) {
+        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
+        if (std::isnan(lo) || std::isnan(hi)) return fail("dense QP: NaN variable bound");
+        if (finite_bound(lo) && lo == hi) {
+            pl.me++;
+            pl.enz++;
+        } else if (finite_bound(lo) || finite_bound(hi)) {
+            pl.mi++;
+            pl.inz++;
+        }
+    }
+    pl.cap = n > DENSE_NMAX || pl.me > DENSE_EMAX;
+    pl.ni = 4 + (size_t)pl.nh + (pl.me + 1) + pl.enz + (pl.mi + 1) + pl.inz;
+    pl.nd = (size_t)n + 1 + pl.nh + pl.me + pl.enz + 2 * (size_t)pl.mi + pl.inz;
+    return pl;
+}
+
+void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, int32_t* ib) {
+    const int n = qp.n;
+    ib[0] = n;
+    ib[1] = pl.me;
+    ib[2] = pl.mi;
+    ib[3] = pl.nh;
+    int32_t* hidx = ib + 4;
+    int32_t* eptr = hidx + pl.nh;
+    int32_t* ecol = eptr + pl.me + 1;
+    int32_t* iptr = ecol + pl.enz;
+    int32_t* icol = iptr + pl.mi + 1;
+    double* c = db;
+    double* hval = db + n + 1;
+    double* erhs = hval + pl.nh;
+    double* evalv = erhs + pl.me;
+    double* ilo = evalv + pl.enz;
+    double* ihi = ilo + pl.mi;
+    double* ivalv = ihi + pl.mi;
+    std::memcpy(c, qp.c, (size_t)n * sizeof(double));
+    db[n] = qp.c0;
+    int h = 0;
+    for (int k = 0; k < n * n; k++)
+        if (qp.H[k] != 0.0) {
+            hidx[h] = k;
+            hval[h++] = qp.H[k];
+        }
+    int e = 0, ez = 0, r = 0, rz = 0;
+    eptr[0] = iptr[0] = 0;
+    auto add = [&](bool eq, const double* a, int unit, double lo, double hi) {
+        int32_t* col = eq ? ecol : icol;
+        double* val = eq ? evalv : ivalv;
+        int& z = eq ? ez : rz;
+        if (a) {
+            for (int j = 0; j < n; j++)
+                if (a[j] != 0.0) {
+                    col[z] = j;
+                    val[z++] = a[j];
+                }
+        } else {
+            col[z] = unit;
+            val[z++] = 1.0;
+        }
+        if (eq) {
+            erhs[e] = lo;
+            eptr[++e] = ez;
+        } else {
+            ilo[r] = lo;
+            ihi[r] = hi;
+            iptr[++r] = rz;
+        }
+    };
+    for (int k = 0; k < qp.m; k++) {
+        const double lo = qp.lo[k], hi = qp.hi[k];
+        const double* a = qp.A + (size_t)k * n;
+        if (finite_bound(lo) && lo == hi) add(true, a, 0, lo, hi);
+        else if (finite_bound(lo) || finite_bound(hi)) add(false, a, 0, lo, hi);
+    }
+    for (int i = 0; i < n; i++) {
+        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
+        if (finite_bound(lo) && lo == hi) add(true, nullptr, i, lo, hi);
+        else if (finite_bound(lo) || finite_bound(hi)) add(false, nullptr, i, lo, hi);
+    }
+}
+
+template <typename F>
+void parallel_for(int count, F f) {
+    const int nthr = count >= 64 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
+    if (nthr <= 1) {
+        f(0, count);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const int chunk = (count + nthr - 1) / nthr;
+    for (int t = 0; t < nthr; t++) {
+        const int k0 = t * chunk, k1 = std::min(count, k0 + chunk);
+        if (k0 < k1) pool.emplace_back(f, k0, k1);
+    }
+    for (auto& th : pool) th.join();
+}
 
 }  // namespace
 }  // namespace mpccbf
@@ -128,141 +603,111 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
                                 double* obj_out, int32_t* status_out) {
     if (count < 0 || (count > 0 && (!qps || !status_out)))
         return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "dense QP batch: null argument");
-    // exact equality elimination on the host, QPs split over up to 16 threads (independent)
-    std::vector<ReducedQP> red(count);
-    std::vector<std::string> err(count);
-    auto reduce_range = [&](int k0, int k1) {
-        for (int k = k0; k < k1; k++) {
-            try {
-                red[k] = reduce_dense_qp(qps[k]);
-            } catch (const std::exception& e) {
-                err[k] = e.what();
-            }
-        }
-    };
-    const int nthr = count >= 64 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
-    if (nthr > 1) {
-        std::vector<std::thread> pool;
-        const int chunk = (count + nthr - 1) / nthr;
-        for (int t = 0; t < nthr; t++) {
-            const int k0 = t * chunk, k1 = std::min(count, k0 + chunk);
-            if (k0 < k1) pool.emplace_back(reduce_range, k0, k1);
-        }
-        for (auto& th : pool) th.join();
-    } else {
-        reduce_range(0, count);
-    }
+    if (count == 0) return MPCCBF_OK;
+    // ---- host: validate, plan, pack (QPs split over up to 16 threads)
+    std::vector<PackPlan> plan(count);
+    parallel_for(count, [&](int k0, int k1) {
+        for (int k = k0; k < k1; k++) plan[k] = plan_qp(qps[k]);
+    });
     for (int k = 0; k < count; k++) {  // the first bad QP's error, as a serial pass would report
-        if (!err[k].empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + err[k]);
-        if (red[k].status < 0 && (red[k].nz > DENSE_NZ || red[k].m > DENSE_ROWS))
-            return set_error(MPCCBF_ERR_CAPACITY,
-                             "QP " + std::to_string(k) + ": reduced dimension " + std::to_string(red[k].nz) +
-                                 " / rows " + std::to_string(red[k].m) + " exceed the dense kernel (8 / 256)");
+        if (!plan[k].err.empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + plan[k].err);
+        if (plan[k].cap)
+            return set_error(MPCCBF_ERR_CAPACITY, "QP " + std::to_string(k) + ": " + std::to_string(plan[k].n) +
+                                                      " variables / " + std::to_string(plan[k].me) +
+                                                      " equalities exceed the device elimination (64 / 64)");
     }
-    // pack the QPs that need a device solve
-    std::vector<int> dev_idx;
-    std::vector<double> buf;
-    std::vector<int32_t> off, mrows, pd;
+    std::vector<int64_t> off_d(count), off_i(count);
+    size_t nd = 0, ni = 0;
     for (int k = 0; k < count; k++) {
-        const ReducedQP& r = red[k];
-        if (r.status >= 0) continue;
-        dev_idx.push_back(k);
-        off.push_back((int32_t)buf.size());
-        mrows.push_back(r.m);
-        pd.push_back(r.pd ? 1 : 0);
-        const size_t o = buf.size();
-        buf.resize(o + DQ_HDR + (size_t)r.m * DQ_ROW, 0.0);
-        double* P = &buf[o];
-        double* LP = P + DENSE_NZ * DENSE_NZ;
-        double* q = LP + DENSE_NZ * DENSE_NZ;
-        double pmax = 0.0;
-        for (int a = 0; a < DENSE_NZ; a++)
-            for (int b = 0; b < DENSE_NZ; b++) {
-                const bool in = a < r.nz && b < r.nz;
-                P[a * DENSE_NZ + b] = in ? r.P(a, b) : (a == b ? 1.0 : 0.0);  // padding: identity
-                LP[a * DENSE_NZ + b] = (in && r.pd) ? r.LP(a, b) : (a == b ? 1.0 : 0.0);
-                if (in) pmax = std::max(pmax, std::fabs(r.P(a, b)));
-            }
-        for (int a = 0; a < r.nz; a++) q[a] = r.q[a];
-        q[DENSE_NZ] = r.pd ? 0.0 : 1e-10 * std::max(1.0, pmax);  // Newton-matrix ridge if P is PSD
-        double* rows = P + DQ_HDR;
-        for (int i = 0; i < r.m; i++) {
-            for (int b = 0; b < r.nz; b++) rows[i * DQ_ROW + b] = r.G(i, b);
-            rows[i * DQ_ROW + DENSE_NZ] = r.lo[i];
-            rows[i * DQ_ROW + DENSE_NZ + 1] = r.hi[i];
-        }
+        off_d[k] = (int64_t)nd;
+        off_i[k] = (int64_t)ni;
+        nd += plan[k].nd;
+        ni += plan[k].ni;
     }
-    const int nd = (int)dev_idx.size();
-    std::vector<double> y((size_t)nd * DENSE_NZ);
-    std::vector<int32_t> st(nd), its(nd);
-    if (nd > 0) {
-        int ndev = 0;
-        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
-            return set_error(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
-        int device = 0;
-        hipError_t e = hipGetDevice(&device);
-        const size_t b_buf = align8(buf.size() * sizeof(double));
-        const size_t b_int = align8((size_t)nd * sizeof(int32_t));
-        const size_t b_y = (size_t)nd * DENSE_NZ * sizeof(double);
-        const size_t need = b_buf + 6 * b_int + b_y;
-        if (e == hipSuccess) e = g_dense_buf.reserve(need, device);
-        if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP buffers: ") + hipGetErrorString(e));
-        char* base = (char*)g_dense_buf.p;
-        double* d_buf = (double*)base;
-        int32_t* d_off = (int32_t*)(base + b_buf);
-        int32_t* d_m = (int32_t*)(base + b_buf + b_int);
-        int32_t* d_pd = (int32_t*)(base + b_buf + 2 * b_int);
-        int32_t* d_st = (int32_t*)(base + b_buf + 3 * b_int);
-        int32_t* d_it = (int32_t*)(base + b_buf + 4 * b_int);
-        double* d_y = (double*)(base + b_buf + 6 * b_int);
-        e = hipMemcpy(d_buf, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d_off, off.data(), nd * sizeof(int32_t), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d_m, mrows.data(), nd * sizeof(int32_t), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(d_pd, pd.data(), nd * sizeof(int32_t), hipMemcpyHostToDevice);
-        DenseArgs a;
-        a.buf = d_buf;
-        a.off = d_off;
-        a.m = d_m;
-        a.pd = d_pd;
-        a.count = nd;
-        a.maxit = 100;
-        a.tol = 1e-9;
-        a.feas_tol = 1e-6;
-        a.y = d_y;
-        a.status = d_st;
-        a.iters = d_it;
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, DQ_R>), dim3(nd), dim3(64), 0, 0, a);
-            e = hipGetLastError();
-        }
-        if (e == hipSuccess) e = hipMemcpy(st.data(), d_st, nd * sizeof(int32_t), hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(its.data(), d_it, nd * sizeof(int32_t), hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(y.data(), d_y, b_y, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP solve: ") + hipGetErrorString(e));
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_error(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
+    int device = 0;
+    hipError_t e = hipGetDevice(&device);
+    const size_t b_d = align16(nd * sizeof(double)), b_i = align16(ni * sizeof(int32_t));
+    const size_t b_off = align16((size_t)count * sizeof(int64_t));
+    if (e == hipSuccess) e = g_dense_host.reserve(b_d + b_i + 2 * b_off);
+    if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP staging: ") + hipGetErrorString(e));
+    char* hb = (char*)g_dense_host.p;
+    double* h_d = (double*)hb;
+    int32_t* h_i = (int32_t*)(hb + b_d);
+    std::memcpy(hb + b_d + b_i, off_d.data(), count * sizeof(int64_t));
+    std::memcpy(hb + b_d + b_i + b_off, off_i.data(), count * sizeof(int64_t));
+    parallel_for(count, [&](int k0, int k1) {
+        for (int k = k0; k < k1; k++) pack_qp(qps[k], plan[k], h_d + off_d[k], h_i + off_i[k]);
+    });
+    // ---- device buffers: packed input | reduced QPs | Z, xp | y | x | obj | int outputs
+    const size_t b_red = align16((size_t)count * DQ_STRIDE * sizeof(double));
+    const size_t b_zx = align16((size_t)count * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX) * sizeof(double));
+    const size_t b_y = align16((size_t)count * DENSE_NZ * sizeof(double));
+    const size_t b_x = align16((size_t)count * DENSE_NMAX * sizeof(double));
+    const size_t b_obj = align16((size_t)count * sizeof(double));
+    const size_t b_int = align16((size_t)count * sizeof(int32_t));
+    const size_t in_bytes = b_d + b_i + 2 * b_off;
+    const size_t need = in_bytes + b_red + b_zx + b_y + b_x + b_obj + 4 * b_int;
+    e = g_dense_buf.reserve(need, device);
+    if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP buffers: ") + hipGetErrorString(e));
+    char* base = (char*)g_dense_buf.p;
+    DenseBatch a;
+    a.dbl = (const double*)base;
+    a.ints = (const int32_t*)(base + b_d);
+    a.off_d = (const int64_t*)(base + b_d + b_i);
+    a.off_i = (const int64_t*)(base + b_d + b_i + b_off);
+    a.count = count;
+    char* p = base + in_bytes;
+    a.red = (double*)p;
+    p += b_red;
+    a.zx = (double*)p;
+    p += b_zx;
+    a.y = (double*)p;
+    p += b_y;
+    a.x = (double*)p;
+    p += b_x;
+    a.obj = (double*)p;
+    p += b_obj;
+    a.status = (int32_t*)p;
+    a.m = (int32_t*)(p + b_int);
+    a.pd = (int32_t*)(p + 2 * b_int);
+    a.iters = (int32_t*)(p + 3 * b_int);
+    a.maxit = 100;
+    a.tol = 1e-9;
+    a.feas_tol = 1e-6;
+    hipStream_t s = nullptr;
+    e = hipMemcpyAsync(base, hb, in_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(count), dim3(64), 0, s, a);
+        e = hipGetLastError();
     }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, DQ_R>), dim3(count), dim3(64), 0, s, a);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(dev::dense_expand_kernel, dim3(count), dim3(64), 0, s, a);
+        e = hipGetLastError();
+    }
+    std::vector<int32_t> st(count);
+    std::vector<double> obj(count), x((size_t)count * DENSE_NMAX);
+    if (e == hipSuccess) e = hipMemcpyAsync(st.data(), a.status, count * sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(obj.data(), a.obj, count * sizeof(double), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(x.data(), a.x, x.size() * sizeof(double), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP solve: ") + hipGetErrorString(e));
+    for (int k = 0; k < count; k++)
+        if (st[k] == RS_CAP_NZ || st[k] == RS_CAP_ROWS)
+            return set_error(MPCCBF_ERR_CAPACITY, "QP " + std::to_string(k) +
+                                                      (st[k] == RS_CAP_NZ ? ": reduced dimension exceeds 8"
+                                                                          : ": reduced rows exceed 256"));
     // outputs: x only for OPTIMAL (Solver.h:33-35)
-    std::vector<double> xtmp;
     for (int k = 0; k < count; k++) {
-        const ReducedQP& r = red[k];
-        status_out[k] = r.status;
-        if (obj_out) obj_out[k] = __builtin_nan("");
-    }
-    const std::vector<double> zero(DENSE_NZ, 0.0);
-    for (int k = 0; k < count; k++) {
-        const ReducedQP& r = red[k];
-        const double* yk = zero.data();
-        if (r.status < 0) {
-            const int j = (int)(std::lower_bound(dev_idx.begin(), dev_idx.end(), k) - dev_idx.begin());
-            status_out[k] = st[j];
-            yk = &y[(size_t)j * DENSE_NZ];
-        }
-        if (status_out[k] == MPCCBF_OPTIMAL) {
-            xtmp.assign(r.n, 0.0);
-            double f = 0.0;
-            expand_solution(r, yk, xtmp.data(), &f);
-            if (obj_out) obj_out[k] = f;
-            if (x_out && x_out[k]) std::memcpy(x_out[k], xtmp.data(), r.n * sizeof(double));
-        }
+        status_out[k] = st[k];
+        if (obj_out) obj_out[k] = st[k] == MPCCBF_OPTIMAL ? obj[k] : __builtin_nan("");
+        if (st[k] == MPCCBF_OPTIMAL && x_out && x_out[k])
+            std::memcpy(x_out[k], &x[(size_t)k * DENSE_NMAX], (size_t)qps[k].n * sizeof(double));
     }
     return MPCCBF_OK;
 }

@@ -52,6 +52,9 @@ struct DevOps {
     // separable layout: the main launch runs the fast start and the dual active set only and
     // defers agents that need the PDIP or phase 1 to the fallback launch (0: one full launch)
     int32_t lean;
+    // dual active set: IMPC iteration 1 starts from iteration 0's final active set when iteration 0
+    // took at least this many steps (0: always cold)
+    int32_t das_warm;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;

@@ -77,6 +77,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
 #pragma unroll
     for (int k = 0; k < 6; k++) s0[k] = args.states[(size_t)self * 6 + k];
     __shared__ double ykeep_s[WNZ], q_s[WNZ];  // wave-uniform vectors kept out of the registers
+    __shared__ double ypd[WNZ];                // slack mode: the slack PDIP's point during its polish
     {
         double q15[NZ], kconst0;
         agent_linear_term<NZ>(op, buf, args, ai, s0, q15, kconst0);
@@ -334,137 +335,178 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             // to phase 1 directly, one it gives up on to the PDIP
             int das = 0, dsteps = 0;
             double drp = 0.0, drd = 0.0, dtlow = 0.0;
+            // slack mode: the dual active set on a hard-row QP per slack pattern. Neighbour i is
+            // either at v_i = 0 (its FoV rows hard: g_a y <= h_a) or, with a leader row l, at
+            // v_i = g_l y - h_l >= 0: w_i g_l joins the linear term, its other rows become
+            // (g_a - g_l) y <= h_a - h_l and row l the bound g_l y >= h_l. A solve is the slack
+            // QP's optimum when every neighbour's multipliers are consistent (stationarity in
+            // v_i: at v_i = 0 the FoV multipliers sum to at most w_i; with a leader, its own
+            // multiplier w_i - sum(others) - mu_i is >= 0). All start at v = 0; a neighbour
+            // over its cost takes its largest-multiplier row as leader, one with a negative
+            // leader multiplier the next-largest. A pattern without a feasible point relaxes a
+            // FoV row of its infeasibility certificate: the unreachable candidate when it is a
+            // slack row (it leads its neighbour), else the certificate's active slack row of
+            // largest weight whose neighbour has no leader. After SLK_PATTERNS patterns, or
+            // when no rule applies, the slack PDIP solves.
+#ifndef MPCCBF_SLK_PATTERNS
+#define MPCCBF_SLK_PATTERNS 8
+#endif
+            constexpr int SLK_PATTERNS = MPCCBF_SLK_PATTERNS;
+            bool lv = false, pattern_ok = false;
+            int ncbf = 0, c_me = 0;
+            if constexpr (SLACK) {
+                lv = slk->live[lane] != 0.0;
+                const unsigned long long lm = __ballot(lv);
+                ncbf = __popcll(lm);
+                c_me = __popcll(lm & ((1ull << lane) - 1ull));
+                if (lane < WSL_NB) slk->lead[lane] = -1;
+                pattern_ok = op.dual_as > 0 && mtot + ncbf <= WROWS;
+            }
+            auto run_patterns = [&](int npat) -> int {
+                if constexpr (!SLACK) {
+                    (void)npat;
+                    return 0;
+                } else {
+                int res = 0, tot_steps = 0;
+                for (int pat = 0; pat < npat; pat++) {
+                    wave_lds_sync();
+                    const int ld = slk->lead[lane >> 3];
+                    if (lv) {
+                        const int r = mtot + c_me;
+                        const double* go = slk->Go + lane * WNZ;
+                        const double* gl_ = slk->Go + (ld < 0 ? lane : ld) * WNZ;
+                        const bool diff = ld >= 0 && ld != lane;
+#pragma unroll
+                        for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = diff ? go[j] - gl_[j] : go[j];
+                        const bool lead_row = ld == lane;
+                        rlo[r] = lead_row ? slk->h[lane] : 0.0;
+                        rml[r] = lead_row ? 1.0 : 0.0;
+                        rhi[r] = lead_row ? 1e300 : (diff ? slk->h[lane] - slk->h[ld] : slk->h[lane]);
+                    }
+                    if (lane < WNZ) {  // q + sum over led neighbours of w_i g_l
+                        double qv = q_s[lane];
+                        for (int g = 0; g < nnb; g++) {
+                            const int l = slk->lead[g];
+                            if (l >= 0) qv = fma(slk->w[g], slk->Go[l * WNZ + lane], qv);
+                        }
+                        sc.q[lane] = qv;
+                    }
+                    wave_lds_sync();
+                    int st_ = 0, cand = -1;
+                    const int d = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
+                                                 opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as,
+                                                 args.dual_res != nullptr, lane, drp, drd, st_, dtlow, &cand);
+                    tot_steps += st_;
+                    if (d < 0) {
+                        // no feasible point with this pattern: a FoV row of the certificate
+                        // takes the slack (wave-uniform choice, every lane scans the same LDS)
+                        int pick = -1;
+                        if (cand >= mtot) {
+                            const int sl = slk->rowl[cand - mtot];
+                            if (slk->lead[sl >> 3] != sl) pick = sl;  // (not the leader's own bound)
+                        } else {
+                            double best = 0.0;
+                            for (int a = 0; a < was.k; a++) {
+                                const int r = was.row[a];
+                                if (r < mtot || was.sg[a] < 0.0) continue;
+                                const int sl = slk->rowl[r - mtot];
+                                if (slk->lead[sl >> 3] < 0 && was.u[a] > best) best = was.u[a], pick = sl;
+                            }
+                        }
+                        if (pick < 0) break;
+                        wave_lds_sync();
+                        if (lane == 0) slk->lead[pick >> 3] = pick;
+                        continue;
+                    }
+                    if (d != 1) break;
+                    wave_lds_sync();
+                    // per neighbour (lane g < nnb): multipliers of its upper sides, of its leader's
+                    // bound, and its largest-multiplier active rows other than the leader
+                    bool bad = false;
+                    int pick = -1;
+                    if (lane < nnb) {
+                        const int l = slk->lead[lane];
+                        double lam = 0.0, mu = 0.0, best = -1.0;
+                        for (int a = 0; a < was.k; a++) {
+                            const int r = was.row[a];
+                            if (r < mtot) continue;
+                            const int sl = slk->rowl[r - mtot];
+                            if ((sl >> 3) != lane) continue;
+                            const double ua = was.u[a];
+                            if (was.sg[a] < 0.0) {
+                                mu += ua;  // the leader's bound v_i >= 0
+                            } else {
+                                lam += ua;
+                                if (sl != l && ua > best) best = ua, pick = sl;
+                            }
+                        }
+                        bad = l < 0 ? !(lam <= slk->w[lane]) : !(slk->w[lane] - lam - mu >= 0.0);
+                    }
+                    const unsigned long long badm = __ballot(bad);
+                    if (badm == 0ull) {
+                        // consistent: v_i = g_l y - h_l for led neighbours, the cost into the objective
+                        double vw = 0.0;
+                        if (lane < nnb) {
+                            const int l = slk->lead[lane];
+                            if (l >= 0) vw = slk->w[lane] * (dotl(slk->Go + l * WNZ, sc.y) - slk->h[l]);
+                        }
+                        vobj = wave_reduce<Op::Sum>(vw);
+                        res = 1;
+                        break;
+                    }
+                    if (__ballot(bad && pick < 0) != 0ull) break;  // no row to lead: the PDIP
+                    wave_lds_sync();
+                    if (bad) slk->lead[lane] = pick;
+                }
+                dsteps += tot_steps;
+                if (res != 1) {
+                    vobj = 0.0;
+                    for (int e = lane; e < ncbf * WNZ; e += 64) Gimg[mtot * WNZ + e] = 0.0;
+                    if (lane < WNZ) sc.q[lane] = q_s[lane];
+                    wave_lds_sync();
+                }
+                return res;
+            }
+            };
+            auto polish = [&]() -> bool {
+                if constexpr (!SLACK) {
+                    return false;
+                } else {
+                // the slack PDIP's solution fixes the pattern — neighbour i with v_i > 0 leads with
+                // its row of largest excess g_r y - h_r — and one active-set solve of that pattern
+                // (plus one exchange) returns its exact optimum, which replaces the interior
+                // point's when consistent (the PDIP's tolerance, priced at slack-cost-sized
+                // multipliers, otherwise shows in the objective)
+                if (!pattern_ok) return false;
+                wave_lds_sync();
+                const double vi = slk->st[lane];  // (WaveSlack::st row 0: this lane's neighbour's v)
+                const double ex = lv ? dotl(slk->Go + lane * WNZ, sc.y) - slk->h[lane] : -1e300;
+                // segment argmax of the excess (8 lanes per neighbour)
+                double m = ex;
+                m = fmax(m, dpp_mov<DPP_XOR1>(m));
+                m = fmax(m, dpp_mov<DPP_XOR2>(m));
+                m = fmax(m, dpp_mov<DPP_HALF_MIRROR>(m));
+                const unsigned long long hit = __ballot(lv && ex == m);
+                const unsigned long long seg = 0xFFull << (lane & ~7);
+                const int lead = __ffsll((long long)(hit & seg)) - 1;
+                if (lane < WNZ) ypd[lane] = sc.y[lane];
+                wave_lds_sync();
+                if ((lane & 7) == 0 && (lane >> 3) < nnb)
+                    slk->lead[lane >> 3] = (vi > 1e-9 && lead >= 0) ? lead : -1;
+                const int r = run_patterns(2);
+                if (r != 1 && lane < WNZ) sc.y[lane] = ypd[lane];  // keep the interior point's
+                wave_lds_sync();
+                return r == 1;
+            }
+            };
             if constexpr (!SLACK) {
                 if (op.dual_as > 0)
                     das = das_solve_wave(image_rows(mtot), Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16),
                                          op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps,
                                          dtlow);
-            } else {
-                // slack mode: the dual active set on a hard-row QP per slack pattern. Neighbour i is
-                // either at v_i = 0 (its FoV rows hard: g_a y <= h_a) or, with a leader row l, at
-                // v_i = g_l y - h_l >= 0: w_i g_l joins the linear term, its other rows become
-                // (g_a - g_l) y <= h_a - h_l and row l the bound g_l y >= h_l. A solve is the slack
-                // QP's optimum when every neighbour's multipliers are consistent (stationarity in
-                // v_i: at v_i = 0 the FoV multipliers sum to at most w_i; with a leader, its own
-                // multiplier w_i - sum(others) - mu_i is >= 0). All start at v = 0; a neighbour
-                // over its cost takes its largest-multiplier row as leader, one with a negative
-                // leader multiplier the next-largest. A pattern without a feasible point relaxes a
-                // FoV row of its infeasibility certificate: the unreachable candidate when it is a
-                // slack row (it leads its neighbour), else the certificate's active slack row of
-                // largest weight whose neighbour has no leader. After SLK_PATTERNS patterns, or
-                // when no rule applies, the slack PDIP solves.
-#ifndef MPCCBF_SLK_PATTERNS
-#define MPCCBF_SLK_PATTERNS 8
-#endif
-                constexpr int SLK_PATTERNS = MPCCBF_SLK_PATTERNS;
-                const bool lv = slk->live[lane] != 0.0;
-                const unsigned long long lm = __ballot(lv);
-                const int ncbf = __popcll(lm);
-                const int c_me = __popcll(lm & ((1ull << lane) - 1ull));
-                if (lane < WSL_NB) slk->lead[lane] = -1;
-                if (op.dual_as > 0 && mtot + ncbf <= WROWS) {
-                    if (lv) slk->rowl[c_me] = lane;
-                    int tot_steps = 0;
-                    for (int pat = 0; pat < SLK_PATTERNS; pat++) {
-                        wave_lds_sync();
-                        const int ld = slk->lead[lane >> 3];
-                        if (lv) {
-                            const int r = mtot + c_me;
-                            const double* go = slk->Go + lane * WNZ;
-                            const double* gl_ = slk->Go + (ld < 0 ? lane : ld) * WNZ;
-                            const bool diff = ld >= 0 && ld != lane;
-#pragma unroll
-                            for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = diff ? go[j] - gl_[j] : go[j];
-                            const bool lead_row = ld == lane;
-                            rlo[r] = lead_row ? slk->h[lane] : 0.0;
-                            rml[r] = lead_row ? 1.0 : 0.0;
-                            rhi[r] = lead_row ? 1e300 : (diff ? slk->h[lane] - slk->h[ld] : slk->h[lane]);
-                        }
-                        if (lane < WNZ) {  // q + sum over led neighbours of w_i g_l
-                            double qv = q_s[lane];
-                            for (int g = 0; g < nnb; g++) {
-                                const int l = slk->lead[g];
-                                if (l >= 0) qv = fma(slk->w[g], slk->Go[l * WNZ + lane], qv);
-                            }
-                            sc.q[lane] = qv;
-                        }
-                        wave_lds_sync();
-                        int st_ = 0, cand = -1;
-                        das = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
-                                             opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as, args.dual_res != nullptr,
-                                             lane, drp, drd, st_, dtlow, &cand);
-                        tot_steps += st_;
-                        if (das < 0) {
-                            // no feasible point with this pattern: a FoV row of the certificate
-                            // takes the slack (wave-uniform choice, every lane scans the same LDS)
-                            int pick = -1;
-                            if (cand >= mtot) {
-                                const int sl = slk->rowl[cand - mtot];
-                                if (slk->lead[sl >> 3] != sl) pick = sl;  // (not the leader's own bound)
-                            } else {
-                                double best = 0.0;
-                                for (int a = 0; a < was.k; a++) {
-                                    const int r = was.row[a];
-                                    if (r < mtot || was.sg[a] < 0.0) continue;
-                                    const int sl = slk->rowl[r - mtot];
-                                    if (slk->lead[sl >> 3] < 0 && was.u[a] > best) best = was.u[a], pick = sl;
-                                }
-                            }
-                            if (pick < 0) break;
-                            wave_lds_sync();
-                            if (lane == 0) slk->lead[pick >> 3] = pick;
-                            das = 0;
-                            continue;
-                        }
-                        if (das != 1) break;
-                        wave_lds_sync();
-                        // per neighbour (lane g < nnb): multipliers of its upper sides, of its leader's
-                        // bound, and its largest-multiplier active rows other than the leader
-                        bool bad = false;
-                        int pick = -1;
-                        if (lane < nnb) {
-                            const int l = slk->lead[lane];
-                            double lam = 0.0, mu = 0.0, best = -1.0;
-                            for (int a = 0; a < was.k; a++) {
-                                const int r = was.row[a];
-                                if (r < mtot) continue;
-                                const int sl = slk->rowl[r - mtot];
-                                if ((sl >> 3) != lane) continue;
-                                const double ua = was.u[a];
-                                if (was.sg[a] < 0.0) {
-                                    mu += ua;  // the leader's bound v_i >= 0
-                                } else {
-                                    lam += ua;
-                                    if (sl != l && ua > best) best = ua, pick = sl;
-                                }
-                            }
-                            bad = l < 0 ? !(lam <= slk->w[lane]) : !(slk->w[lane] - lam - mu >= 0.0);
-                        }
-                        const unsigned long long badm = __ballot(bad);
-                        if (badm == 0ull) {
-                            // consistent: v_i = g_l y - h_l for led neighbours, the cost into the objective
-                            double vw = 0.0;
-                            if (lane < nnb) {
-                                const int l = slk->lead[lane];
-                                if (l >= 0) vw = slk->w[lane] * (dotl(slk->Go + l * WNZ, sc.y) - slk->h[l]);
-                            }
-                            vobj = wave_reduce<Op::Sum>(vw);
-                            break;
-                        }
-                        das = 0;
-                        if (__ballot(bad && pick < 0) != 0ull) break;  // no row to lead: the PDIP
-                        wave_lds_sync();
-                        if (bad) slk->lead[lane] = pick;
-                    }
-                    dsteps = tot_steps;
-                    if (das != 1) {
-                        das = 0;
-                        vobj = 0.0;
-                        for (int e = lane; e < ncbf * WNZ; e += 64) Gimg[mtot * WNZ + e] = 0.0;
-                        if (lane < WNZ) sc.q[lane] = q_s[lane];
-                        wave_lds_sync();
-                    }
-                }
+            } else if (pattern_ok) {
+                if (lv) slk->rowl[c_me] = lane;
+                das = run_patterns(SLK_PATTERNS);
             }
             WaveSlack sk{};
             if constexpr (SLACK) {
@@ -514,6 +556,15 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 nit = dsteps + po.iters;
                 prs = po.rp;
                 drs = po.rd;
+                if (SLACK && st == ST_OPTIMAL) {
+                    double vkeep = vobj;
+                    if (polish()) {  // the pattern's exact optimum (sc.y, drp / drd, vobj)
+                        prs = drp;
+                        drs = drd;
+                    } else {
+                        vobj = vkeep;
+                    }
+                }
                 // slack mode: the slack rows are always satisfiable, phase 1 certifies the box and
                 // Voronoi rows (the ordinary image)
                 if (st != ST_OPTIMAL) {

@@ -416,6 +416,20 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     const PdipCfg cfg{op.maxit, op.tol};
     SepWarm<SB> warm{keep + 16 * NZ};  // box duals of the previous OPTIMAL solve (iteration 1 warm start)
     const double warm_delta = SLACK ? 0.0 : op.warm_delta;
+    // the dual active set's warm start: iteration 0's final active set (side ids, their count at
+    // act[POL_K]) starts iteration 1's solve (same box rows and cost, sample-0 CBF rows) when
+    // iteration 0 took at least op.das_warm steps. Measured on the bench swarm: after a long
+    // iteration-0 solve (a transient: several sides) iteration 1 then takes 0 steps where a cold
+    // start repeats them; after a 1-2 step solve (steady state: one CBF side, which iteration 1's
+    // sample-1 row usually replaces) the warm set costs a step more than the cold start.
+    double* act = s0k + 8;  // (no such area in slack mode: never touched there)
+    if (!SLACK && gl == 0) act[POL_K] = 0.0;
+    int steps0 = 0;  // iteration 0's solver steps
+    auto warm_count = [&](int it) -> int {
+        if (SLACK || it == 0 || op.das_warm <= 0 || steps0 < op.das_warm) return 0;
+        wave_lds_sync();
+        return (int)act[POL_K];
+    };
 
     for (int it = 0; it < op.impc_iter; it++) {
         const size_t oi = (size_t)ai * op.impc_iter + it;
@@ -496,8 +510,10 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 yu[o + 1] = -fma(Pi[3 * d + 1], q[o], Pi[3 * d + 2] * q[o + 1]);
             }
             double tl = 0.0;
+            const int k0 = warm_count(it);
             const int r = sep_dual_as<G, SB, CB>(rw, live, opp(buf, op.o_Pr), Pi, q, yu, op.tol, op.dual_as, stage, y,
-                                                 prs, drs, nit, nullptr, true, tl);
+                                                 prs, drs, nit, nullptr, true, tl, nullptr, k0, act,
+                                                 it == 0 ? act : nullptr);
             if (r > 0) {
                 st = ST_OPTIMAL;
             } else if (r < 0 && tl > 10.0 * op.feas_tol) {
@@ -528,7 +544,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
             // warm start or divergence test.
             // (with the dual active-set solve first, the PDIP runs cold: no warm-start duals kept)
             const bool warm_try = it > 0 && warm_delta > 0.0 && op.dual_as <= 0;
-            int tr_warm = 0, tr_cold = 0, tr_p1 = 0;  // diagnostics (MPCCBF_SOLVE_TRACE)
+            int tr_warm = 0, tr_cold = 0, tr_p1 = 0;  // per kind (MPCCBF_SOLVE_TRACE); phase-1 steps
             int attempt = 0, total = 0;
             bool certified = false, infeas = false;
             double tstar = 0.0;
@@ -540,10 +556,12 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 ca.robust = attempt == 2;
                 ca.dual_as = attempt == 0 ? op.dual_as : 0;
                 ca.want_rd = args.dual_res != nullptr;
+                const int k0 = attempt == 0 ? warm_count(it) : 0;
                 po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_Pinv), q, y,
                                                       ca, dbg, wslack, &vslack, red, &warm,
                                                       (attempt == 0 && warm_try) ? warm_delta : 0.0,
-                                                      SLACK ? nullptr : stage);
+                                                      SLACK ? nullptr : stage, k0, SLACK ? nullptr : act,
+                                                      (!SLACK && attempt == 0 && it == 0) ? act : nullptr);
                 total += po.iters;
                 ((attempt == 0 && warm_try) ? tr_warm : tr_cold) += po.iters;
                 if (po.status == ST_OPTIMAL) break;
@@ -580,13 +598,13 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 else break;
             }
             st = po.status;
-            nit = total;
+            nit = total + tr_p1;  // active-set, PDIP and phase-1 steps
             prs = st == ST_INFEASIBLE ? tstar : po.rp;
             drs = po.rd;
 #ifdef MPCCBF_SOLVE_TRACE  // diagnostics build: warm + 100 cold + 10000 phase-1 iterations
             nit = tr_warm + 100 * tr_cold + 10000 * tr_p1;
 #else
-            (void)tr_warm, (void)tr_cold, (void)tr_p1;
+            (void)tr_warm, (void)tr_cold;
 #endif
         }
         double objv = __builtin_nan("");
@@ -600,6 +618,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
             success = false;
         }
         write_iteration(args, oi, gl, st, objv, nit, prs, drs);
+        if (it == 0) steps0 = nit;
         if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
         wave_lds_sync();
     }
@@ -621,8 +640,9 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     __shared__ double stage_all[GPB][SLACK ? 1 : CB * 16 * (SEP_NZ + 1)];
     __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
-    // kept solution | warm-start duals (not in the lean launch) | the agent's state
-    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8];
+    // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
+    // set's warm-start side ids and their count (not in slack mode)
+    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1)];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     if constexpr (!QUEUE) {

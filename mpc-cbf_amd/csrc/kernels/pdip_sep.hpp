@@ -348,12 +348,22 @@ __device__ __forceinline__ void sep_gram(const double* __restrict__ pol, int k, 
     do {                \
     } while (0)
 #endif
+// Warm start (k0 > 0): warm_ids[0 .. k0-1] name sides (POL_ID values) of an earlier solve with
+// the same box rows and cost — IMPC iteration 0's final active set for iteration 1, whose CBF rows
+// of sample 0 are iteration 0's rows (the curve at h_samples(0) = 0 is the state) in the same
+// slots. Each side is staged from this QP's own rows by the lane that owns it; when the equality QP
+// on them has multipliers of the right signs, that point (dual feasible, the sides exact) is the
+// start instead of the unconstrained minimiser; else the solve starts cold. Any set of this QP's
+// sides is a valid start, so a side whose slot now holds another row only costs steps.
+// save: at convergence the final active set's side ids are written there (lane 0; their count
+// at save[POL_K]).
 template <int G, int SB, int CB>
 __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                            const double* __restrict__ Pinv, const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
                            double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
                            int& steps, SepWarm<SB>* warm, bool want_rd, double& tlow,
-                           long long* dbg = nullptr) {
+                           long long* dbg = nullptr, int k0 = 0, const double* __restrict__ warm_ids = nullptr,
+                           double* __restrict__ save = nullptr) {
     static_assert(G == 16, "rows of pol are copied one column per lane");
     (void)dbg;
     GSTAMP(0, true);
@@ -377,6 +387,19 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #pragma unroll
         for (int c = 0; c < CB; c++) sc[s++] = rcp(1.0 + fabs(rw.chi[c]));
     }
+    // candidate rule: among the sides violated beyond the tolerance (scaled as above), the one
+    // with the largest violation per unit norm in the P^-1 metric, v / sqrt(g P^-1 g) — the side
+    // whose addition alone raises the dual objective most (v^2 / 2 g P^-1 g). The plain scaled
+    // rule picked sides that later left again: on the driver bench's slowest QPs 10-12 steps
+    // where this rule needs 4-8 (tools/das_sim.py, the same QPs in numpy). The weights are
+    // formed in each scan from the uniform P^-1 blocks (scalar registers), not kept live.
+    auto row_wn = [&](double g0, double g1, double g2, double g3, int d0, bool two) -> float {
+        asm volatile("" : "+v"(g0), "+v"(g1));  // per scan: not hoisted out of the step loop
+        const double* a = Pinv + 3 * d0;
+        double n2 = fma(fma(a[0], g0, 2.0 * a[1] * g1), g0, a[2] * g1 * g1);
+        if (two) n2 += fma(fma(Pinv[3], g2, 2.0 * Pinv[4] * g3), g2, Pinv[5] * g3 * g3);
+        return rsqrtf((float)fmax(n2, 1e-30));
+    };
     double y[SEP_NZ], u[POL_K];
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
@@ -413,12 +436,57 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #pragma unroll
         for (int j = i; j < POL_K; j++) L[S6::idx(i, j)] = i == j ? 1.0 : 0.0;
     }
+    if (k0 > 0) {
+        // the EQP on the given sides: lam = K^-1 (G_A yu - b_A), y = yu - P^-1 G_A^T lam; start
+        // there when every multiplier u_i = sign_i lam_i >= 0 (group-uniform: LDS rows)
+        double rhs[POL_K], lam[POL_K];
+        for (int i = 0; i < k0; i++) {
+            const int id = (int)warm_ids[i];
+            if ((id & 15) == gl) sep_stage_side<SB, CB>(rw, pi, id >> 4, gl, pol + i * 16);
+        }
+        wave_lds_sync();
+        sep_gram<POL_K>(pol, k0, L);
+#pragma unroll
+        for (int i = 0; i < POL_K; i++) {
+            const double* ri = pol + (i < k0 ? i : 0) * 16;
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], yu[j], t);
+            rhs[i] = i < k0 ? t - ri[POL_B] : 0.0;
+        }
+        bool ok = chol_packed<POL_K>(L, dl);
+        chol_solve<POL_K>(L, dl, rhs, lam);
+#pragma unroll
+        for (int i = 0; i < POL_K; i++) {
+            const double* ri = pol + (i < k0 ? i : 0) * 16;
+            u[i] = i < k0 ? ri[POL_SGN] * lam[i] : 0.0;
+            ok = ok && (i >= k0 || (u[i] >= 0.0 && isfinite(u[i])));
+        }
+        if (ok) {
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) {
+                const double* wi = pol + (i < k0 ? i : 0) * 16 + POL_W;
+#pragma unroll
+                for (int j = 0; j < SEP_NZ; j++) y[j] = fma(i < k0 ? -lam[i] : 0.0, wi[j], y[j]);
+            }
+            k = k0;
+        } else {  // cold: empty active set, identity factor
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) {
+                u[i] = 0.0;
+                dl[i] = 1.0;
+#pragma unroll
+                for (int j = i; j < POL_K; j++) L[S6::idx(i, j)] = i == j ? 1.0 : 0.0;
+            }
+        }
+    }
     double m = 0.0;
     GSTAMP(1, true);
     for (int outer = 0;; outer++) {
         (void)outer;
-        // the most violated side of the group (lowest lane on ties)
-        double vb = -1.0;
+        // the group's largest scaled violation (convergence) and its candidate (lowest lane on
+        // ties): the eligible side with the largest normalised violation
+        double vb = -1.0, eb = -1.0;
         int sb = 0;
         {
             int s = 0;
@@ -427,11 +495,16 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #pragma unroll
                 for (int kk = 0; kk < SB; kk++) {
                     const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
-                    const double vl = (rw.blo[d][kk] - t) * sc[s];
-                    if (vl > vb) vb = vl, sb = s;
+                    const double al = rw.blo[d][kk] - t, vl = al * sc[s];
+                    const float w = row_wn(rw.bg[d][kk][0], rw.bg[d][kk][1], 0.0, 0.0, d, false);
+                    const double el = vl > add_tol ? al * w : -1.0;
+                    vb = fmax(vb, vl);
+                    if (el > eb) eb = el, sb = s;
                     s++;
-                    const double vu = (t - rw.bhi[d][kk]) * sc[s];
-                    if (vu > vb) vb = vu, sb = s;
+                    const double au = t - rw.bhi[d][kk], vu = au * sc[s];
+                    const double eu = vu > add_tol ? au * w : -1.0;
+                    vb = fmax(vb, vu);
+                    if (eu > eb) eb = eu, sb = s;
                     s++;
                 }
             if (has_cbf) {
@@ -440,16 +513,21 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                     double t = 0.0;
 #pragma unroll
                     for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
-                    const double vc = (t - rw.chi[c]) * sc[s];
-                    if (vc > vb) vb = vc, sb = s;
+                    const double ac = t - rw.chi[c], vc = ac * sc[s];
+                    const float w = row_wn(rw.cg[c][0], rw.cg[c][1], rw.cg[c][2], rw.cg[c][3], 0, true);
+                    const double ec = vc > add_tol ? ac * w : -1.0;
+                    vb = fmax(vb, vc);
+                    if (ec > eb) eb = ec, sb = s;
                 }
             }
         }
-        m = grp_max<G>(vb);
+        m = vb;
+        double em = eb;
+        grp_max2<G>(m, em);
         GSTAMP(2 + 6 * outer, outer < 2);
         if (!(m > add_tol)) break;
         if (steps >= maxstep) return 0;
-        const int owner = __ffsll((long long)grp_ballot<G>(vb == m)) - 1;
+        const int owner = __ffsll((long long)grp_ballot<G>(eb == em)) - 1;
         if (gl == owner) sep_stage_side<SB, CB>(rw, pi, sb, gl, cand);
         wave_lds_sync();
         GSTAMP(3, outer == 0);
@@ -651,8 +729,22 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     }
     rd *= rcp(1.0 + qn);
     GSTAMP(9, true);
-    if (!(rd <= tol))
-        return sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm) ? 1 : 0;
+    auto save_sides = [&]() {  // the final active set's side ids, for a later warm start
+        if (save == nullptr) return;
+        if (gl == 0) {
+#pragma unroll
+            for (int i = 0; i < POL_K; i++)
+                if (i < k) save[i] = pol[i * 16 + POL_ID];
+            save[POL_K] = (double)k;
+        }
+    };
+    if (!(rd <= tol)) {
+        // rounding accumulated over the steps: the active set's equality QP, re-solved exactly
+        const bool ok = sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm);
+        if (ok) save_sides();
+        wave_lds_sync();
+        return ok ? 1 : 0;
+    }
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
     rp_out = fmax(m, 0.0);
@@ -674,6 +766,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 warm->zu(d, kk) = mu;
             }
     }
+    save_sides();
     wave_lds_sync();  // the scratch is reused
     GSTAMP(10, true);
     return 1;
@@ -695,7 +788,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                                   double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg = nullptr,
                                   double wv_cost = 0.0, double* v_out = nullptr, double* red = nullptr,
                                   SepWarm<SB>* warm = nullptr, double warm_delta = 0.0,
-                                  double* pol = nullptr) {
+                                  double* pol = nullptr, int das_k0 = 0, const double* das_ids = nullptr,
+                                  double* das_save = nullptr) {
     (void)dbg;
     const bool slk = SLACK && has_cbf;  // group-uniform
     GSTAMP(12, true);
@@ -770,7 +864,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             if (das) {
                 double yg[SEP_NZ], rpg = 0.0, rdg = 0.0, tlg = 0.0;
                 const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, Pinv, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
-                                                     rdg, as_steps, nullptr, cfg.want_rd, tlg, dbg);
+                                                     rdg, as_steps, nullptr, cfg.want_rd, tlg, dbg, das_k0, das_ids,
+                                                     das_save);
                 if (r != 0) {
                     PdipOut fo{r > 0 ? ST_OPTIMAL : ST_UNKNOWN, as_steps};
 #pragma unroll

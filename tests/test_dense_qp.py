@@ -1,9 +1,11 @@
 """Generic dense-QP boundary (mpccbf_qp_solve_dense*), the path a qpcpp::Solver<double> adapter
 uses in place of CPLEXSolver::solve (qpcpp/src/solvers/CPLEX.cpp:35-177).
 
-CPU tests: argument validation happens before any device work, and a valid QP without a GPU
-fails loudly (no CPU fallback). GPU tests: the CPLEXTest toy (qpcpp/tests/CPLEXTest.cpp:28-56),
-the 42 golden MPC-CBF QPs in their full (un-condensed) CPLEX form, and status cases.
+CPU tests: argument validation happens on the host before any device work, and a valid QP
+without a GPU fails loudly (no CPU fallback). GPU tests (the equality elimination runs on the
+device): the CPLEXTest toy (qpcpp/tests/CPLEXTest.cpp:28-56), the 42 golden MPC-CBF QPs in their
+full (un-condensed) CPLEX form, status cases, rank-deficient and inconsistent equalities, fixed
+variables, and random QPs against the oracle's independent dense solver.
 """
 import os
 
@@ -38,8 +40,9 @@ def test_dense_without_gpu_fails_loudly(mpclib):
         mpclib.dense_qp_solve_batch([toy()])
 
 
+@pytest.mark.gpu
 def test_dense_fully_determined_needs_no_solve(mpclib):
-    # equalities pin x completely: decided during elimination, no device launch
+    # equalities pin x completely: decided by the device elimination, no interior-point solve
     q = dict(H=np.eye(2), c=np.array([1.0, 0.0]), A=np.eye(2), lo=np.array([1.0, 2.0]),
              hi=np.array([1.0, 2.0]))
     st, xs, obj = mpclib.dense_qp_solve_batch([q])
@@ -102,3 +105,63 @@ def test_dense_golden_mpc_qps(mpclib):
         ref = float(g[f"c{i}_obj"])
         assert abs(obj[i] - ref) <= 1e-4 * max(1.0, abs(ref)), (i, obj[i], ref)
         assert np.max(np.abs(xs[i] - g[f"c{i}_x"])) <= 1e-5
+
+
+def _random_qp(rng, n, me, mi, redundant=0, fixed=0):
+    """A strictly convex QP with me equalities (redundant copies appended), mi two-sided rows
+    and `fixed` fixed variables, feasible by construction around x0."""
+    M = rng.standard_normal((n, n))
+    H = M @ M.T / n + 0.1 * np.eye(n)
+    c = rng.standard_normal(n)
+    x0 = rng.standard_normal(n)
+    E = rng.standard_normal((me, n))
+    if redundant:
+        E = np.vstack([E, rng.standard_normal((redundant, me)) @ E])
+    G = rng.standard_normal((mi, n))
+    gx = G @ x0
+    A = np.vstack([E, G])
+    lo = np.concatenate([E @ x0, gx - rng.uniform(0.05, 1.0, mi)])
+    hi = np.concatenate([E @ x0, gx + rng.uniform(0.05, 1.0, mi)])
+    vlo = np.full(n, -INF)
+    vhi = np.full(n, INF)
+    for i in range(fixed):
+        vlo[i] = vhi[i] = x0[i]
+    return dict(H=H, c=c, A=A, lo=lo, hi=hi, vlo=vlo, vhi=vhi, c0=0.25)
+
+
+@pytest.mark.gpu
+def test_dense_random_qps_match_oracle(mpclib, oracle):
+    """Random strictly convex QPs through the device elimination (Householder QR with column
+    pivoting, minimum-norm particular solution, null-space basis) and the interior-point kernel,
+    against the oracle's dense solve of the same full-space QP: statuses equal, objectives within
+    1e-6 relative, solutions within 1e-5. Covers fixed variables (unit equality rows), up to 64
+    variables and 58 equalities, a QP without inequality rows, in one batch (the oracle's KKT solve
+    needs independent equalities: dependent ones are tested against their closed form below)."""
+    rng = np.random.default_rng(11)
+    qps = []
+    for n, me, mi, red, fx in ((6, 2, 5, 0, 0), (12, 5, 20, 0, 1), (36, 30, 60, 0, 0), (40, 33, 40, 0, 2),
+                               (64, 58, 30, 0, 0), (20, 14, 0, 0, 3)):
+        qps.append(_random_qp(rng, n, me, mi, red, fx))
+    st, xs, obj = mpclib.dense_qp_solve_batch(qps)
+    for k, q in enumerate(qps):
+        r = oracle.solve_dense_qp(dict(n=q["c"].shape[0], H=q["H"], c=q["c"], c0=q["c0"], A=q["A"], lo=q["lo"],
+                                       hi=q["hi"], vlo=q["vlo"], vhi=q["vhi"]))
+        assert st[k] == r["status"] == mpclib.OPTIMAL, (k, st[k], r["status"])
+        assert abs(obj[k] - r["obj"]) <= 1e-6 * max(1.0, abs(r["obj"])), (k, obj[k], r["obj"])
+        np.testing.assert_allclose(xs[k], r["x"], atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_dense_inconsistent_and_dependent_equalities(mpclib):
+    """Dependent equalities with consistent right-hand sides are dropped by the pivoted QR's
+    rank test; inconsistent ones make the QP INFEASIBLE; more equalities than variables."""
+    base = dict(H=np.eye(3), c=np.zeros(3))
+    A = np.array([[1.0, 1.0, 0.0], [2.0, 2.0, 0.0], [0.0, 1.0, 1.0], [1.0, 2.0, 1.0]])
+    ok = dict(base, A=A, lo=np.array([1.0, 2.0, 1.0, 2.0]), hi=np.array([1.0, 2.0, 1.0, 2.0]))
+    bad = dict(base, A=A, lo=np.array([1.0, 2.5, 1.0, 2.0]), hi=np.array([1.0, 2.5, 1.0, 2.0]))
+    st, xs, obj = mpclib.dense_qp_solve_batch([ok, bad])
+    assert st[0] == mpclib.OPTIMAL and st[1] == mpclib.INFEASIBLE
+    x = xs[0]
+    np.testing.assert_allclose([x[0] + x[1], x[1] + x[2]], [1.0, 1.0], atol=1e-10)
+    # min |x|^2 on the two planes: x = (1/3, 2/3, 1/3)
+    np.testing.assert_allclose(x, [1 / 3, 2 / 3, 1 / 3], atol=1e-9)

@@ -65,8 +65,9 @@ def _run(mpclib, torch, cfg, states, targets, steps, nranks):
     return results
 
 
-@pytest.mark.parametrize("nranks,n_agents", [(2, 1024), (4, 1024)])
+@pytest.mark.parametrize("nranks,n_agents", [(2, 1024), (4, 1024), (8, 8192)])
 def test_local_group_matches_single_rank(mpclib, nranks, n_agents):
+    """(8, 8192) is BASELINE config 4's shape: 8 ranks x 1024 agents of an 8192-agent table."""
     torch = _torch()
     cfg = swarm.config(15)
     states, targets = swarm.lattice_swarm(n_agents, seed=13)
@@ -82,3 +83,37 @@ def test_local_group_matches_single_rank(mpclib, nranks, n_agents):
         np.testing.assert_array_equal(x, single[2][r * per:(r + 1) * per])
     assert not np.array_equal(single[0], states)
     assert np.any(single[1] == 3), "the crowded swarm should produce INFEASIBLE QPs"
+
+
+def test_local_group_rank_failure_does_not_hang(mpclib):
+    """A rank whose mpccbf_run_steps disagrees (a different num_steps) or fails aborts the
+    in-process group: every rank returns an error instead of waiting at a barrier forever."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(256, seed=3)
+    dev = torch.device("cuda", 0)
+    comms = mpclib.Comm.local_group(2, 0)
+    errors = [None, None]
+
+    def rank_main(r):
+        try:
+            ctx = mpclib.Context(cfg)
+            a = torch.tensor(states, device=dev)
+            b = torch.empty_like(a)
+            tg = torch.tensor(targets[r * 128:(r + 1) * 128], device=dev)
+            ctx.run_steps(a, b, 3 + r, targets=tg, agent_first=r * 128, num_agents=128, knn_k=8,
+                          knn_radius=6.0, comm=comms[r])
+            torch.cuda.synchronize()
+        except mpclib.MpccbfError as e:
+            errors[r] = str(e)
+
+    threads = [threading.Thread(target=rank_main, args=(r,)) for r in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=60)
+    assert not any(th.is_alive() for th in threads), "a rank hung in the group barrier"
+    for c in comms:
+        c.close()
+    assert errors[0] is not None and errors[1] is not None, errors
+    assert any("num_steps" in e for e in errors), errors

@@ -1,0 +1,129 @@
+"""Offline study of the dual active-set (Goldfarb-Idnani) step counts on real QPs: for the agents a
+`bench.py --dump` (with the state trace) records, the oracle assembles IMPC iteration 0's QP, the
+equalities are eliminated (null space), and the range-space dual active-set method of
+pdip_sep.hpp sep_dual_as runs in numpy with different candidate rules:
+  scaled  — the device's rule: the largest violation scaled by 1 / (1 + |bound|)
+  normal  — the violation divided by the side's norm in the P^-1 metric, sqrt(g P^-1 g)
+Prints the step counts per rule (test infrastructure: CPU only).
+
+    python tools/das_sim.py gpurun_out/<tag>/dump.npz [min_steps] [sample]
+"""
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "mpc-cbf_amd"))
+import oracle_lib as O  # noqa: E402
+from mpccbf import swarm  # noqa: E402
+
+
+def reduce_qp(qp):
+    """x = xp + Z y over the equality rows; returns P, q, sides (N y <= b)."""
+    A, lo, hi = qp["A"], qp["lo"], qp["hi"]
+    eq = lo == hi
+    E, e = A[eq], lo[eq]
+    xp = np.linalg.lstsq(E, e, rcond=None)[0]
+    _, s, vt = np.linalg.svd(E)
+    r = int((s > 1e-10 * s[0]).sum())
+    Z = vt[r:].T
+    H2 = qp["H"] + qp["H"].T  # objective x^T H x (H upper): Hessian H + H^T
+    P = Z.T @ H2 @ Z
+    q = Z.T @ (H2 @ xp + qp["c"])
+    Gi, l, h = A[~eq] @ Z, lo[~eq] - A[~eq] @ xp, hi[~eq] - A[~eq] @ xp
+    keep = np.abs(Gi).sum(axis=1) > 1e-12
+    Gi, l, h = Gi[keep], l[keep], h[keep]
+    N = np.vstack([Gi, -Gi])
+    b = np.concatenate([h, -l])
+    fin = np.isfinite(b) & (np.abs(b) < 1e19)
+    return P, q, N[fin], b[fin]
+
+
+def gi(P, q, N, b, rule, tol=1e-6, maxstep=64):
+    Pi = np.linalg.inv(P)
+    y = -Pi @ q
+    sc = 1.0 / (1.0 + np.abs(b))
+    nrm = np.sqrt(np.einsum("ij,jk,ik->i", N, Pi, N))
+    A, u = [], []
+    steps = 0
+    while True:
+        v = (N @ y - b)
+        m = (v * sc).max()
+        if m <= 0.1 * tol:
+            return steps, len(A), y
+        sel = {"scaled": v * sc, "normal": v / nrm, "normal2": v / nrm**2,
+               "normsc": v * sc / (nrm * sc.max() + 0 * nrm)}[rule]
+        p = int(np.argmax(np.where(v * sc > 0.1 * tol, sel, -np.inf)))
+        up = 0.0
+        while True:
+            steps += 1
+            if steps > maxstep:
+                return -1, len(A), y
+            npv = N[p]
+            if A:
+                NA = N[A]
+                K = NA @ Pi @ NA.T
+                rho = np.linalg.solve(K, NA @ Pi @ npv)
+                z = Pi @ (npv - NA.T @ rho)
+            else:
+                rho = np.zeros(0)
+                z = Pi @ npv
+            zn = npv @ z
+            blk = [(u[i] / rho[i], i) for i in range(len(A)) if rho[i] > 0]
+            t1, l = min(blk) if blk else (np.inf, -1)
+            t2 = (npv @ y - b[p]) / zn if zn > 1e-10 * (npv @ Pi @ npv) else np.inf
+            if l < 0 and not np.isfinite(t2):
+                return -2, len(A), y  # infeasible
+            t = min(t1, t2)
+            if np.isfinite(t2):
+                y = y - t * z
+            u = [u[i] - t * rho[i] for i in range(len(A))]
+            up += t
+            if t2 <= t1:
+                A.append(p)
+                u.append(up)
+                break
+            del A[l]
+            del u[l]
+
+
+def main():
+    d = np.load(sys.argv[1])
+    min_steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    sample = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    traj, warm = d["traj"], int(d["warmup"])
+    iters = d["iters"]
+    n = traj.shape[0]
+    cfg = swarm.config(15)
+    p = O.make_params(cfg)
+    _, targets = swarm.lattice_swarm(n)
+    refs = swarm.refs_from_targets(targets, cfg["k_hor"])
+    rng = np.random.default_rng(0)
+    tot = {"scaled": [], "normal": [], "normal2": []}
+    for s in range(iters.shape[0]):
+        ags = list(np.where(iters[s, :, 0] >= min_steps)[0])
+        if sample:
+            more = np.where((iters[s, :, 0] > 0) & (iters[s, :, 0] < min_steps))[0]
+            ags += list(rng.choice(more, min(sample, len(more)), replace=False)) if len(more) else []
+        if not ags:
+            continue
+        states = traj[:, warm + s, :]
+        rp, col = swarm.knn_csr(states, 8, 3.0 * cfg["d_min"])
+        for a in ags:
+            nb = col[rp[a]:rp[a + 1]]
+            qp = O.assemble_qp(p, states[a], refs[a], states[nb], it=0)
+            P, q, N, b = reduce_qp(qp)
+            res = {rule: gi(P, q, N, b, rule) for rule in tot}
+            for rule in tot:
+                tot[rule].append(res[rule][0])
+            print(f"step {s} agent {a}: gpu {iters[s, a, 0]}  " +
+                  "  ".join(f"{k} {v[0]} (k={v[1]})" for k, v in res.items()))
+    for rule, v in tot.items():
+        v = np.array(v)
+        print(rule, "mean", v[v >= 0].mean(), "max", v.max(), "gave up", int((v == -1).sum()))
+
+
+if __name__ == "__main__":
+    main()

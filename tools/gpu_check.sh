@@ -24,7 +24,7 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
   step driver; timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 > $O/driver.json 2> $O/driver.err
   step 1000; timeout -k 10 200 $B > $O/coll.json 2> $O/coll.err
   step 8192; timeout -k 10 200 $B --agents-per-gpu 8192 > $O/8192.json 2> $O/8192.err
-  step rank-share; timeout -k 10 200 $B --agents-per-gpu 1024 > $O/share.json 2> $O/share.err
+  step rank-share; timeout -k 10 200 $B --rank-share 8 --agents-total 8192 > $O/share.json 2> $O/share.err
   step fov; timeout -k 10 200 $B --workload fov > $O/fov.json 2> $O/fov.err
   step fovs; timeout -k 10 200 $B --workload fov --slack > $O/fovs.json 2> $O/fovs.err
 fi
