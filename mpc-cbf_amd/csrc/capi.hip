@@ -391,6 +391,31 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
             for (int a = 0; a < o.nz; a++) Pi16[a * 16 + b] = x[a];
         }
         pack(v, d.o_Pinv16, Pi16);
+        std::vector<double> wb(o.G.r, 0.0);  // the box rows' weights in the active-set candidate rule
+        for (int i = 0; i < o.G.r; i++) {
+            double n2 = 0.0;
+            for (int a = 0; a < o.nz; a++)
+                for (int b = 0; b < o.nz; b++) n2 += o.G(i, a) * Pi16[a * 16 + b] * o.G(i, b);
+            wb[i] = 1.0 / std::sqrt(std::max(n2, 1e-30));
+        }
+        pack(v, d.o_wbox, wb);
+        auto pgram = [&](const Mat& A, int i, int j) {  // A_i P^-1 A_j^T
+            double g = 0.0;
+            for (int a = 0; a < o.nz; a++)
+                for (int b = 0; b < o.nz; b++) g += A(i, a) * Pi16[a * 16 + b] * A(j, b);
+            return g;
+        };
+        std::vector<double> wv, wf;
+        for (const Mat& V : o.VZ) {
+            wv.push_back(pgram(V, 0, 0));
+            wv.push_back(pgram(V, 0, 1));
+            wv.push_back(pgram(V, 1, 1));
+        }
+        for (const Mat& U : o.UZ)
+            for (int i = 0; i < 3; i++)
+                for (int j = i; j < 3; j++) wf.push_back(pgram(U, i, j));
+        pack(v, d.o_wvor, wv);
+        pack(v, d.o_wfov, wf);
     }
     v.push_back(0.0);  // keep every offset addressable even for empty operators
     for (int i = 0; i < 3; i++) {

@@ -2,8 +2,8 @@
 // per wavefront on the layouts of pdip_wave.hpp: the FoV controller's first attempt, the PDIP
 // solving only the QPs it hands on.
 //
-// From the unconstrained minimiser y = -P^-1 q, the most violated side (scaled as the primal
-// residual) is the candidate; the direction z = P^-1 (n_p - N_A r) keeps the active sides exact
+// From the unconstrained minimiser y = -P^-1 q, the violated side with the largest violation per
+// unit P^-1 norm is the candidate; the direction z = P^-1 (n_p - N_A r) keeps the active sides exact
 // and moves y onto the candidate unless an active multiplier reaches zero first, in which case
 // that side leaves and the step is retried. Every step keeps the iterate dual feasible and raises
 // the objective. With K = G_A P^-1 G_A^T = L L^T (k <= 15 active rows):
@@ -30,6 +30,7 @@ struct WaveAS {
     double u[WNZ];           // multipliers (shift scratch; at the optimum: the active rows')
     int32_t row[WNZ];        // active rows' image row
     int32_t k;               // at the optimum: the number of active rows
+    float wn[WROWS];         // candidate weights 1 / sqrt(g P^-1 g) per image row
 };
 
 // first half of solve_rows: v = L^-1 b on the row layout
@@ -65,7 +66,8 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
 __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, WaveScratch& sc,
                               WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
                               double tol, int maxstep, bool want_rd, int lane, double& rp_out,
-                              double& rd_out, int& steps, double& tlow, int* cand = nullptr) {
+                              double& rd_out, int& steps, double& tlow, int* cand = nullptr,
+                              int nfirst = 0, int nrows = WROWS) {
     const int i = lane16_opaque(lane);
     steps = 0;
     for (int e = lane; e < WNZ * WNZ; e += 64) ws.Pi[(e >> 4) * 17 + (e & 15)] = ldg_nohoist(Pinv + e);
@@ -96,27 +98,63 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
     int k = 0;
     double m = 0.0;
     const double add_tol = 0.1 * tol;
+    // candidate rule (as pdip_sep.hpp sep_dual_as): among the sides violated beyond the tolerance
+    // (scaled as the primal residual), the largest violation per unit P^-1 norm, v / sqrt(g P^-1 g).
+    // On the FoV bench's infeasible iteration-1 QPs the scaled rule cycled 24 steps on average (47
+    // at most) before the certificate, this rule 7 (12) (tools/das_sim.py --fov --it1). The
+    // weights are formed once, at the first scan that finds a violation (most QPs never get
+    // there), for the image rows nfirst .. nrows-1 (rows below nfirst are constant, their weights
+    // the caller's): four rows per pass (one per 16-lane row of the wave; lane i forms
+    // (P^-1 g)_i from P^-1's row i in LDS), kept in LDS.
+    bool have_wn = nfirst >= nrows;  // (every weight given: no lazy pass)
+    auto row_weights = [&]() {
+        const int grp = lane >> 4;
+        for (int r0 = nfirst; r0 < nrows; r0 += 4) {
+            const int r = r0 + grp;
+            const double* g = Gs + (r < nrows ? r : 0) * WNZ;
+            double w = 0.0;
+#pragma unroll
+            for (int j = 0; j < WNZ; j++) w = fma(ws.Pi[i * 17 + j], g[j], w);
+            const double n2 = grp_sum<16>(g[i] * w);
+            if (i == 0 && r < nrows) ws.wn[r] = rsqrtf((float)fmax(n2, 1e-30));
+        }
+        wave_lds_sync();
+    };
     for (;;) {
-        // the most violated side of the wave (lowest lane on ties)
-        double vb = -1.0;
+        // the largest scaled violation of the wave (convergence) and the candidate (lowest lane
+        // on ties): the eligible side with the largest normalised violation (before the weights
+        // exist: the largest scaled one)
+        double vb = -1.0, eb = -1.0;
         int rb = 0, sdb = 1;
         double bb = 0.0;
         bool nf = false;  // a NaN row or iterate fails every comparison: give up instead
 #pragma unroll
         for (int s = 0; s < WR; s++) {
             const double t = dotl(rw.g[s], sc.y);
-            const double vl = rw.ml[s] > 0.0 ? (rw.lo[s] - t) * pl[s] : -1.0;
-            const double vu = (t - rw.hi[s]) * pu[s];
+            const double al = rw.lo[s] - t, au = t - rw.hi[s];
+            const double vl = rw.ml[s] > 0.0 ? al * pl[s] : -1.0;
+            const double vu = au * pu[s];
             const int r = wave_owner_row(lane, s);
             nf = nf || vl != vl || vu != vu;
-            if (vl > vb) vb = vl, rb = r, sdb = 0, bb = rw.lo[s];
-            if (vu > vb) vb = vu, rb = r, sdb = 1, bb = rw.hi[s];
+            vb = fmax(vb, fmax(vl, vu));
+            const double w = have_wn ? (double)ws.wn[r < nrows ? r : 0] : 0.0;
+            const double el = have_wn ? (vl > add_tol ? al * w : -1.0) : vl;
+            const double eu = have_wn ? (vu > add_tol ? au * w : -1.0) : vu;
+            if (el > eb) eb = el, rb = r, sdb = 0, bb = rw.lo[s];
+            if (eu > eb) eb = eu, rb = r, sdb = 1, bb = rw.hi[s];
         }
         if (__ballot(nf) != 0ull) return 0;
-        m = wave_reduce<Op::Max>(vb);
+        m = vb;
+        double em = eb;
+        wave_reduce2<Op::Max, Op::Max>(m, em);
         if (!(m > add_tol)) break;
+        if (!have_wn) {  // first violation: form the weights and scan again
+            row_weights();
+            have_wn = true;
+            continue;
+        }
         if (steps >= maxstep) return 0;
-        const int owner = __ffsll((long long)__ballot(vb == m)) - 1;
+        const int owner = __ffsll((long long)__ballot(eb == em)) - 1;
         const int rp = __shfl(rb, owner, 64);
         const double sp = __shfl(sdb, owner, 64) ? 1.0 : -1.0;
         const double bp = __shfl(bb, owner, 64);

@@ -31,6 +31,11 @@ struct DevOps {
     double fov_beta, fov_Ds, fov_Rs, bbox[3];
     int32_t o_VZ, o_VS, o_Wbox, o_P16, o_LP16;
     int32_t o_Pinv16;  // FoV: P^-1 padded to 16 x 16 (dual active-set solve)
+    int32_t o_wbox;    // FoV: box rows' candidate weights 1 / sqrt(g P^-1 g) (dual active-set solve)
+    // FoV: the P^-1 Grams of the Voronoi rows' two parts per control point (C x [xx xy yy]) and
+    // of the FoV rows' three acceleration rows per CBF sample (cbf_h x [00 01 02 11 12 22]): a
+    // row's weight from its few coefficients
+    int32_t o_wvor, o_wfov;
     // closed-loop simulator: stored-curve evaluation (EB0 / EB1: C x C Bernstein monomials of
     // value / first derivative, cum: P cumulative piece parameters)
     int32_t P, o_EB0, o_EB1, o_cum;

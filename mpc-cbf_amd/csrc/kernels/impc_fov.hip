@@ -107,6 +107,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             rlo[r] = src[WNZ + 6] - sh;
             rhi[r] = src[WNZ + 7] - sh;
             rml[r] = 1.0;
+            was.wn[r] = (float)opp(buf, op.o_wbox)[r];  // (constant rows: the host's weights)
         }
     }
     if (lane < WNZ) Gimg[WROWS * WNZ + lane] = 0.0;
@@ -184,6 +185,8 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             rlo[r] = 0.0;
             rml[r] = 0.0;
             rhi[r] = -off - 1e-8 - sh;
+            const double* M = opp(buf, op.o_wvor) + 3 * j;  // g P^-1 g = (nx, ny) M (nx, ny)^T
+            was.wn[r] = rsqrtf((float)fmax(fma(nx, fma(M[0], nx, 2.0 * M[1] * ny), M[2] * ny * ny), 1e-30));
         }
         // ---- FoV CBF rows, compacted after the Voronoi rows
         const int nk = (it == 0) ? 1 : op.cbf_h;
@@ -261,6 +264,10 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 rlo[r] = 0.0;
                 rml[r] = 0.0;
                 rhi[r] = bb + a[0] * us[0] + a[1] * us[1] + a[2] * us[2];
+                const double* M = opp(buf, op.o_wfov) + 6 * k;  // g P^-1 g = a^T M_k a
+                const double n2 = a[0] * (M[0] * a[0] + 2.0 * (M[1] * a[1] + M[2] * a[2])) +
+                                  a[1] * (M[3] * a[1] + 2.0 * M[4] * a[2]) + a[2] * M[5] * a[2];
+                was.wn[r] = rsqrtf((float)fmax(n2, 1e-30));
             }
             count += __popcll(msk);
         }
@@ -395,7 +402,8 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                     int st_ = 0, cand = -1;
                     const int d = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
                                                  opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as,
-                                                 args.dual_res != nullptr, lane, drp, drd, st_, dtlow, &cand);
+                                                 args.dual_res != nullptr, lane, drp, drd, st_, dtlow, &cand,
+                                                 mtot, mtot + ncbf);
                     tot_steps += st_;
                     if (d < 0) {
                         // no feasible point with this pattern: a FoV row of the certificate
@@ -503,7 +511,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 if (op.dual_as > 0)
                     das = das_solve_wave(image_rows(mtot), Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16),
                                          op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps,
-                                         dtlow);
+                                         dtlow, nullptr, mtot, mtot);
             } else if (pattern_ok) {
                 if (lv) slk->rowl[c_me] = lane;
                 das = run_patterns(SLK_PATTERNS);

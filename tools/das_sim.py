@@ -6,7 +6,8 @@ pdip_sep.hpp sep_dual_as runs in numpy with different candidate rules:
   normal  — the violation divided by the side's norm in the P^-1 metric, sqrt(g P^-1 g)
 Prints the step counts per rule (test infrastructure: CPU only).
 
-    python tools/das_sim.py gpurun_out/<tag>/dump.npz [min_steps] [sample]
+    python tools/das_sim.py gpurun_out/<tag>/dump.npz [min_steps] [sample] [--fov [--slack]] [--it1]
+(--fov: a `bench.py --workload fov` dump, config 5 with the FoV-filtered neighbours.)
 """
 import os
 import sys
@@ -45,7 +46,12 @@ def gi(P, q, N, b, rule, tol=1e-6, maxstep=64):
     Pi = np.linalg.inv(P)
     y = -Pi @ q
     sc = 1.0 / (1.0 + np.abs(b))
-    nrm = np.sqrt(np.einsum("ij,jk,ik->i", N, Pi, N))
+    if rule == "diag":
+        nrm = np.sqrt((N * N) @ np.diag(Pi))
+    elif rule == "euclid":
+        nrm = np.linalg.norm(N, axis=1)
+    else:
+        nrm = np.sqrt(np.einsum("ij,jk,ik->i", N, Pi, N))
     A, u = [], []
     steps = 0
     while True:
@@ -53,8 +59,7 @@ def gi(P, q, N, b, rule, tol=1e-6, maxstep=64):
         m = (v * sc).max()
         if m <= 0.1 * tol:
             return steps, len(A), y
-        sel = {"scaled": v * sc, "normal": v / nrm, "normal2": v / nrm**2,
-               "normsc": v * sc / (nrm * sc.max() + 0 * nrm)}[rule]
+        sel = v * sc if rule == "scaled" else (v / nrm**2 if rule == "normal2" else v / nrm)
         p = int(np.argmax(np.where(v * sc > 0.1 * tol, sel, -np.inf)))
         up = 0.0
         while True:
@@ -75,7 +80,7 @@ def gi(P, q, N, b, rule, tol=1e-6, maxstep=64):
             t1, l = min(blk) if blk else (np.inf, -1)
             t2 = (npv @ y - b[p]) / zn if zn > 1e-10 * (npv @ Pi @ npv) else np.inf
             if l < 0 and not np.isfinite(t2):
-                return -2, len(A), y  # infeasible
+                return 1000 + steps, len(A), y  # infeasible (1000 + steps)
             t = min(t1, t2)
             if np.isfinite(t2):
                 y = y - t * z
@@ -90,39 +95,63 @@ def gi(P, q, N, b, rule, tol=1e-6, maxstep=64):
 
 
 def main():
-    d = np.load(sys.argv[1])
-    min_steps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-    sample = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    fov = "--fov" in sys.argv
+    it1 = "--it1" in sys.argv
+    slack = "--slack" in sys.argv
+    av = [a for a in sys.argv[1:] if not a.startswith("--")]
+    d = np.load(av[0])
+    min_steps = int(av[1]) if len(av) > 1 else 4
+    sample = int(av[2]) if len(av) > 2 else 0
     traj, warm = d["traj"], int(d["warmup"])
     iters = d["iters"]
     n = traj.shape[0]
-    cfg = swarm.config(15)
+    if fov:
+        over = dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.9) if slack else {}
+        cfg = swarm.fov_config(20, **over)
+        _, targets = swarm.heading_swarm(n)
+    else:
+        cfg = swarm.config(15)
+        _, targets = swarm.lattice_swarm(n)
     p = O.make_params(cfg)
-    _, targets = swarm.lattice_swarm(n)
     refs = swarm.refs_from_targets(targets, cfg["k_hor"])
     rng = np.random.default_rng(0)
-    tot = {"scaled": [], "normal": [], "normal2": []}
+    tot = {"scaled": [], "normal": [], "diag": [], "euclid": []}
     for s in range(iters.shape[0]):
-        ags = list(np.where(iters[s, :, 0] >= min_steps)[0])
+        ags = list(np.where(iters[s, :, 1 if it1 else 0] >= min_steps)[0])
         if sample:
             more = np.where((iters[s, :, 0] > 0) & (iters[s, :, 0] < min_steps))[0]
             ags += list(rng.choice(more, min(sample, len(more)), replace=False)) if len(more) else []
         if not ags:
             continue
         states = traj[:, warm + s, :]
-        rp, col = swarm.knn_csr(states, 8, 3.0 * cfg["d_min"])
+        if fov:
+            rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+        else:
+            rp, col = swarm.knn_csr(states, 8, 3.0 * cfg["d_min"])
         for a in ags:
             nb = col[rp[a]:rp[a + 1]]
             qp = O.assemble_qp(p, states[a], refs[a], states[nb], it=0)
+            if it1:  # IMPC iteration 1: CBF rows at the iteration-0 curve's h_samples(k)
+                r0 = O.impc_optimize(p, states, a, nb, refs[a])
+                if r0["status"][0] != O.OPTIMAL:
+                    continue
+                x0 = r0["x"][0][:qp["n"]]
+                pred = np.array([np.concatenate([O.eval_curve(p, x0, k * cfg["h"], 0),
+                                                 O.eval_curve(p, x0, k * cfg["h"], 1)])
+                                 for k in range(cfg["cbf_horizon"])])
+                qp = O.assemble_qp(p, states[a], refs[a], states[nb], it=1, pred=pred)
             P, q, N, b = reduce_qp(qp)
             res = {rule: gi(P, q, N, b, rule) for rule in tot}
             for rule in tot:
                 tot[rule].append(res[rule][0])
-            print(f"step {s} agent {a}: gpu {iters[s, a, 0]}  " +
+            print(f"step {s} agent {a}: gpu {iters[s, a, 1 if it1 else 0]}  " +
                   "  ".join(f"{k} {v[0]} (k={v[1]})" for k, v in res.items()))
     for rule, v in tot.items():
         v = np.array(v)
-        print(rule, "mean", v[v >= 0].mean(), "max", v.max(), "gave up", int((v == -1).sum()))
+        f, inf = v[(v >= 0) & (v < 1000)], v[v >= 1000] - 1000
+        print(rule, "feasible: n", len(f), "mean", f.mean() if len(f) else 0, "max", f.max() if len(f) else 0,
+              "| infeasible: n", len(inf), "mean", inf.mean() if len(inf) else 0, "max", inf.max() if len(inf) else 0,
+              "| gave up", int((v == -1).sum()))
 
 
 if __name__ == "__main__":
