@@ -344,39 +344,61 @@ def dense_qp_solve(H, c, A, lo, hi, vlo=None, vhi=None, c0=0.0):
     return int(st[0]), x, float(obj[0])
 
 
+class DenseBatchCall:
+    """A batch of generic dense QPs marshalled once into the C ABI's mpccbf_dense_qp array (what a
+    C++ caller holds anyway: pointers to its own arrays); run() is one
+    mpccbf_qp_solve_dense_batch call on them. qps: list of dicts with H, c, A, lo, hi and
+    optional vlo, vhi, c0."""
+
+    def __init__(self, qps):
+        self.L = load()
+        self.keep = []  # hold the arrays alive for the calls
+        self.count = len(qps)
+        self.arr = (DenseQP * max(self.count, 1))()
+        self.xs = []
+        for k, q in enumerate(qps):
+            c = np.ascontiguousarray(q["c"], dtype=np.float64)
+            n = c.shape[0]
+            H = np.ascontiguousarray(q["H"], dtype=np.float64).reshape(n, n)
+            A = np.ascontiguousarray(q.get("A", np.zeros((0, n))), dtype=np.float64).reshape(-1, n)
+            lo = np.ascontiguousarray(q.get("lo", np.zeros(0)), dtype=np.float64)
+            hi = np.ascontiguousarray(q.get("hi", np.zeros(0)), dtype=np.float64)
+            vlo = q.get("vlo")
+            vhi = q.get("vhi")
+            vlo = None if vlo is None else np.ascontiguousarray(vlo, dtype=np.float64)
+            vhi = None if vhi is None else np.ascontiguousarray(vhi, dtype=np.float64)
+            self.keep += [c, H, A, lo, hi, vlo, vhi]
+            self.arr[k] = DenseQP(n=n, m=A.shape[0], H=H.ctypes.data, c=c.ctypes.data, c0=q.get("c0", 0.0),
+                                  A=A.ctypes.data if A.size else None, lo=lo.ctypes.data if lo.size else None,
+                                  hi=hi.ctypes.data if hi.size else None,
+                                  vlo=None if vlo is None else vlo.ctypes.data,
+                                  vhi=None if vhi is None else vhi.ctypes.data)
+            self.xs.append(np.full(n, np.nan))
+        self.xptr = (C.c_void_p * max(self.count, 1))(*[x.ctypes.data for x in self.xs])
+        self.obj = np.zeros(max(self.count, 1))
+        self.st = np.zeros(max(self.count, 1), dtype=np.int32)
+
+    def run(self):
+        """Returns (status[count], list of x (None unless OPTIMAL), obj[count])."""
+        for x in self.xs:
+            x.fill(np.nan)
+        _check(self.L.mpccbf_qp_solve_dense_batch(self.count, self.arr, C.cast(self.xptr, C.c_void_p),
+                                                  self.obj.ctypes.data, self.st.ctypes.data))
+        n = self.count
+        return (self.st[:n].copy(), [self.xs[k].copy() if self.st[k] == 0 else None for k in range(n)],
+                self.obj[:n].copy())
+
+    def run_raw(self):
+        """The C call alone (outputs stay in self.st / self.obj / self.xs)."""
+        _check(self.L.mpccbf_qp_solve_dense_batch(self.count, self.arr, C.cast(self.xptr, C.c_void_p),
+                                                  self.obj.ctypes.data, self.st.ctypes.data))
+
+
 def dense_qp_solve_batch(qps):
     """Batched generic dense QPs (mpccbf_qp_solve_dense_batch): one launch for all of them.
     qps: list of dicts with H, c, A, lo, hi and optional vlo, vhi, c0. Returns
     (status[count], list of x (None unless OPTIMAL), obj[count])."""
-    L = load()
-    keep = []  # hold the arrays alive for the call
-    arr = (DenseQP * max(len(qps), 1))()
-    xs = []
-    for k, q in enumerate(qps):
-        c = np.ascontiguousarray(q["c"], dtype=np.float64)
-        n = c.shape[0]
-        H = np.ascontiguousarray(q["H"], dtype=np.float64).reshape(n, n)
-        A = np.ascontiguousarray(q.get("A", np.zeros((0, n))), dtype=np.float64).reshape(-1, n)
-        lo = np.ascontiguousarray(q.get("lo", np.zeros(0)), dtype=np.float64)
-        hi = np.ascontiguousarray(q.get("hi", np.zeros(0)), dtype=np.float64)
-        vlo = q.get("vlo")
-        vhi = q.get("vhi")
-        vlo = None if vlo is None else np.ascontiguousarray(vlo, dtype=np.float64)
-        vhi = None if vhi is None else np.ascontiguousarray(vhi, dtype=np.float64)
-        keep += [c, H, A, lo, hi, vlo, vhi]
-        arr[k] = DenseQP(n=n, m=A.shape[0], H=H.ctypes.data, c=c.ctypes.data, c0=q.get("c0", 0.0),
-                         A=A.ctypes.data if A.size else None, lo=lo.ctypes.data if lo.size else None,
-                         hi=hi.ctypes.data if hi.size else None,
-                         vlo=None if vlo is None else vlo.ctypes.data,
-                         vhi=None if vhi is None else vhi.ctypes.data)
-        xs.append(np.full(n, np.nan))
-    xptr = (C.c_void_p * max(len(qps), 1))(*[x.ctypes.data for x in xs])
-    obj = np.zeros(max(len(qps), 1))
-    st = np.zeros(max(len(qps), 1), dtype=np.int32)
-    _check(L.mpccbf_qp_solve_dense_batch(len(qps), arr, C.cast(xptr, C.c_void_p), obj.ctypes.data,
-                                         st.ctypes.data))
-    n = len(qps)
-    return st[:n], [xs[k] if st[k] == 0 else None for k in range(n)], obj[:n]
+    return DenseBatchCall(qps).run()
 
 
 COMM_ID_BYTES = 128
