@@ -65,8 +65,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--loop", choices=["native", "python"], default="native",
                     help="native: mpccbf_run_steps (C++ loop, RCCL); python: one call per step")
-    ap.add_argument("--neighbours", choices=["grid", "csr"], default="grid",
-                    help="grid: fused in-kernel spatial-hash query; csr: separate KNN kernels")
+    ap.add_argument("--neighbours", choices=["grid", "csr", "all"], default="grid",
+                    help="grid: fused in-kernel spatial-hash query; csr: separate KNN kernels; all: "
+                         "every other robot as a neighbour (the reference's own lists, "
+                         "ConnectivityIMPCCBF.cpp:59-67), fixed CSR lists in the native loop")
     ap.add_argument("--crowded", action="store_true",
                     help="collision workload on a crowded lattice (0.6 x the spacing: 3 m, jitter +-0.3 m), "
                          "where the dual active set and the interior-point fallback do the work")
@@ -263,7 +265,12 @@ def main():
 
     replay_same = None
     trace_res = None
-    if args.loop == "native" and args.neighbours == "grid":
+    nb_lists = {}
+    if args.neighbours == "all":  # every other robot, as the reference hands them to optimize()
+        rp_all = np.arange(per + 1, dtype=np.int32) * (total - 1)
+        col_all = np.array([j for a in range(first, first + per) for j in range(total) if j != a], dtype=np.int32)
+        nb_lists = dict(nb_row_ptr=torch.tensor(rp_all, device=dev), nb_col=torch.tensor(col_all, device=dev))
+    if args.loop == "native" and args.neighbours in ("grid", "all"):
         # the whole closed loop in libmpccbf (mpccbf_run_steps): per step the fused IMPC kernel
         # (neighbour query, both IMPC QPs, next-step neighbour table) and, across ranks, one
         # in-place RCCL all-gather of agent states
@@ -284,9 +291,10 @@ def main():
             # pos_std / vel_std of base_config.json physical_limits (example :150-221)
             traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
             out["x"].fill_(float("nan"))
-            common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn,
-                          knn_radius=radius, x=out["x"], obj=out["obj"], comm=comm, traj_t=traj_t,
-                          pos_std=0.001, vel_std=0.01, noise_seed=20251015, cov=cov)
+            nbsel = nb_lists or dict(knn_k=args.knn, knn_radius=radius)
+            common = dict(targets=targets, agent_first=first, num_agents=per, x=out["x"], obj=out["obj"],
+                          comm=comm, traj_t=traj_t, pos_std=0.001, vel_std=0.01, noise_seed=20251015,
+                          cov=cov, **nbsel)
             r = ctx.run_steps(tables[0], tables[1], args.warmup, status=out["status"],
                               iters=out["iters"], reserve_steps=nsteps, **common)
             if r["final"] is not tables[0]:
@@ -319,9 +327,10 @@ def main():
             nt = args.warmup + nsteps
             trace_dev = torch.empty((nt + 1, total, 6), dtype=torch.float64, device=dev)
             trace_dev[0].copy_(tables[0])
-            common = dict(targets=targets, agent_first=first, num_agents=per, knn_k=args.knn, knn_radius=radius,
-                          x=out["x"], obj=out["obj"], traj_t=traj_t, pos_std=0.001, vel_std=0.01,
-                          noise_seed=20251015, cov=cov, status=out["status"], iters=out["iters"])
+            nbsel = nb_lists or dict(knn_k=args.knn, knn_radius=radius)
+            common = dict(targets=targets, agent_first=first, num_agents=per, x=out["x"], obj=out["obj"],
+                          traj_t=traj_t, pos_std=0.001, vel_std=0.01, noise_seed=20251015, cov=cov,
+                          status=out["status"], iters=out["iters"], **nbsel)
             last_status = None
             for s in range(nt):
                 r = ctx.run_steps(tables[0], tables[1], 1, step_index=s, **common)
@@ -423,7 +432,8 @@ def main():
     # one rank, the native loop: a step is the IMPC launch alone (plus the capacity fallback's
     # launch when its slots can be exceeded), so the timed region's events divided by the steps
     # are the kernel's average duration without the dispatch gap that per-launch events add
-    fallback = kname.startswith("impc_sep_kernel") and not args.slack and args.knn * cfg["cbf_horizon"] > 16
+    nbk = total - 1 if args.neighbours == "all" else args.knn  # neighbours per agent (at most)
+    fallback = kname.startswith("impc_sep_kernel") and nbk * cfg["cbf_horizon"] > 16
     kernel_only = world == 1 and region_ms is not None and not fallback and args.rank_share <= 0
     if kernel_only:
         kern_avg = region_ms / nsteps
@@ -442,7 +452,7 @@ def main():
         # wave-level VALU instructions per launch (PMC SQ_INSTS_VALU) / launch time against the
         # issue peak (every SIMD one wave64 VALU op per 4 cycles: 1024 SIMDs x 2.4 GHz / 4)
         valu_insts, valu_src = pmc_lookup(kname, wl, "SQ_INSTS_VALU")
-        abytes = algorithmic_bytes_per_agent(ctx.n, args.knn, cfg["impc_iter"], cov is not None) * per
+        abytes = algorithmic_bytes_per_agent(ctx.n, nbk, cfg["impc_iter"], cov is not None) * per
         bound = "mfma" if kname.startswith("impc_fov") else "valu"
         res = {
             "metric": "QP solves/sec (whole node) + p99 step latency, N-agent horizon-15 MPC-CBF",
@@ -459,7 +469,7 @@ def main():
             "dtype": "f64",
             "data": ("synthetic (jittered-lattice swarm, seed 20251015); closed loop with the "
                      "example's trajectory fallback and state noise (pos 1e-3, vel 1e-2)"
-                     if args.loop == "native" and args.neighbours == "grid" else
+                     if args.loop == "native" and args.neighbours in ("grid", "all") else
                      "synthetic (jittered-lattice swarm, seed 20251015); closed loop"),
             "config": {
                 "workload": (
@@ -468,7 +478,8 @@ def main():
                      if fov else
                      f"config3{' crowded (0.6 x spacing)' if args.crowded else ''}: {total} agents, horizon "
                      f"{cfg['k_hor']}, pairwise collision CBF, "
-                     f"knn{args.knn} r={radius:g}m ({args.neighbours})")
+                     + (f"every other robot as a neighbour ({total - 1}, fixed CSR lists)" if args.neighbours == "all"
+                        else f"knn{args.knn} r={radius:g}m ({args.neighbours})"))
                     + (f", slack_mode (cost 1000, decay {args.slack_decay:g})" if args.slack else "")
                     + ", base_config.json; 2 IMPC QPs/agent/step"
                     + ("" if world == 1 else f"; {per}/GPU, RCCL all-gather of states")
@@ -640,6 +651,10 @@ def cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h=None):
     refs = swarm.refs_from_targets(targets_h, cfg["k_hor"])
     if cfg.get("cbf_mode", 0) == 1:
         rp, col = swarm.fov_csr(states_h, args.knn, radius, cfg["fov_beta"])
+    elif args.neighbours == "all":
+        n_ = len(states_h)
+        rp = np.arange(n_ + 1, dtype=np.int32) * (n_ - 1)
+        col = np.array([j for a in range(n_) for j in range(n_) if j != a], dtype=np.int32)
     else:
         rp, col = swarm.knn_csr(states_h, args.knn, radius)
     n = len(states_h)
