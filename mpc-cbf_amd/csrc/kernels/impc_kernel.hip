@@ -338,10 +338,28 @@ __device__ __forceinline__ void defer_agent(const ImpcArgs& args, int ai, int gl
 
 // One agent's IMPC step on the separable layout (the body of impc_sep_kernel). stage / red / nbs:
 // this group's LDS (CBF-row staging, Newton-sum all-reduce, neighbour query).
+// The (non-slack) fallback launch keeps a lane's rows (SepRows, e.g. 8 CBF slots: 60 doubles) in
+// LDS instead of registers: its occupancy is one wave per SIMD either way, and in registers they
+// spilled (1236 -> 424 B/lane for 8 slots, 44 -> 0 for 1). Padded to an odd number of doubles per
+// lane (bank spread of the per-lane struct reads). The slack fallback keeps them in registers: in
+// LDS its results changed in the last bits and one all-neighbour slack QP of the stress line
+// (255 slacks, weights down to 1e-9) flipped to UNKNOWN.
+template <int SB, int CB>
+struct SepRowsLds {
+    SepRows<SB, CB> r;
+    double pad[(sizeof(SepRows<SB, CB>) / 8) % 2 == 0 ? 1 : 2];
+};
+
+template <bool LDS, int SB, int CB>
+__device__ __forceinline__ SepRows<SB, CB>& pick_rows(SepRows<SB, CB>& reg, SepRowsLds<SB, CB>* lds) {
+    if constexpr (LDS) return lds[threadIdx.x].r;
+    else return reg;
+}
+
 template <int SB, int CB, bool SLACK, bool QUEUE, bool LEAN = false>
 __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
                                const int ai, const int gl, double* stage, double* red, NbScratch& nbs,
-                               double* keep) {
+                               double* keep, SepRowsLds<SB, CB>* rows_lds = nullptr) {
     constexpr int G = 16;
     constexpr int NZ = SEP_NZ;
     constexpr int cap = CB * G;  // CBF rows per agent
@@ -356,7 +374,8 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
 
     // ---- box rows: channel d, slot k -> row k * G + gl of that channel (packed by the host:
     // per row [g0, g1, Gs(6), lo, hi], two-sided; unused rows inert: g = 0, Gs = 0, [-1, 1])
-    SepRows<SB, CB> rw;
+    SepRows<SB, CB> rw_reg;  // (the fallback launch: rows in LDS)
+    SepRows<SB, CB>& rw = pick_rows<QUEUE && !SLACK>(rw_reg, rows_lds);
     {
         const double* B = opp(buf, op.o_Gsep);
 #pragma unroll
@@ -637,12 +656,16 @@ template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = fa
 __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
                                                        const ImpcArgs args) {
     constexpr int GPB = BS / 16;
-    __shared__ double stage_all[GPB][SLACK ? 1 : CB * 16 * (SEP_NZ + 1)];
+    // CBF-row staging, reused as the dual active set's scratch (sep_pol_doubles)
+    constexpr int STAGE = CB * 16 * (SEP_NZ + 1) > sep_pol_doubles<SB, CB>() ? CB * 16 * (SEP_NZ + 1)
+                                                                             : sep_pol_doubles<SB, CB>();
+    __shared__ double stage_all[GPB][SLACK ? 1 : STAGE];
     __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
     // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
     // set's warm-start side ids and their count (not in slack mode)
     __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1)];
+    __shared__ SepRowsLds<SB, CB> rows_lds[QUEUE && !SLACK ? BS : 1];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     if constexpr (!QUEUE) {
@@ -657,7 +680,7 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
         const int k = blockIdx.x * GPB + gib;
         if (k < args.queue[0])
             impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
-                                                nb_scratch[gib], keep_all[gib]);
+                                                nb_scratch[gib], keep_all[gib], rows_lds);
         __syncthreads();
         if (threadIdx.x == 0) {
             __threadfence();

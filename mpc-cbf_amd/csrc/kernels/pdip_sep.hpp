@@ -85,6 +85,12 @@ __device__ __forceinline__ void sep_solve(const double (&Mxy)[10], const double 
 constexpr int POL_K = 6;
 // staged row (16 doubles): g (6) | b | side sign (+1 upper, -1 lower) | P^-1 g (6) | side id | -
 constexpr int POL_B = 6, POL_SGN = 7, POL_W = 8, POL_ID = 14;
+// sep_dual_as scratch (doubles per group): POL_K staged rows + the candidate, then the candidate
+// weights (one float per row and lane)
+template <int SB, int CB>
+constexpr int sep_pol_doubles() {
+    return (POL_K + 1) * 16 + 8 * (3 * SB + CB);
+}
 
 // inverse of P's 2x2 channel blocks (DevOps::o_Pinv, computed on the host): pi[d] = (a, b, c)
 // of [[a b] [b c]]
@@ -373,6 +379,14 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     const int gl = lane_bits_opaque<G - 1>();
     double pi[SEP_D][3];
     sep_pinv(Pinv, pi);
+    // P's 2x2 channel blocks for the dual residual at the end, loaded here (uniform: scalar
+    // registers) so the loads are not on the converged solve's critical path
+    double pb[SEP_NZ][2];
+#pragma unroll
+    for (int o = 0; o < SEP_NZ; o++) {
+        pb[o][0] = P[o * 6 + 2 * (o / 2)];
+        pb[o][1] = P[o * 6 + 2 * (o / 2) + 1];
+    }
     constexpr int NS = 2 * SEP_D * SB + CB;
     double sc[NS];  // violation scale 1 / (1 + |bound|) per side
     {
@@ -391,15 +405,28 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     // with the largest violation per unit norm in the P^-1 metric, v / sqrt(g P^-1 g) — the side
     // whose addition alone raises the dual objective most (v^2 / 2 g P^-1 g). The plain scaled
     // rule picked sides that later left again: on the driver bench's slowest QPs 10-12 steps
-    // where this rule needs 4-8 (tools/das_sim.py, the same QPs in numpy). The weights are
-    // formed in each scan from the uniform P^-1 blocks (scalar registers), not kept live.
-    auto row_wn = [&](double g0, double g1, double g2, double g3, int d0, bool two) -> float {
-        asm volatile("" : "+v"(g0), "+v"(g1));  // per scan: not hoisted out of the step loop
-        const double* a = Pinv + 3 * d0;
-        double n2 = fma(fma(a[0], g0, 2.0 * a[1] * g1), g0, a[2] * g1 * g1);
-        if (two) n2 += fma(fma(Pinv[3], g2, 2.0 * Pinv[4] * g3), g2, Pinv[5] * g3 * g3);
-        return rsqrtf((float)fmax(n2, 1e-30));
-    };
+    // where this rule needs 4-8 (tools/das_sim.py, the same QPs in numpy). One weight per row
+    // (both sides of a box row share it), formed once per solve into the scratch after the
+    // staged rows (wrow[r * 16 + lane]); inert rows (g = 0) are never violated.
+    float* wrow = (float*)(pol + (POL_K + 1) * 16);
+    {
+        int r = 0;
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+            for (int kk = 0; kk < SB; kk++, r++) {
+                const double g0 = rw.bg[d][kk][0], g1 = rw.bg[d][kk][1];
+                const double n2 = fma(fma(pi[d][0], g0, 2.0 * pi[d][1] * g1), g0, pi[d][2] * g1 * g1);
+                wrow[r * 16 + gl] = rsqrtf((float)fmax(n2, 1e-30));
+            }
+#pragma unroll
+        for (int c = 0; c < CB; c++, r++) {
+            const double* g = rw.cg[c];
+            const double n2 = fma(fma(pi[0][0], g[0], 2.0 * pi[0][1] * g[1]), g[0], pi[0][2] * g[1] * g[1]) +
+                              fma(fma(pi[1][0], g[2], 2.0 * pi[1][1] * g[3]), g[2], pi[1][2] * g[3] * g[3]);
+            wrow[r * 16 + gl] = rsqrtf((float)fmax(n2, 1e-30));
+        }
+    }
     double y[SEP_NZ], u[POL_K];
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
@@ -407,25 +434,6 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     for (int i = 0; i < POL_K; i++) u[i] = 0.0;
     int k = 0;
     steps = 0;
-    {
-        // a non-finite start or row (NaN / Inf state, target or neighbour state) fails every
-        // violation comparison below, so the scan would pass it as converged: give up and let the
-        // PDIP's finiteness checks decide
-        bool nf = false;
-#pragma unroll
-        for (int j = 0; j < SEP_NZ; j++) nf = nf || !isfinite(yu[j]);
-#pragma unroll
-        for (int d = 0; d < SEP_D; d++)
-#pragma unroll
-            for (int kk = 0; kk < SB; kk++)
-                nf = nf || !isfinite(rw.bg[d][kk][0] + rw.bg[d][kk][1] + rw.blo[d][kk] + rw.bhi[d][kk]);
-        if (has_cbf) {
-#pragma unroll
-            for (int c = 0; c < CB; c++)
-                nf = nf || !isfinite(rw.cg[c][0] + rw.cg[c][1] + rw.cg[c][2] + rw.cg[c][3] + rw.chi[c]);
-        }
-        if (grp_ballot<G>(nf) != 0ull) return 0;
-    }
     const double add_tol = 0.1 * tol;
     double* cand = pol + POL_K * 16;
     using S6 = Sym<POL_K>;
@@ -484,43 +492,47 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     GSTAMP(1, true);
     for (int outer = 0;; outer++) {
         (void)outer;
-        // the group's largest scaled violation (convergence) and its candidate (lowest lane on
-        // ties): the eligible side with the largest normalised violation
+        // the group's largest scaled violation (convergence) and the candidate (lowest lane on
+        // ties): the side violated beyond the tolerance with the largest normalised violation. A
+        // NaN row or iterate (a NaN state, target or neighbour state) shows as a NaN violation on
+        // the first scan: give up, the caller's finiteness checks decide.
         double vb = -1.0, eb = -1.0;
         int sb = 0;
+        bool nanv = false;
         {
-            int s = 0;
+            int s = 0, r = 0;
 #pragma unroll
             for (int d = 0; d < SEP_D; d++)
 #pragma unroll
-                for (int kk = 0; kk < SB; kk++) {
+                for (int kk = 0; kk < SB; kk++, r++) {
                     const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
+                    const double w = (double)wrow[r * 16 + gl];
                     const double al = rw.blo[d][kk] - t, vl = al * sc[s];
-                    const float w = row_wn(rw.bg[d][kk][0], rw.bg[d][kk][1], 0.0, 0.0, d, false);
                     const double el = vl > add_tol ? al * w : -1.0;
-                    vb = fmax(vb, vl);
                     if (el > eb) eb = el, sb = s;
                     s++;
                     const double au = t - rw.bhi[d][kk], vu = au * sc[s];
                     const double eu = vu > add_tol ? au * w : -1.0;
-                    vb = fmax(vb, vu);
                     if (eu > eb) eb = eu, sb = s;
                     s++;
+                    nanv = nanv || vl != vl || vu != vu;
+                    vb = fmax(vb, fmax(vl, vu));
                 }
             if (has_cbf) {
 #pragma unroll
-                for (int c = 0; c < CB; c++, s++) {
+                for (int c = 0; c < CB; c++, s++, r++) {
                     double t = 0.0;
 #pragma unroll
                     for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
                     const double ac = t - rw.chi[c], vc = ac * sc[s];
-                    const float w = row_wn(rw.cg[c][0], rw.cg[c][1], rw.cg[c][2], rw.cg[c][3], 0, true);
-                    const double ec = vc > add_tol ? ac * w : -1.0;
-                    vb = fmax(vb, vc);
+                    const double ec = vc > add_tol ? ac * (double)wrow[r * 16 + gl] : -1.0;
                     if (ec > eb) eb = ec, sb = s;
+                    nanv = nanv || vc != vc;
+                    vb = fmax(vb, vc);
                 }
             }
         }
+        if (outer == 0 && grp_ballot<G>(nanv) != 0ull) return 0;
         m = vb;
         double em = eb;
         grp_max2<G>(m, em);
@@ -712,18 +724,37 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         if (grp_ballot<G>(nf) != 0ull) return 0;
     }
     double rd = 0.0, qn = 0.0;
+    if (k == 0) {  // (group-uniform) the unconstrained minimiser, most QPs: P y + q alone
 #pragma unroll
-    for (int d = 0; d < SEP_D; d++) {
+        for (int o = 0; o < SEP_NZ; o++) {
+            const int d = o / 2;
+            rd = fmax(rd, fabs(fma(pb[o][0], y[2 * d], fma(pb[o][1], y[2 * d + 1], q[o]))));
+            qn = fmax(qn, fabs(q[o]));
+        }
+    } else {
+        // G_A^T lam over the wave's largest active count only (scalar loop bound), each active
+        // row's entries read once
+        int kw = 0;
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int o = 2 * d + h;
-            double r = fma(P[o * 6 + 2 * d], y[2 * d], fma(P[o * 6 + 2 * d + 1], y[2 * d + 1], q[o]));
+        for (int i = 1; i <= POL_K; i++) kw += __ballot(k >= i) != 0ull ? 1 : 0;
+        double r[SEP_NZ];
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) {
+        for (int o = 0; o < SEP_NZ; o++) {
+            const int d = o / 2;
+            r[o] = fma(pb[o][0], y[2 * d], fma(pb[o][1], y[2 * d + 1], q[o]));
+        }
+#pragma unroll
+        for (int i = 0; i < POL_K; i++) {
+            if (i < kw) {
                 const double* ri = pol + (i < k ? i : 0) * 16;
-                r = fma(i < k ? ri[POL_SGN] * u[i] : 0.0, ri[o], r);
+                const double li = i < k ? ri[POL_SGN] * u[i] : 0.0;
+#pragma unroll
+                for (int o = 0; o < SEP_NZ; o++) r[o] = fma(li, ri[o], r[o]);
             }
-            rd = fmax(rd, fabs(r));
+        }
+#pragma unroll
+        for (int o = 0; o < SEP_NZ; o++) {
+            rd = fmax(rd, fabs(r[o]));
             qn = fmax(qn, fabs(q[o]));
         }
     }
@@ -731,12 +762,8 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     GSTAMP(9, true);
     auto save_sides = [&]() {  // the final active set's side ids, for a later warm start
         if (save == nullptr) return;
-        if (gl == 0) {
-#pragma unroll
-            for (int i = 0; i < POL_K; i++)
-                if (i < k) save[i] = pol[i * 16 + POL_ID];
-            save[POL_K] = (double)k;
-        }
+        if (gl < k) save[gl] = pol[gl * 16 + POL_ID];
+        if (gl == 0) save[POL_K] = (double)k;
     };
     if (!(rd <= tol)) {
         // rounding accumulated over the steps: the active set's equality QP, re-solved exactly
