@@ -7,7 +7,7 @@
 #   FP64 instruction mix, and the FoV kernels' FP64 MFMA counters.
 # Order: PMC passes first (their summary goes to profiles/<tag>_pmc_summary.json, which the bench
 # lines read), then the bench lines and kernel traces, then the GPU tests and the stamp profile.
-# Usage: bash tools/profile_round.sh <tag> [nopmc]
+# Usage: bash tools/profile_round.sh <tag> [nopmc|pmc]   (pmc: the PMC passes only; nopmc: the rest)
 set -e -o pipefail
 TAG=${1:-rNN}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -45,9 +45,14 @@ pmc collision_cache -- SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_ICAC
 python3 $ROOT/tools/pmc_summary.py $OUT/${TAG}_pmc > $ROOT/profiles/${TAG}_pmc_summary.json
 cp $ROOT/profiles/${TAG}_pmc_summary.json $OUT/${TAG}_pmc_summary.json
 }
+[ "$2" = "pmc" ] && { step done; exit 0; }
 step bench driver; timeout -k 10 200 $B --steps 20 --warmup 5 > $OUT/${TAG}_bench_driver.json 2> $OUT/${TAG}_bench_driver.err
 step bench 1000; timeout -k 10 300 $B > $OUT/${TAG}_bench_collision.json 2> $OUT/${TAG}_bench_collision.err
 step bench 8192; timeout -k 10 300 $B --agents-per-gpu 8192 --no-cpu-baseline > $OUT/${TAG}_bench_8192.json 2> $OUT/${TAG}_bench_8192.err
+step bench share; timeout -k 10 300 $B --rank-share 8 --agents-total 8192 --no-cpu-baseline > $OUT/${TAG}_bench_share.json 2> $OUT/${TAG}_bench_share.err
+step bench crowded; timeout -k 10 300 $B --crowded --steps 300 --warmup 20 > $OUT/${TAG}_bench_crowded.json 2> $OUT/${TAG}_bench_crowded.err
+step bench all256; timeout -k 10 300 $B --neighbours all --agents-per-gpu 256 --crowded --steps 200 --warmup 20 > $OUT/${TAG}_bench_all256.json 2> $OUT/${TAG}_bench_all256.err
+step bench all256 slack; timeout -k 10 300 $B --neighbours all --agents-per-gpu 256 --crowded --slack --steps 200 --warmup 20 > $OUT/${TAG}_bench_all256_slack.json 2> $OUT/${TAG}_bench_all256_slack.err
 step bench fov; timeout -k 10 300 $B --workload fov > $OUT/${TAG}_bench_fov.json 2> $OUT/${TAG}_bench_fov.err
 step bench fov slack; timeout -k 10 300 $B --workload fov --slack > $OUT/${TAG}_bench_fov_slack.json 2> $OUT/${TAG}_bench_fov_slack.err
 prof() {  # name, bench args
@@ -58,11 +63,16 @@ prof() {  # name, bench args
 prof driver --steps 20 --warmup 5
 prof collision
 prof 8192 --agents-per-gpu 8192
+prof share --rank-share 8 --agents-total 8192
+prof crowded --crowded --steps 300 --warmup 20
+prof all256 --neighbours all --agents-per-gpu 256 --crowded --steps 200 --warmup 20 --no-trace
 prof fov --workload fov
 prof fov_slack --workload fov --slack
 step bench dense; timeout -k 10 300 $B --workload dense --steps 10 --warmup 2 > $OUT/${TAG}_bench_dense.json 2> $OUT/${TAG}_bench_dense.err
 prof dense --workload dense --steps 10 --warmup 2
 step pytest; (cd $ROOT && timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/${TAG}_pytest_gpu.log 2>&1)
 step fovs status; MPCCBF_CHECK_SLACK=1 timeout -k 10 300 python3 $ROOT/tools/fov_status_check.py 1000 $OUT/${TAG}_fovs_status.npz > $OUT/${TAG}_fovs_status.log 2>&1
-step stamps; MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 $ROOT/tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1
+step stamps; (cd $ROOT && timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1)
+step stamps pdip; (cd $ROOT && MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision_das.log 2>&1)
+step stamps fov; (cd $ROOT && WORKLOAD=fov timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov.log 2>&1)
 echo done
