@@ -369,8 +369,18 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     double s0[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) s0[i] = args.states[(size_t)self * 6 + i];
-    double q[NZ], kconst;
-    agent_linear_term<NZ>(op, buf, args, ai, s0, q, kconst);
+    // the linear term and constant, group-uniform: kept in LDS (qk, after the warm-start ids) and
+    // read back inside each IMPC iteration, so they are not live in registers across the loop
+    double* qk = keep + 16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1);
+    {
+        double q0[NZ], kc0;
+        agent_linear_term<NZ>(op, buf, args, ai, s0, q0, kc0);
+        if (gl == 0) {
+#pragma unroll
+            for (int j = 0; j < NZ; j++) qk[j] = q0[j];
+            qk[NZ] = kc0;
+        }
+    }
 
     // ---- box rows: channel d, slot k -> row k * G + gl of that channel (packed by the host:
     // per row [g0, g1, Gs(6), lo, hi], two-sided; unused rows inert: g = 0, Gs = 0, [-1, 1])
@@ -460,6 +470,11 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         int count = 0;
         bool live = false;
         bool slack_overflow = false;
+        wave_lds_sync();
+        asm volatile("" ::: "memory");  // (the reads below stay inside the iteration)
+        double q[NZ];
+#pragma unroll
+        for (int j = 0; j < NZ; j++) q[j] = qk[j];
         if constexpr (SLACK) {
             // slack mode: rows stay in their neighbour's lane; a slack row is never infeasible
             double sx[6];  // the state again (not kept in registers across the solves)
@@ -628,7 +643,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         }
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {
-            objv = reduced_objective<NZ>(op, buf, q, y, kconst);
+            objv = reduced_objective<NZ>(op, buf, q, y, qk[NZ]);
             if constexpr (SLACK) objv += grp_sum<G>(live ? wslack * vslack : 0.0);  // + w^T v
 #pragma unroll
             for (int i = 0; i < NZ; i++) ykeep[16 * i] = y[i];
@@ -663,8 +678,8 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
     // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
-    // set's warm-start side ids and their count (not in slack mode)
-    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1)];
+    // set's warm-start side ids and their count (not in slack mode) | linear term and constant
+    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 8];
     __shared__ SepRowsLds<SB, CB> rows_lds[QUEUE && !SLACK ? BS : 1];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
