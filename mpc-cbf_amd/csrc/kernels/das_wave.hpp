@@ -25,6 +25,7 @@ namespace dev {
 struct WaveAS {
     double W[WNZ * WNZ];     // active row a: P^-1 g_a (16 doubles)
     double Pi[WNZ * 17];     // P^-1, rows padded to 17 doubles (lane i reads row i: spread banks)
+    double P[WNZ * 17];      // P, the same layout (dual residual)
     double w[WNZ];           // the candidate's P^-1 g
     double b[WNZ], sg[WNZ];  // active rows' bound and side sign (+1 upper, -1 lower)
     double u[WNZ];           // multipliers (shift scratch; at the optimum: the active rows')
@@ -32,6 +33,25 @@ struct WaveAS {
     int32_t k;               // at the optimum: the number of active rows
     float wn[WROWS];         // candidate weights 1 / sqrt(g P^-1 g) per image row
 };
+
+// lane l's double as a wave-uniform (scalar) value
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)lo);
+}
+
+// a row (LDS) times a vector of scalar operands
+__device__ __forceinline__ double dot_rows_s(const double* a, const double (&ys)[WNZ]) {
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < WNZ; j += 2) {
+        s0 = fma(a[j], ys[j], s0);
+        s1 = fma(a[j + 1], ys[j + 1], s1);
+    }
+    return s0 + s1;
+}
 
 // first half of solve_rows: v = L^-1 b on the row layout
 __device__ __forceinline__ double fwd_rows(const double (&L)[WNZ], double inv_i, double b, int i) {
@@ -57,20 +77,44 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
     return xl;
 }
 
+// P and P^-1 (16 x 16, global) into the workspace, once per agent: every das_solve_wave call of
+// the agent reads them there (a per-call copy was a global round trip on each solve's chain)
+__device__ __forceinline__ void das_load_operators(WaveAS& ws, const double* __restrict__ P,
+                                                   const double* __restrict__ Pinv, int lane) {
+    for (int e = lane; e < WNZ * WNZ; e += 64) {
+        ws.Pi[(e >> 4) * 17 + (e & 15)] = Pinv[e];
+        ws.P[(e >> 4) * 17 + (e & 15)] = P[e];
+    }
+    wave_lds_sync();
+}
+
 // Returns 1: optimal (sc.y, rp_out, rd_out; the active rows' multipliers in ws.u[0 .. ws.k)); -1: no
 // step reaches the candidate (no feasible point; tlow = the certificate's lower bound on phase
 // 1's t*; cand = the unreachable candidate's image row, the active rows in ws.row[0 .. ws.k) with
 // their certificate weights in ws.u: candidate + sum_a u_a n_a = 0); 0: gave up (step limit,
 // breakdown, dual residual) — the PDIP solves.
-// Pinv: P^-1 padded to 16 x 16 (global); P for the dual residual (want_rd).
+// ws.Pi / ws.P: P^-1 and P (das_load_operators); the P / Pinv arguments are not read.
 __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, WaveScratch& sc,
                               WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
                               double tol, int maxstep, bool want_rd, int lane, double& rp_out,
                               double& rd_out, int& steps, double& tlow, int* cand = nullptr,
-                              int nfirst = 0, int nrows = WROWS) {
+                              int nfirst = 0, int nrows = WROWS, long long* dbg = nullptr) {
+    (void)dbg;
+#ifdef MPCCBF_PDIP_STAMPS  // profiling build: shader-clock stamps of the solve's first steps
+#define WSTAMP(kk, cond)                                                              \
+    do {                                                                              \
+        if (dbg && lane == 0 && (cond)) dbg[kk] = (long long)__builtin_amdgcn_s_memtime(); \
+    } while (0)
+    if (dbg && lane == 0) dbg[15] = 2;
+#else
+#define WSTAMP(kk, cond) \
+    do {                 \
+    } while (0)
+#endif
+    WSTAMP(0, true);
     const int i = lane16_opaque(lane);
     steps = 0;
-    for (int e = lane; e < WNZ * WNZ; e += 64) ws.Pi[(e >> 4) * 17 + (e & 15)] = ldg_nohoist(Pinv + e);
+    (void)Pinv;  // (ws.Pi / ws.P: loaded once per agent by das_load_operators)
     // per-slot violation scales, the factor of the empty active set (identity)
     double pl[WR], pu[WR];
 #pragma unroll
@@ -95,6 +139,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         yi = -a;
     }
     publish16(sc.y, yi, lane);
+    WSTAMP(1, true);
     int k = 0;
     double m = 0.0;
     const double add_tol = 0.1 * tol;
@@ -128,9 +173,14 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         int rb = 0, sdb = 1;
         double bb = 0.0;
         bool nf = false;  // a NaN row or iterate fails every comparison: give up instead
+        // the iterate as scalar operands (lane j of the row layout holds y_j): the row scans then
+        // read only their rows from LDS
+        double ys[WNZ];
+#pragma unroll
+        for (int j = 0; j < WNZ; j++) ys[j] = readlane_d(yi, j);
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            const double t = dotl(rw.g[s], sc.y);
+            const double t = dot_rows_s(rw.g[s], ys);
             const double al = rw.lo[s] - t, au = t - rw.hi[s];
             const double vl = rw.ml[s] > 0.0 ? al * pl[s] : -1.0;
             const double vu = au * pu[s];
@@ -147,6 +197,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         m = vb;
         double em = eb;
         wave_reduce2<Op::Max, Op::Max>(m, em);
+        WSTAMP(steps == 0 ? 2 : 8, steps <= 1);
         if (!(m > add_tol)) break;
         if (!have_wn) {  // first violation: form the weights and scan again
             row_weights();
@@ -165,6 +216,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         for (int j = 0; j < WNZ; j++) wi = fma(ws.Pi[i * 17 + j], gp[j], wi);
         publish16(ws.w, wi, lane);
         const double nw = dotl(gp, ws.w);
+        WSTAMP(3, steps == 0);
         double up = 0.0;  // the candidate's multiplier
         for (;;) {
             if (++steps > maxstep) return 0;
@@ -176,6 +228,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
             const double rhoi = bwd_rows(sc.M, inv_i, vi, i);
             const double zn = nw - grp_sum<16>(vi * vi);
             const double vp = sp * (dotl(gp, sc.y) - bp);
+            WSTAMP(4, steps == 1);
             // dual step: the first active multiplier to reach zero
             const double r_i = sgi * rhoi;
             const double ratio = (i < k && r_i > 0.0) ? ui * rcp(r_i) : 1e300;
@@ -183,6 +236,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
             const int l = t1 < 1e300 ? __ffsll((long long)grp_ballot<16>(ratio == t1)) - 1 : -1;
             const bool full = zn > 1e-10 * nw;  // else n_p lies in the span of the active sides
             const double t2 = full ? vp * rcp(zn) : 1e300;
+            WSTAMP(5, steps == 1);
             if (l < 0 && !full) {
                 // certificate lam = (1, -r) >= 0 (every r <= 0): t* >= vp / (1 - sum r)
                 tlow = vp * rcp(1.0 + grp_sum<16>((i < k && r_i < 0.0) ? -r_i : 0.0));
@@ -205,6 +259,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
             ui = i < k ? fma(-t, r_i, ui) : ui;
             up += t;
             publish16(sc.y, yi, lane);
+            WSTAMP(6, steps == 1);
             if (t2 <= t1) {  // the candidate joins: L gains (v^T, sqrt(zn))
                 if (k == WNZ - 1) return 0;
                 const double dz = sqrt(zn), rz = rcp(dz);
@@ -227,6 +282,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
                 ui = i == k ? up : ui;
                 k++;
                 wave_lds_sync();
+                WSTAMP(7, steps == 1);
                 break;
             }
             // side l leaves: rows above it move down (lane j: column j), K refactored
@@ -256,6 +312,8 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         }
     }
     // a non-finite iterate fails every violation test, so it would pass as converged: give up
+    WSTAMP(9, true);
+    if (dbg && lane == 0) dbg[14] = steps;
     if (__ballot(!isfinite(yi)) != 0ull) return 0;
     // converged: primal residual = the last scan's worst violation; dual residual of the iterate
     // P y + q + G_A^T lam (lam_a = sign_a u_a), checked whether or not the caller stores it
@@ -264,7 +322,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
     {
         double r = sc.q[i];
 #pragma unroll
-        for (int j = 0; j < WNZ; j++) r = fma(ldg_nohoist(P + i * WNZ + j), sc.y[j], r);
+        for (int j = 0; j < WNZ; j++) r = fma(ws.P[i * 17 + j], sc.y[j], r);
 #pragma unroll
         for (int a = 0; a < WNZ - 1; a++) {
             const double la = bcast16v(a, ui * (i < k ? ws.sg[i < k ? i : 0] : 0.0));
@@ -278,8 +336,10 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
     if (lane == 0) ws.k = k;
     rp_out = fmax(m, 0.0);
     rd_out = rd;
+    WSTAMP(10, true);
     return 1;
 }
+#undef WSTAMP
 
 }  // namespace dev
 }  // namespace mpccbf

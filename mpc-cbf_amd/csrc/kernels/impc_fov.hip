@@ -113,6 +113,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     if (lane < WNZ) Gimg[WROWS * WNZ + lane] = 0.0;
     zero_row = &Gimg[WROWS * WNZ];
     const bool infeasible = constant_rows_infeasible<64>(op, buf, s0, lane);
+    das_load_operators(was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16), lane);
     stamp(args, ai, lane, 1);
 
     const bool grid_mode = args.nb_row_ptr == nullptr;
@@ -511,7 +512,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 if (op.dual_as > 0)
                     das = das_solve_wave(image_rows(mtot), Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16),
                                          op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps,
-                                         dtlow, nullptr, mtot, mtot);
+                                         dtlow, nullptr, mtot, mtot, dbg);
             } else if (pattern_ok) {
                 if (lv) slk->rowl[c_me] = lane;
                 das = run_patterns(SLK_PATTERNS);

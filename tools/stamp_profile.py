@@ -92,6 +92,20 @@ for v in VARIANTS:
             for name, a, b in (names0 if nstep == 0 else names):
                 d = ps[m, b] - ps[m, a]
                 print(f"   {name:15s} mean {d.mean():7.0f}  p50 {np.median(d):7.0f} cycles")
+    if PDIP and v == 0 and FOV:  # the wave dual active set's stamps (das_wave.hpp, solve 0)
+        ps = allst[N * 8:].reshape(N, 16).astype(np.float64)
+        names = [("init", 0, 1), ("scan 1", 1, 2), ("candidate P^-1 g", 2, 3), ("subst + dots", 3, 4),
+                 ("step lengths", 4, 5), ("update y, u", 5, 6), ("join", 6, 7), ("scan 2", 7, 8)]
+        names0 = [("init", 0, 1), ("scan", 1, 2), ("converged", 2, 9), ("dual residual", 9, 10)]
+        for nstep in (0, 1, 2, 3):
+            m = (ps[:, 15] == 2) & (ps[:, 14] == nstep) & (ps[:, 10] > 0)
+            if m.sum() == 0:
+                continue
+            print(f"variant {v}: wave active-set solves with {nstep} step(s): {m.sum()} agents, "
+                  f"cycles entry->exit mean {np.mean(ps[m, 10] - ps[m, 0]):.0f}")
+            for name, a, b in (names0 if nstep == 0 else names + [("rest to exit", 8, 10)]):
+                d = ps[m, b] - ps[m, a]
+                print(f"   {name:17s} mean {d.mean():7.0f}  p50 {np.median(d):7.0f} cycles")
     status = out["status"].cpu().numpy()
     t0 = s[:, 0].min()
     start = s[:, 0] - t0
