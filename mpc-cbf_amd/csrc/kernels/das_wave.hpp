@@ -53,11 +53,13 @@ __device__ __forceinline__ double dot_rows_s(const double* a, const double (&ys)
     return s0 + s1;
 }
 
-// first half of solve_rows: v = L^-1 b on the row layout
-__device__ __forceinline__ double fwd_rows(const double (&L)[WNZ], double inv_i, double b, int i) {
+// first half of solve_rows: v = L^-1 b on the row layout, over the first kk rows (kk wave-uniform:
+// rows from kk on are identity rows of L with a zero right-hand side, v_i = 0 there)
+__device__ __forceinline__ double fwd_rows(const double (&L)[WNZ], double inv_i, double b, int i, int kk) {
     double res = b, wl = 0.0;
 #pragma unroll
     for (int k = 0; k < WNZ; k++) {
+        if (k >= kk) break;
         const double wk = bcast16v(k, res * inv_i);
         res = fma(-L[k], wk, res);
         wl = (i == k) ? wk : wl;
@@ -65,11 +67,13 @@ __device__ __forceinline__ double fwd_rows(const double (&L)[WNZ], double inv_i,
     return wl;
 }
 
-// second half of solve_rows: x = L^-T v (L's columns from the row-major copy Lm)
-__device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double inv_i, double v, int i) {
+// second half of solve_rows: x = L^-T v (L's columns from the row-major copy Lm), over the first kk
+// rows (v_i = 0 from kk on, so x_i = 0 there)
+__device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double inv_i, double v, int i, int kk) {
     double res = v, xl = 0.0;
 #pragma unroll
     for (int k = WNZ - 1; k >= 0; k--) {
+        if (k >= kk) continue;
         const double xk = bcast16v(k, res * inv_i);
         res = fma(-Lm[k * WNZ + i], xk, res);
         xl = (i == k) ? xk : xl;
@@ -94,7 +98,8 @@ __device__ __forceinline__ void das_load_operators(WaveAS& ws, const double* __r
 // their certificate weights in ws.u: candidate + sum_a u_a n_a = 0); 0: gave up (step limit,
 // breakdown, dual residual) — the PDIP solves.
 // ws.Pi / ws.P: P^-1 and P (das_load_operators); the P / Pinv arguments are not read.
-__device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, WaveScratch& sc,
+template <bool BOUND = true>
+__device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, WaveScratch& sc,
                               WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
                               double tol, int maxstep, bool want_rd, int lane, double& rp_out,
                               double& rd_out, int& steps, double& tlow, int* cand = nullptr,
@@ -220,12 +225,19 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
         double up = 0.0;  // the candidate's multiplier
         for (;;) {
             if (++steps > maxstep) return 0;
+            // BOUND: the active count as a wave-uniform bound — the substitutions, the direction and
+            // the dual residual run over the active rows only (scalar branches; typically k <= 3 of
+            // 15). The slack-pattern solves keep the full loops (bounded, their kernel spills).
+            const int kk = BOUND ? __builtin_amdgcn_readfirstlane(k) : WNZ;
             // c_a = n_a-side coefficient: g_a P^-1 n_p (lane a < k), v = L^-1 c, r = L^-T v
-            const int ra = i < k ? ws.row[i] : rp;
-            const double ci = i < k ? sp * dotl(Gs + ra * WNZ, ws.w) : 0.0;
-            const double sgi = i < k ? ws.sg[i] : 0.0;
-            const double vi = fwd_rows(L, inv_i, ci, i);
-            const double rhoi = bwd_rows(sc.M, inv_i, vi, i);
+            double ci = 0.0, sgi = 0.0;
+            if (kk > 0) {
+                const int ra = i < k ? ws.row[i] : rp;
+                ci = i < k ? sp * dotl(Gs + ra * WNZ, ws.w) : 0.0;
+                sgi = i < k ? ws.sg[i] : 0.0;
+            }
+            const double vi = fwd_rows(L, inv_i, ci, i, kk);
+            const double rhoi = bwd_rows(sc.M, inv_i, vi, i, kk);
             const double zn = nw - grp_sum<16>(vi * vi);
             const double vp = sp * (dotl(gp, sc.y) - bp);
             WSTAMP(4, steps == 1);
@@ -251,6 +263,7 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
                 double zi = sp * wi;
 #pragma unroll
                 for (int a = 0; a < WNZ - 1; a++) {
+                    if (a >= kk) break;
                     const double ra_ = bcast16v(a, rhoi);
                     zi = fma(a < k ? -ra_ : 0.0, ws.W[(a < k ? a : 0) * WNZ + i], zi);
                 }
@@ -316,16 +329,21 @@ __device__ int das_solve_wave(const WaveRows& rw, const double* __restrict__ Gs,
     if (dbg && lane == 0) dbg[14] = steps;
     if (__ballot(!isfinite(yi)) != 0ull) return 0;
     // converged: primal residual = the last scan's worst violation; dual residual of the iterate
-    // P y + q + G_A^T lam (lam_a = sign_a u_a), checked whether or not the caller stores it
-    (void)want_rd;
+    // P y + q + G_A^T lam (lam_a = sign_a u_a), checked whether or not the caller stores it when a
+    // side is active
+    // With no active side the iterate is -P^-1 q (P^-1 from the host): its dual residual is rounding,
+    // so (BOUND) it is only evaluated when the caller stores it.
     double rd = 0.0;
-    {
+    const int kk = BOUND ? __builtin_amdgcn_readfirstlane(k) : WNZ;
+    if (kk > 0 || want_rd) {
         double r = sc.q[i];
 #pragma unroll
         for (int j = 0; j < WNZ; j++) r = fma(ws.P[i * 17 + j], sc.y[j], r);
+        const double lsi = ui * (i < k ? ws.sg[i < k ? i : 0] : 0.0);
 #pragma unroll
         for (int a = 0; a < WNZ - 1; a++) {
-            const double la = bcast16v(a, ui * (i < k ? ws.sg[i < k ? i : 0] : 0.0));
+            if (a >= kk) break;
+            const double la = bcast16v(a, lsi);
             r = fma(a < k ? la : 0.0, Gs[(a < k ? ws.row[a] : 0) * WNZ + i], r);
         }
         double qn = fabs(sc.q[i]);

@@ -133,6 +133,22 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Diagnostics build (make poison): every kernel that calls this fills its block's static LDS with
+// MPCCBF_LDS_POISON before any other work, so two builds with different fill values give
+// bit-identical results unless something reads LDS it never wrote (tools/lds_poison_check.py).
+__device__ __forceinline__ void lds_poison() {
+#ifdef MPCCBF_LDS_POISON
+    const unsigned n = __builtin_amdgcn_groupstaticsize() / 8;
+    const double v = MPCCBF_LDS_POISON;
+    for (unsigned e = threadIdx.x; e < n; e += blockDim.x) {
+        const unsigned addr = e * 8;
+        asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+#endif
+}
+
 // Value of lane k (0..15) of this lane's 16-lane row (DPP row_newbcast; k folds to a constant
 // after unrolling).
 template <int K>

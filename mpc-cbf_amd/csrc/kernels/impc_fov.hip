@@ -56,6 +56,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     constexpr int NZ = 15;
     const int lane = threadIdx.x;
     const int ai = blockIdx.x;
+    lds_poison();
     grid_clear(args);
     if (ai >= args.num_agents) return;
     stamp(args, ai, lane, 0);
@@ -401,7 +402,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                     }
                     wave_lds_sync();
                     int st_ = 0, cand = -1;
-                    const int d = das_solve_wave(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
+                    const int d = das_solve_wave<false>(image_rows(mtot + ncbf), Gimg, sc, was, opp(buf, op.o_P16),
                                                  opp(buf, op.o_Pinv16), op.tol, 2 * op.dual_as,
                                                  args.dual_res != nullptr, lane, drp, drd, st_, dtlow, &cand,
                                                  mtot, mtot + ncbf);

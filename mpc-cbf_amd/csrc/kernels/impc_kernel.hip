@@ -683,6 +683,7 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     __shared__ SepRowsLds<SB, CB> rows_lds[QUEUE && !SLACK ? BS : 1];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
+    lds_poison();
     if constexpr (!QUEUE) {
         grid_clear(args);
         const int ai = blockIdx.x * GPB + gib;
