@@ -212,11 +212,14 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
     }
     if (full) total = (uint32_t)args.num_states;
     int cnt = 0;
-    for (uint32_t t0 = 0; t0 < total; t0 += G) {
-        const uint32_t t = t0 + gl;
+    // candidate t: its agent index (bucket slot, or t itself when scanning the whole table), state,
+    // squared distance and whether it is a neighbour (within the radius and, for the FoV
+    // controller, the cone)
+    auto load_cand = [&](uint32_t t, int& j, double& d2, double& nx, double& ny, double& nvx, double& nvy) -> bool {
         bool keep = false;
-        int j = -1;
-        double d2 = 0.0, nx = 0.0, ny = 0.0, nvx = 0.0, nvy = 0.0;
+        j = -1;
+        d2 = 0.0;
+        nx = ny = nvx = nvy = 0.0;
         if (t < total) {
             if (full) {
                 j = (int)t;
@@ -241,6 +244,10 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
                 keep = fabs(offa) < gr.cone;
             }
         }
+        return keep;
+    };
+    // compaction of one chunk of G candidates into sc (in candidate order)
+    auto put_chunk = [&](bool keep, int j, double d2, double nx, double ny, double nvx, double nvy) {
         const unsigned long long msk = grp_ballot<G>(keep);
         const int slot = cnt + __popcll(msk & ((1ull << gl) - 1ull));
         if (keep && slot < NB_CAP) {
@@ -252,6 +259,26 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
             sc.cst[3][slot] = nvy;
         }
         cnt += __popcll(msk);
+    };
+    if constexpr (G == 16) {
+        // two chunks per pass (candidates gl and G + gl): both chunks' dependent loads (bucket slot,
+        // then the agent's state) are in flight together — the 9 cells typically hold 17-32
+        // candidates, which took two serial round-trip pairs chunk by chunk
+        for (uint32_t t0 = 0; t0 < total; t0 += 2 * G) {
+            int ja, jb;
+            double da, xa, ya, vxa, vya, db, xb, yb, vxb, vyb;
+            const bool ka = load_cand(t0 + gl, ja, da, xa, ya, vxa, vya);
+            const bool kb = load_cand(t0 + G + gl, jb, db, xb, yb, vxb, vyb);
+            put_chunk(ka, ja, da, xa, ya, vxa, vya);
+            put_chunk(kb, jb, db, xb, yb, vxb, vyb);
+        }
+    } else {
+        for (uint32_t t0 = 0; t0 < total; t0 += G) {
+            int j;
+            double d2, nx, ny, nvx, nvy;
+            const bool keep = load_cand(t0 + gl, j, d2, nx, ny, nvx, nvy);
+            put_chunk(keep, j, d2, nx, ny, nvx, nvy);
+        }
     }
     if (cnt > NB_CAP) return grid_neighbors_stream<G>(args, self, px, py, sc, gl, yaw, hs, nc, off, total, full);
     wave_lds_sync();
