@@ -59,10 +59,11 @@ __device__ __forceinline__ double fwd_rows(const double (&L)[WNZ], double inv_i,
     double res = b, wl = 0.0;
 #pragma unroll
     for (int k = 0; k < WNZ; k++) {
-        if (k >= kk) break;
-        const double wk = bcast16v(k, res * inv_i);
-        res = fma(-L[k], wk, res);
-        wl = (i == k) ? wk : wl;
+        if (k < kk) {  // (uniform branch; a break here defeats the full unroll the DPP needs)
+            const double wk = bcast16v(k, res * inv_i);
+            res = fma(-L[k], wk, res);
+            wl = (i == k) ? wk : wl;
+        }
     }
     return wl;
 }
@@ -73,10 +74,11 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
     double res = v, xl = 0.0;
 #pragma unroll
     for (int k = WNZ - 1; k >= 0; k--) {
-        if (k >= kk) continue;
-        const double xk = bcast16v(k, res * inv_i);
-        res = fma(-Lm[k * WNZ + i], xk, res);
-        xl = (i == k) ? xk : xl;
+        if (k < kk) {
+            const double xk = bcast16v(k, res * inv_i);
+            res = fma(-Lm[k * WNZ + i], xk, res);
+            xl = (i == k) ? xk : xl;
+        }
     }
     return xl;
 }
@@ -263,9 +265,10 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
                 double zi = sp * wi;
 #pragma unroll
                 for (int a = 0; a < WNZ - 1; a++) {
-                    if (a >= kk) break;
-                    const double ra_ = bcast16v(a, rhoi);
-                    zi = fma(a < k ? -ra_ : 0.0, ws.W[(a < k ? a : 0) * WNZ + i], zi);
+                    if (a < kk) {
+                        const double ra_ = bcast16v(a, rhoi);
+                        zi = fma(a < k ? -ra_ : 0.0, ws.W[(a < k ? a : 0) * WNZ + i], zi);
+                    }
                 }
                 yi = fma(-t, zi, yi);
             }
@@ -342,9 +345,10 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         const double lsi = ui * (i < k ? ws.sg[i < k ? i : 0] : 0.0);
 #pragma unroll
         for (int a = 0; a < WNZ - 1; a++) {
-            if (a >= kk) break;
-            const double la = bcast16v(a, lsi);
-            r = fma(a < k ? la : 0.0, Gs[(a < k ? ws.row[a] : 0) * WNZ + i], r);
+            if (a < kk) {
+                const double la = bcast16v(a, lsi);
+                r = fma(a < k ? la : 0.0, Gs[(a < k ? ws.row[a] : 0) * WNZ + i], r);
+            }
         }
         double qn = fabs(sc.q[i]);
         rd = grp_max<16>(fabs(r)) * rcp(1.0 + grp_max<16>(qn));

@@ -9,10 +9,26 @@
 namespace mpccbf {
 namespace dev {
 
+// The FoV border rows' constants (FovCBF.cpp initLeftCBF / initRightCBF): kap = tan of the half
+// angle of the cone (fov < pi) or of its complement (fov > pi), the left border's sign (the right
+// border's is its negative); none: a 360-degree field of view has no border rows.
+struct FovBorder {
+    double kap, sig_left;
+    bool none;
+};
+
+__device__ __forceinline__ FovBorder fov_border(double fov) {
+    if (fov < M_PI) return FovBorder{tan(0.5 * fov), 1.0, false};
+    if (fov == M_PI) return FovBorder{1.0, 0.0, false};
+    if (fabs(fov - 2.0 * M_PI) <= 1e-9 * 2.0 * M_PI) return FovBorder{0.0, 0.0, true};
+    return FovBorder{tan(0.5 * (2.0 * M_PI - fov)), -1.0, false};
+}
+
 // FoV HOCBF rows at ego e against target (tx, ty): closed form of FovCBF::init*CBF with
 // alpha(x) = 0.1 x^5 (see oracle/oracle.cpp fov_rows for the derivation). present = false for
-// the vacuous border rows of a 360-degree field of view.
-__device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double tx, double ty, double fov,
+// the vacuous border rows of a 360-degree field of view. fb: fov_border(fov), formed once per
+// agent by callers that evaluate many rows.
+__device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double tx, double ty, const FovBorder& fb,
                                             double Ds, double Rs, double a[3], double& b, bool& present) {
     constexpr double gamma = 0.1;
     const double vx = e[3], vy = e[4], w = e[5];
@@ -30,23 +46,13 @@ __device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double 
         bval = kind == 0 ? dx * dx + dy * dy - Ds * Ds : Rs * Rs - dx * dx - dy * dy;
         lf2 = 2.0 * sgn * (vx * vx + vy * vy);
     } else {
-        double kap, sig;
-        const bool left = kind == 1;
-        if (fov < M_PI) {
-            kap = tan(0.5 * fov);
-            sig = left ? 1.0 : -1.0;
-        } else if (fov == M_PI) {
-            kap = 1.0;
-            sig = 0.0;
-        } else if (fabs(fov - 2.0 * M_PI) <= 1e-9 * 2.0 * M_PI) {
+        if (fb.none) {
             a[0] = a[1] = a[2] = 0.0;
             b = 1.7976931348623157e308;
             present = false;
             return;
-        } else {
-            kap = tan(0.5 * (2.0 * M_PI - fov));
-            sig = left ? -1.0 : 1.0;
         }
+        const double kap = fb.kap, sig = kind == 1 ? fb.sig_left : -fb.sig_left;
         bval = kap * rx + sig * ry;
         a[0] = -kap * cs + sig * sn;
         a[1] = -kap * sn - sig * cs;
@@ -58,6 +64,11 @@ __device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double 
     const double psi = lf + gamma * b4 * bval;
     const double p2 = psi * psi;
     b = lf2 + 5.0 * gamma * b4 * lf + gamma * p2 * p2 * psi;
+}
+
+__device__ __forceinline__ void fov_cbf_row(int kind, const double e[6], double tx, double ty, double fov, double Ds,
+                                            double Rs, double a[3], double& b, bool& present) {
+    fov_cbf_row(kind, e, tx, ty, fov_border(fov), Ds, Rs, a, b, present);
 }
 
 // Voronoi row of the FoV controller: separating_hyperplanes::voronoi of the planar positions

@@ -61,7 +61,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     if (ai >= args.num_agents) return;
     stamp(args, ai, lane, 0);
     const double* zero_row = nullptr;
-    double kconst;
     FovSlackLds* slk = nullptr;
     if constexpr (SLACK) {
         __shared__ FovSlackLds slk_mem;
@@ -79,6 +78,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     for (int k = 0; k < 6; k++) s0[k] = args.states[(size_t)self * 6 + k];
     __shared__ double ykeep_s[WNZ], q_s[WNZ];  // wave-uniform vectors kept out of the registers
     __shared__ double ypd[WNZ];                // slack mode: the slack PDIP's point during its polish
+    __shared__ double kconst_s;                // the objective's constant (read once per IMPC iteration)
     {
         double q15[NZ], kconst0;
         agent_linear_term<NZ>(op, buf, args, ai, s0, q15, kconst0);
@@ -90,25 +90,30 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             }
             q_s[WNZ - 1] = 0.0;
             ykeep_s[WNZ - 1] = 0.0;
+            kconst_s = kconst0;
         }
-        kconst = kconst0;
     }
 
     // ---- shared box rows into the image (rows 0 .. mb-1), bounds shifted by Gs s0
     const int mb = op.m;
     {
         const double* W = opp(buf, op.o_Wbox);
-        for (int r = lane; r < mb; r += 64) {
-            const double* src = W + (size_t)r * WBOX_ROW;
-            double sh = 0.0;
+        // (unrolled over the image's row slots: every slot's loads go out together)
 #pragma unroll
-            for (int k = 0; k < 6; k++) sh = fma(src[WNZ + k], s0[k], sh);
+        for (int sl = 0; sl < WR; sl++) {
+            const int r = lane + 64 * sl;
+            if (r < mb) {
+                const double* src = W + (size_t)r * WBOX_ROW;
+                double sh = 0.0;
 #pragma unroll
-            for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = src[j];
-            rlo[r] = src[WNZ + 6] - sh;
-            rhi[r] = src[WNZ + 7] - sh;
-            rml[r] = 1.0;
-            was.wn[r] = (float)opp(buf, op.o_wbox)[r];  // (constant rows: the host's weights)
+                for (int k = 0; k < 6; k++) sh = fma(src[WNZ + k], s0[k], sh);
+#pragma unroll
+                for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = src[j];
+                rlo[r] = src[WNZ + 6] - sh;
+                rhi[r] = src[WNZ + 7] - sh;
+                rml[r] = 1.0;
+                was.wn[r] = (float)opp(buf, op.o_wbox)[r];  // (constant rows: the host's weights)
+            }
         }
     }
     if (lane < WNZ) Gimg[WROWS * WNZ + lane] = 0.0;
@@ -158,6 +163,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
     const int C = op.C;
+    const FovBorder fborder = fov_border(op.fov_beta);  // (once per agent, not per row)
 
     for (int it = 0; it < op.impc_iter; it++) {
         // (keeps the operator tables' loads inside the iteration: hoisted out of it they stay live
@@ -168,9 +174,10 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             write_iteration(args, oi, lane, ST_UNKNOWN, __builtin_nan(""), 0);
             continue;
         }
-        // ---- Voronoi rows: rows mb .. mb + nnb*C - 1 (same in every iteration)
+        // ---- Voronoi rows: rows mb .. mb + nnb*C - 1, the same in every iteration: formed in
+        // iteration 0 and kept in the image (the solves never write rows below the FoV rows)
         const int nvor = nnb * C;
-        for (int v = lane; v < nvor; v += 64) {
+        for (int v = lane; v < nvor && it == 0; v += 64) {
             const int i = v / C, j = v % C;
             double ox, oy, nx, ny, off;
             nb_position(args, nb_scratch, grid_mode, nb0, i, ox, oy);
@@ -223,7 +230,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
                 cbf_ego_state<NZ>(op, buf, it, k, s0, yk, e);
                 bool present;
-                fov_cbf_row(kind, e, npx, npy, op.fov_beta, op.fov_Ds, op.fov_Rs, a, bb, present);
+                fov_cbf_row(kind, e, npx, npy, fborder, op.fov_Ds, op.fov_Rs, a, bb, present);
                 double bmax = 0.0, bmin = 0.0;
 #pragma unroll
                 for (int d = 0; d < 3; d++) {
@@ -588,13 +595,13 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         }
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {
-            double yk[NZ], q15[NZ];
+            // 1/2 y^T P y + q^T y + k on the row layout: (P y)_i from P's row in LDS (lane i)
+            const int i16 = lane & 15;
+            double pyi = 0.0;
 #pragma unroll
-            for (int j = 0; j < NZ; j++) {
-                yk[j] = sc.y[j];
-                q15[j] = q_s[j];
-            }
-            objv = reduced_objective<NZ>(op, buf, q15, yk, kconst) + vobj;
+            for (int j = 0; j < WNZ; j++) pyi = fma(was.P[i16 * 17 + j], sc.y[j], pyi);
+            const double term = i16 < NZ ? sc.y[i16] * fma(0.5, pyi, q_s[i16]) : 0.0;
+            objv = grp_sum<16>(term) + kconst_s + vobj;
             wave_lds_sync();
             if (lane < NZ) ykeep_s[lane] = sc.y[lane];
             have_curve = true;
