@@ -79,9 +79,18 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     __shared__ double ykeep_s[WNZ], q_s[WNZ];  // wave-uniform vectors kept out of the registers
     __shared__ double ypd[WNZ];                // slack mode: the slack PDIP's point during its polish
     __shared__ double kconst_s;                // the objective's constant (read once per IMPC iteration)
+    __shared__ double ego_s[2][8];             // IMPC iteration >= 1: the ego state at each CBF sample
+    // non-finite QP data (a NaN / Inf state, target or neighbour position), checked where the rows
+    // are formed (v * 0 is NaN for a non-finite v): the rows that persist across the IMPC
+    // iterations (q, box-row bounds, Voronoi rows) and each iteration's FoV rows
+    bool nfin_fixed = false;
     {
         double q15[NZ], kconst0;
         agent_linear_term<NZ>(op, buf, args, ai, s0, q15, kconst0);
+        double chk = kconst0 * 0.0;
+#pragma unroll
+        for (int j = 0; j < NZ; j++) chk = fma(q15[j], 0.0, chk);
+        nfin_fixed = !(chk == 0.0);
         if (lane == 0) {
 #pragma unroll
             for (int j = 0; j < NZ; j++) {
@@ -111,6 +120,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = src[j];
                 rlo[r] = src[WNZ + 6] - sh;
                 rhi[r] = src[WNZ + 7] - sh;
+                nfin_fixed = nfin_fixed || !(sh * 0.0 == 0.0);  // (the rows themselves: host constants)
                 rml[r] = 1.0;
                 was.wn[r] = (float)opp(buf, op.o_wbox)[r];  // (constant rows: the host's weights)
             }
@@ -194,6 +204,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             rlo[r] = 0.0;
             rml[r] = 0.0;
             rhi[r] = -off - 1e-8 - sh;
+            nfin_fixed = nfin_fixed || !(fma(nx, 0.0, ny * 0.0) + (off + sh) * 0.0 == 0.0);
             const double* M = opp(buf, op.o_wvor) + 3 * j;  // g P^-1 g = (nx, ny) M (nx, ny)^T
             was.wn[r] = rsqrtf((float)fmax(fma(nx, fma(M[0], nx, 2.0 * M[1] * ny), M[2] * ny * ny), 1e-30));
         }
@@ -205,6 +216,23 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         const double* UZ = opp(buf, op.o_UZ);
         const double* US = opp(buf, op.o_US);
         const int ntask = nnb * 4 * nk;
+        if (it > 0) {
+            // the ego state at each CBF sample (the previous curve at h_samples(k)), once per sample:
+            // lane 6 k + s forms component s of sample k (ConnectivityIMPCCBF.cpp:161-168)
+            if (lane < 6 * nk && nk <= 2) {
+                const int k = lane / 6, c = lane - 6 * k;
+                const double* PZ = opp(buf, op.o_PZ) + (size_t)k * 6 * NZ + c * NZ;
+                const double* PS = opp(buf, op.o_PS) + (size_t)k * 36 + c * 6;
+                double v = 0.0;
+#pragma unroll
+                for (int u = 0; u < 6; u++) v = fma(PS[u], s0[u], v);
+#pragma unroll
+                for (int j = 0; j < NZ; j++) v = fma(PZ[j], ykeep_s[j], v);
+                ego_s[k][c] = v;
+            }
+            wave_lds_sync();
+        }
+        bool nfin_it = false;
         if constexpr (SLACK) {
             // slack mode: neighbour i's rows go to lanes 8 i .. 8 i + 7 of the slack images
             // (WaveSlack), uncompacted; every row starts inert, pads stay zero
@@ -224,11 +252,17 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 i = task / (4 * nk);
                 kind = (task / nk) % 4;
                 k = task % nk;
-                double e[6], yk[NZ], npx, npy;
+                double e[6], npx, npy;
                 nb_position(args, nb_scratch, grid_mode, nb0, i, npx, npy);
+                if (it == 0 || nk > 2) {
+                    double yk[NZ];
 #pragma unroll
-                for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
-                cbf_ego_state<NZ>(op, buf, it, k, s0, yk, e);
+                    for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
+                    cbf_ego_state<NZ>(op, buf, it, k, s0, yk, e);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 6; c++) e[c] = ego_s[k][c];
+                }
                 bool present;
                 fov_cbf_row(kind, e, npx, npy, fborder, op.fov_Ds, op.fov_Rs, a, bb, present);
                 double bmax = 0.0, bmin = 0.0;
@@ -272,7 +306,9 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 Gimg[r * WNZ + NZ] = 0.0;
                 rlo[r] = 0.0;
                 rml[r] = 0.0;
-                rhi[r] = bb + a[0] * us[0] + a[1] * us[1] + a[2] * us[2];
+                const double hr = bb + a[0] * us[0] + a[1] * us[1] + a[2] * us[2];
+                rhi[r] = hr;
+                nfin_it = nfin_it || !(fma(a[0], 0.0, fma(a[1], 0.0, a[2] * 0.0)) + hr * 0.0 == 0.0);
                 const double* M = opp(buf, op.o_wfov) + 6 * k;  // g P^-1 g = a^T M_k a
                 const double n2 = a[0] * (M[0] * a[0] + 2.0 * (M[1] * a[1] + M[2] * a[2])) +
                                   a[1] * (M[3] * a[1] + 2.0 * M[4] * a[2]) + a[2] * M[5] * a[2];
@@ -303,11 +339,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         double prs = __builtin_nan(""), drs = __builtin_nan("");
         double vobj = 0.0;  // slack mode: sum_i w_i v_i (addSlackCost, MPCCBFQPGeneratorBase.cpp:121-130)
         // non-finite data (a NaN / Inf state, target or neighbour position): not solved, ERROR
-        bool nfin = lane < WNZ && !isfinite(sc.q[lane]);
-        for (int r = lane; r < mtot && r < WROWS; r += 64) {
-            nfin = nfin || !isfinite(rlo[r]) || !isfinite(rhi[r]);
-            for (int j = 0; j < WNZ; j++) nfin = nfin || !isfinite(Gimg[r * WNZ + j]);
-        }
+        bool nfin = nfin_fixed || nfin_it;
         if constexpr (SLACK) {  // the slack rows (lane = row) and the neighbours' slack weights
             if (slk->live[lane] != 0.0) {
                 nfin = nfin || !isfinite(slk->h[lane]);
