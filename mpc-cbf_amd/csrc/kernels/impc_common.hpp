@@ -580,20 +580,32 @@ __device__ __forceinline__ double normal_sample(uint64_t seed, int64_t step, int
 // lower_bound piece lookup, local parameter min(T, t - cum[i-1]); Bezier::eval with the
 // monomial Bernstein basis). The control points come from xrow (stored curve) or, when xrow is
 // null, from x = Xs s0 + Z y of this step's solution.
-template <int NZ>
+// CC > 0: the control points per piece as a compile-time constant (op.C == CC; every loop unrolls,
+// so the piece's operator rows are loaded together instead of one dependent round trip per
+// control point); CC = 0: op.C at run time. The piece index counts the cumulative parameters below
+// t (branch-free over at most 8 pieces, else the loop).
+template <int NZ, int CC = 0>
 __device__ double curve_component(const DevOps& op, const double* buf, const double* xrow,
                                   const double (&s0)[6], const double (&yk)[NZ], double t, int comp) {
     const double* cum = opp(buf, op.o_cum);
     int piece = 0;
-    while (piece < op.P - 1 && cum[piece] < t) piece++;
+    if (op.P <= 8) {
+#pragma unroll
+        for (int p = 0; p < 7; p++) {
+            const double c = cum[p < op.P - 1 ? p : 0];
+            piece += (p < op.P - 1 && c < t) ? 1 : 0;
+        }
+    } else {
+        while (piece < op.P - 1 && cum[piece] < t) piece++;
+    }
     const double par = piece == 0 ? t : fmin(cum[0], t - cum[piece - 1]);
     const int d = comp % 3;
     const double* EB = opp(buf, comp < 3 ? op.o_EB0 : op.o_EB1);
     const double* Z = opp(buf, op.o_Z);
     const double* Xs = opp(buf, op.o_Xs);
-    const int C = op.C;
+    const int C = CC > 0 ? CC : op.C;
     double v = 0.0;
-    for (int cp = 0; cp < C; cp++) {
+    for (int cp = 0; cp < C; cp++) {  // (constant trip count when CC > 0: unrolled)
         const int idx = piece * 3 * C + d * C + cp;
         double xv;
         if (xrow) {
@@ -612,12 +624,23 @@ __device__ double curve_component(const DevOps& op, const double* buf, const dou
     return v;
 }
 
+template <int NZ, bool FIXED = true>
+__device__ __forceinline__ double curve_component_any(const DevOps& op, const double* buf, const double* xrow,
+                                                      const double (&s0)[6], const double (&yk)[NZ], double t,
+                                                      int comp) {
+    if constexpr (FIXED)
+        if (op.C == 4) return curve_component<NZ, 4>(op, buf, xrow, s0, yk, t, comp);
+    return curve_component<NZ, 0>(op, buf, xrow, s0, yk, t, comp);
+}
+
 // Control points of the kept curve and the closed-loop next state.
 //   default: x = this step's curve (NaN if none), next state = that curve at t = h, or the
 //            current state when optimize() produced no curve;
 //   args.traj_t set (closed-loop simulator, MPCCBFFormationControl_example.cpp:150-221): x is
 //            the persistent last successful curve, next state = it at the advanced time.
-template <int NZ, int G>
+// FIXED: the curve evaluation's compile-time control-point count (C = 4) when it applies (off for the
+// FoV slack kernel, whose registers it pushes into scratch)
+template <int NZ, int G, bool FIXED = true>
 __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const double* buf,
                                                     const ImpcArgs& args, int ai, int gl,
                                                     const double (&s0)[6], const double (&yk)[NZ],
@@ -650,10 +673,10 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
         if (have_curve || t_prev >= 0.0) {
             t_new = fmin(t_prev + op.eval_step, tmax);  // example :190-193
             const double* xr = have_curve ? nullptr : args.x + (size_t)ai * op.n;
-            v = curve_component<NZ>(op, buf, xr, s0, yk, t_new, gl);
+            v = curve_component_any<NZ, FIXED>(op, buf, xr, s0, yk, t_new, gl);
             if (args.substeps) {  // sub-steps 1 .. nsub - 1: the curve at t_prev + Ts k, own draws
                 for (int k = 1; k < op.nsub; k++) {
-                    double u = curve_component<NZ>(op, buf, xr, s0, yk, fmin(t_prev + op.Ts * k, tmax), gl);
+                    double u = curve_component_any<NZ, FIXED>(op, buf, xr, s0, yk, fmin(t_prev + op.Ts * k, tmax), gl);
                     if (sd > 0.0) u = fma(sd, normal_sample(args.noise_seed, args.step_index, agent, gl, op.nsub - k), u);
                     args.substeps[((size_t)ai * op.nsub + k - 1) * 6 + gl] = u;
                 }

@@ -105,4 +105,8 @@ def test_fov_closed_loop_is_deterministic(mpclib, slack):
     for s in range(steps):
         for a, b, name in zip(runs[0][s], runs[1][s], ("status", "iters", "obj", "next_states")):
             same = torch.equal(a, b) if name != "obj" else bool(torch.all((a == b) | (torch.isnan(a) & torch.isnan(b))))
-            assert same, (s, name, torch.nonzero(a != b)[:4].tolist())
+            if not same:
+                idx = torch.nonzero(a != b)[:4].tolist()
+                vals = [(i, a[tuple(i)].item(), b[tuple(i)].item(),
+                         [runs[r][s][0][i[0]].tolist() for r in (0, 1)]) for i in idx]
+            assert same, (s, name, vals if not same else None)

@@ -7,7 +7,8 @@
 #   FP64 instruction mix, and the FoV kernels' FP64 MFMA counters.
 # Order: PMC passes first (their summary goes to profiles/<tag>_pmc_summary.json, which the bench
 # lines read), then the bench lines and kernel traces, then the GPU tests and the stamp profile.
-# Usage: bash tools/profile_round.sh <tag> [nopmc|pmc]   (pmc: the PMC passes only; nopmc: the rest)
+# Usage: bash tools/profile_round.sh <tag> [nopmc|pmc|bench|prof]   (pmc: the PMC passes only;
+# nopmc: the rest; bench: the bench lines only; prof: the kernel traces, GPU tests and stamps only)
 set -e -o pipefail
 TAG=${1:-rNN}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -16,7 +17,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 B="python3 $ROOT/bench.py"
 step() { echo "[$(date +%T)] $*"; }
-[ "$2" = "nopmc" ] || {
+[ "$2" = "nopmc" ] || [ "$2" = "bench" ] || [ "$2" = "prof" ] || {
 pmc() {  # dir, bench args..., -- counters
   local d=$1; shift
   local args=()
@@ -46,6 +47,7 @@ python3 $ROOT/tools/pmc_summary.py $OUT/${TAG}_pmc > $ROOT/profiles/${TAG}_pmc_s
 cp $ROOT/profiles/${TAG}_pmc_summary.json $OUT/${TAG}_pmc_summary.json
 }
 [ "$2" = "pmc" ] && { step done; exit 0; }
+[ "$2" = "prof" ] || {
 step bench driver; timeout -k 10 200 $B --steps 20 --warmup 5 > $OUT/${TAG}_bench_driver.json 2> $OUT/${TAG}_bench_driver.err
 step bench 1000; timeout -k 10 300 $B > $OUT/${TAG}_bench_collision.json 2> $OUT/${TAG}_bench_collision.err
 step bench 8192; timeout -k 10 300 $B --agents-per-gpu 8192 --no-cpu-baseline > $OUT/${TAG}_bench_8192.json 2> $OUT/${TAG}_bench_8192.err
@@ -55,6 +57,9 @@ step bench all256; timeout -k 10 300 $B --neighbours all --agents-per-gpu 256 --
 step bench all256 slack; timeout -k 10 300 $B --neighbours all --agents-per-gpu 256 --crowded --slack --steps 200 --warmup 20 > $OUT/${TAG}_bench_all256_slack.json 2> $OUT/${TAG}_bench_all256_slack.err
 step bench fov; timeout -k 10 300 $B --workload fov > $OUT/${TAG}_bench_fov.json 2> $OUT/${TAG}_bench_fov.err
 step bench fov slack; timeout -k 10 300 $B --workload fov --slack > $OUT/${TAG}_bench_fov_slack.json 2> $OUT/${TAG}_bench_fov_slack.err
+step bench dense; timeout -k 10 300 $B --workload dense --steps 10 --warmup 2 > $OUT/${TAG}_bench_dense.json 2> $OUT/${TAG}_bench_dense.err
+}
+[ "$2" = "bench" ] && { step done; exit 0; }
 prof() {  # name, bench args
   step prof $1
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_prof_$1 -o run \
@@ -68,11 +73,12 @@ prof crowded --crowded --steps 300 --warmup 20
 prof all256 --neighbours all --agents-per-gpu 256 --crowded --steps 200 --warmup 20 --no-trace
 prof fov --workload fov
 prof fov_slack --workload fov --slack
-step bench dense; timeout -k 10 300 $B --workload dense --steps 10 --warmup 2 > $OUT/${TAG}_bench_dense.json 2> $OUT/${TAG}_bench_dense.err
 prof dense --workload dense --steps 10 --warmup 2
 step pytest; (cd $ROOT && timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/${TAG}_pytest_gpu.log 2>&1)
 step fovs status; MPCCBF_CHECK_SLACK=1 timeout -k 10 300 python3 $ROOT/tools/fov_status_check.py 1000 $OUT/${TAG}_fovs_status.npz > $OUT/${TAG}_fovs_status.log 2>&1
 step stamps; (cd $ROOT && timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1)
 step stamps pdip; (cd $ROOT && MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision_das.log 2>&1)
 step stamps fov; (cd $ROOT && WORKLOAD=fov timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov.log 2>&1)
+step stamps fov das; (cd $ROOT && WORKLOAD=fov MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov_das.log 2>&1)
+step determinism; (cd $ROOT && timeout -k 10 200 python3 tools/determinism_loop.py 6 1 30 > $OUT/${TAG}_determinism_fovs.log 2>&1)
 echo done
