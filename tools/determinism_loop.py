@@ -20,6 +20,17 @@ R = int(sys.argv[1]) if len(sys.argv) > 1 else 6
 # PERTURB=1: before each repetition, a few steps of other IMPC kernels (collision, FoV without
 # slack) run, so each repetition starts from different register / LDS contents left on the CUs
 PERTURB = os.environ.get("PERTURB", "0") == "1"
+# REGFILL=1: before every step, tools/regfill.hip writes a per-repetition pattern into every VGPR and
+# AGPR of the chip, so a kernel reading a register it never wrote sees different values per
+# repetition (build: hipcc --offload-arch=gfx950 -O2 -shared -fPIC tools/regfill.hip -o
+# tools/build/libregfill.so)
+REGFILL = os.environ.get("REGFILL", "0") == "1"
+PATTERNS = (0x00000000, 0x7ff80000, 0x3ff00000, 0x40590000, 0xFFFFFFFF, 0x00000001)
+_rf = None
+if REGFILL:
+    import ctypes
+    _rf = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "build", "libregfill.so"))
+    _rf.regfill_launch.argtypes = [ctypes.c_uint, ctypes.c_int]
 SLACK = (sys.argv[2] != "0") if len(sys.argv) > 2 else True
 STEPS = int(sys.argv[3]) if len(sys.argv) > 3 else 30
 n = 512
@@ -59,6 +70,9 @@ for rep in range(R):
     tg = torch.tensor(targets, device=dev)
     log = {k: [] for k in ("status", "iters", "obj", "next_states")}
     for s in range(STEPS):
+        if _rf is not None:
+            torch.cuda.synchronize()
+            assert _rf.regfill_launch(PATTERNS[rep % len(PATTERNS)], 8192) == 0
         ctx.impc_solve(cur, targets=tg, knn_k=8, knn_radius=cfg["fov_Rs"], cov=cov, traj_t=traj_t, step_index=s,
                        pos_std=0.001, vel_std=0.01, noise_seed=20251015, **out)
         for k in log:
