@@ -6,8 +6,10 @@ xGMI when --gpus > 1), neighbour lists, two dependent QP solves per agent (fused
 the closed-loop state update. value = QPs solved by all ranks / wall time.
 
 Default workload (N=1): BASELINE config 3 — 4096 agents, horizon 15, pairwise collision CBF,
-8 nearest neighbours within 3 d_min, base_config.json parameters. Multi-GPU: weak scaling,
-4096 agents per GPU (config 4's 8192 agents at --gpus 2; --agents-total 8192 pins config 4).
+8 nearest neighbours within 3 d_min, base_config.json parameters. Multi-GPU (N > 1): BASELINE
+config 4 — 8192 agents in total sharded over the N GPUs (1024 per GPU at N = 8), strong scaling;
+--weak keeps 4096 agents per GPU instead. FoV (--workload fov): config 5's 512-agent per-GPU
+share at N = 1, its 4096 agents in total at N > 1.
 
     python bench.py [--gpus N --steps K --warmup W]      (N > 1: relaunches itself as N ranks)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -47,7 +49,11 @@ def parse():
                          "qpcpp::Solver path (mpccbf_qp_solve_dense_batch) on the golden QPs")
     ap.add_argument("--agents-per-gpu", type=int, default=0,
                     help="default 4096 (collision), 512 (fov: config 5 = 4096 agents on 8 GPUs)")
-    ap.add_argument("--agents-total", type=int, default=0, help="strong scaling: fixed total")
+    ap.add_argument("--agents-total", type=int, default=0,
+                    help="strong scaling: fixed total (default at --gpus > 1: 8192 collision = config 4, "
+                         "4096 fov = config 5)")
+    ap.add_argument("--weak", action="store_true",
+                    help="--gpus > 1: weak scaling, --agents-per-gpu agents on every GPU")
     ap.add_argument("--rank-share", type=int, default=0,
                     help="one GPU times rank 0's share of an N-rank run: agents-total / N agents of "
                          "the agents-total table, the other rows carried over and inserted into the "
@@ -220,6 +226,9 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     fov = args.workload == "fov"
+    if world > 1 and not args.weak and args.agents_total <= 0 and args.agents_per_gpu <= 0:
+        # BASELINE config 4 (8192 agents sharded over the node's GPUs) / config 5 (4096 FoV agents)
+        args.agents_total = 4096 if fov else 8192
     if args.agents_per_gpu <= 0:
         args.agents_per_gpu = 512 if fov else 4096
     if args.k_hor <= 0:
@@ -476,7 +485,9 @@ def main():
                     (f"config5: {total} agents ({per}/GPU), FoV 120 deg + Voronoi CBF, horizon "
                      f"{cfg['k_hor']}, 4 Bezier pieces, {args.knn} nearest observed within {radius:g} m"
                      if fov else
-                     f"config3{' crowded (0.6 x spacing)' if args.crowded else ''}: {total} agents, horizon "
+                     f"{'config4' if (world > 1 and total == 8192) else 'config3'}"
+                     f"{' crowded (0.6 x spacing)' if args.crowded else ''}: {total} agents"
+                     f"{f' sharded {world}xMI355X' if world > 1 else ''}, horizon "
                      f"{cfg['k_hor']}, pairwise collision CBF, "
                      + (f"every other robot as a neighbour ({total - 1}, fixed CSR lists)" if args.neighbours == "all"
                         else f"knn{args.knn} r={radius:g}m ({args.neighbours})"))

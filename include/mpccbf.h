@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 9
+#define MPCCBF_ABI_VERSION 10
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -96,13 +96,20 @@ typedef struct mpccbf_options {
     int32_t max_pdip_iters;    /* default 60 */
     double tolerance;          /* PDIP relative tolerance, default 1e-9 */
     /* Interior-point warm start of IMPC iteration 1 — used only when the dual active-set solve
-     * is off (environment MPCCBF_DUAL_AS=0; by default the active set solves first, IMPC
-     * iteration 1 starting from iteration 0's active box sides, and the PDIP runs cold):
+     * is off (dual_as_steps < 0; by default the active set solves first and the PDIP runs cold):
      * iteration 0's primal-dual point, slacks and duals floored at warm_delta: 0 = default
      * (0.3), < 0 = cold start. A warm start that does not converge is certified by phase 1 and,
-     * when the QP is feasible, re-solved cold, so statuses do not depend on it. Environment
-     * variable MPCCBF_WARM_DELTA (read here, a number) overrides it for tuning. */
+     * when the QP is feasible, re-solved cold, so statuses do not depend on it. */
     double warm_delta;
+    /* Solver pipeline (ABI 10). Zero selects the default; these are the only inputs that change
+     * the solver's path (no environment variable does, except in the diagnostics build). */
+    int32_t dual_as_steps;     /* dual active-set step limit per QP: 0 = 24, < 0 = off (the PDIP alone) */
+    int32_t no_fast_start;     /* 1: no unconstrained-minimiser fast start in the PDIP path */
+    int32_t early_it;          /* PDIP divergence test from this iteration on: 0 = 10, < 0 = off */
+    int32_t das_warm_steps;    /* IMPC iteration 1 starts the active set from iteration 0's when that
+                                  took at least this many steps: 0 = 3, < 0 = never */
+    int32_t lean;              /* 1: lean main launch (fast start + active set; the rest deferred to
+                                  the fallback launch). Collision controller only */
 } mpccbf_options;
 
 /* Validates p like parsing.hpp:37-135,182-214, builds the parameter-only operators on the host
@@ -158,7 +165,11 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *               curve was found.
  *   stamps      diagnostics, normally NULL: num_agents x 8 int64 shader-clock stamps (s_memtime)
  *               at the kernel's phase boundaries (start, setup, neighbours, CBF rows 0, solve 0,
- *               CBF rows 1, solve 1, end). */
+ *               CBF rows 1, solve 1, end).
+ *   nb_out      diagnostics, normally NULL (ABI 10): num_agents x 16 int32, the neighbour list each
+ *               agent's QPs were built from, in the kernel's order (grid mode: the in-kernel query's
+ *               k nearest, sorted by index; CSR: the given list), -1 after the last; lists longer
+ *               than 16 are truncated here (not in the solve). */
 typedef struct mpccbf_batch {
     int32_t num_states;
     const double* states;
@@ -205,6 +216,7 @@ typedef struct mpccbf_batch {
      * noise, or, with no curve yet, the held position with the noise accumulated over the
      * sub-steps and a zero velocity plus noise. The last record is the next state. NULL: none. */
     double* substeps;
+    int32_t* nb_out;          /* out, num_agents x 16, or NULL (see above) */
 } mpccbf_batch;
 
 int mpccbf_impc_solve(mpccbf_ctx* ctx, const mpccbf_batch* batch, void* hip_stream);

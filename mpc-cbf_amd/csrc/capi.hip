@@ -178,6 +178,7 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.primal_res = b->primal_res;
     a.dual_res = b->dual_res;
     a.substeps = b->substeps;
+    a.nb_out = b->nb_out;
     if (b->substeps && !b->traj_t)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "substeps (closed-loop records) needs traj_t");
     // fallback launch: agents the main launch defers (the lean launch: QPs that need the PDIP or
@@ -426,21 +427,17 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     d.cbf_filter = c->opt.no_cbf_filter ? 0 : 1;
     d.maxit = c->opt.max_pdip_iters > 0 ? c->opt.max_pdip_iters : 60;
     d.tol = c->opt.tolerance > 0 ? c->opt.tolerance : 1e-9;
-    d.warm_delta = c->opt.warm_delta == 0.0 ? 0.3 : (c->opt.warm_delta > 0.0 ? c->opt.warm_delta : 0.0);
-    if (const char* w = getenv("MPCCBF_WARM_DELTA")) {  // tuning override of the IMPC warm start
-        char* end = nullptr;
-        const double v = std::strtod(w, &end);
-        if (end == w || *end != '\0' || !std::isfinite(v)) {
-            delete c;
-            return fail(MPCCBF_ERR_INVALID_ARGUMENT, std::string("MPCCBF_WARM_DELTA is not a number: ") + w);
-        }
-        d.warm_delta = v > 0.0 ? v : 0.0;
-    }
+    // solver pipeline: from mpccbf_options only (zero = default)
+    const mpccbf_options& so = c->opt;
+    d.warm_delta = so.warm_delta == 0.0 ? 0.3 : (so.warm_delta > 0.0 ? so.warm_delta : 0.0);
     d.feas_tol = 1e-6;  // CPLEX default feasibility tolerance
-    d.early_it = 10;
-    d.fast_start = 1;
-    d.dual_as = 24;
-    {  // tuning overrides (diagnostics)
+    d.early_it = so.early_it == 0 ? 10 : (so.early_it > 0 ? so.early_it : 0);
+    d.fast_start = so.no_fast_start ? 0 : 1;
+    d.dual_as = so.dual_as_steps == 0 ? 24 : (so.dual_as_steps > 0 ? so.dual_as_steps : 0);
+    d.lean = so.lean ? 1 : 0;  // measured no faster at occupancy 1
+    d.das_warm = so.das_warm_steps == 0 ? 3 : (so.das_warm_steps > 0 ? so.das_warm_steps : 0);
+#ifdef MPCCBF_DIAG_ENV
+    {  // diagnostics build only (make diag): tuning overrides from the environment
         const char* e = getenv("MPCCBF_EARLY_IT");
         if (e) d.early_it = atoi(e);
         const char* f = getenv("MPCCBF_FAST_START");
@@ -448,10 +445,13 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
         const char* g = getenv("MPCCBF_DUAL_AS");
         if (g) d.dual_as = atoi(g);
         const char* l = getenv("MPCCBF_LEAN");
-        d.lean = l ? atoi(l) : 0;  // measured no faster at occupancy 1
+        if (l) d.lean = atoi(l);
         const char* w = getenv("MPCCBF_DAS_WARM");
-        d.das_warm = w ? atoi(w) : 3;  // iteration-0 steps that enable the warm start (0: never)
+        if (w) d.das_warm = atoi(w);
+        const char* wd = getenv("MPCCBF_WARM_DELTA");
+        if (wd) d.warm_delta = std::max(0.0, std::strtod(wd, nullptr));
     }
+#endif
     c->variant = 0;
     hipError_t e = hipSetDevice(c->device);
     if (e == hipSuccess) e = hipMalloc(&c->dbuf, v.size() * sizeof(double));

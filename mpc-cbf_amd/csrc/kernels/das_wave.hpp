@@ -267,7 +267,13 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
                 for (int a = 0; a < WNZ - 1; a++) {
                     if (a < kk) {
                         const double ra_ = bcast16v(a, rhoi);
-                        zi = fma(a < k ? -ra_ : 0.0, ws.W[(a < k ? a : 0) * WNZ + i], zi);
+                        // (a select, not a product with 0: rows a >= k of ws.W were never written in
+                        // this block — LDS left by an earlier kernel, NaN / Inf included, and
+                        // 0 * NaN is NaN. The slack patterns' unbounded loops (kk = 16) read them
+                        // on every step from an empty active set: that was the FoV-slack step-0
+                        // nondeterminism of round 3)
+                        const double wa = ws.W[(a < k ? a : 0) * WNZ + i];
+                        zi = a < k ? fma(-ra_, wa, zi) : zi;
                     }
                 }
                 yi = fma(-t, zi, yi);
@@ -347,7 +353,8 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         for (int a = 0; a < WNZ - 1; a++) {
             if (a < kk) {
                 const double la = bcast16v(a, lsi);
-                r = fma(a < k ? la : 0.0, Gs[(a < k ? ws.row[a] : 0) * WNZ + i], r);
+                const double ga = Gs[(a < k ? ws.row[a] : 0) * WNZ + i];
+                r = a < k ? fma(la, ga, r) : r;  // (a select: see the direction above)
             }
         }
         double qn = fabs(sc.q[i]);

@@ -134,12 +134,17 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // Diagnostics build (make poison): every kernel that calls this fills its block's static LDS with
-// MPCCBF_LDS_POISON before any other work, so two builds with different fill values give
+// MPCCBF_LDS_POISON (NaN with MPCCBF_LDS_POISON_NAN) before any other work, so builds with
+// different fill values give
 // bit-identical results unless something reads LDS it never wrote (tools/lds_poison_check.py).
 __device__ __forceinline__ void lds_poison() {
 #ifdef MPCCBF_LDS_POISON
     const unsigned n = __builtin_amdgcn_groupstaticsize() / 8;
+#ifdef MPCCBF_LDS_POISON_NAN  // a quiet NaN: also exposes unwritten LDS that is multiplied by 0
+    const double v = __builtin_nan("");
+#else
     const double v = MPCCBF_LDS_POISON;
+#endif
     for (unsigned e = threadIdx.x; e < n; e += blockDim.x) {
         const unsigned addr = e * 8;
         asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");

@@ -149,6 +149,8 @@ struct ImpcArgs {
     // closed-loop simulator: the state after every control sub-step (num_agents x nsub x 6), the
     // records the example writes to states.json, or nullptr
     double* substeps;
+    // diagnostics: num_agents x 16 neighbour ids as the kernel uses them (-1 padded), or nullptr
+    int32_t* nb_out;
 };
 
 constexpr int NSTAMP = 8;

@@ -739,6 +739,15 @@ __device__ __forceinline__ void stamp(const ImpcArgs& args, int ai, int gl, int 
     }
 }
 
+// diagnostics (args.nb_out): the first 16 entries of the agent's neighbour list as the kernel built
+// its rows from (grid mode: the query's result in LDS, sorted by index; CSR: the caller's list)
+__device__ __forceinline__ void write_nb_out(const ImpcArgs& args, int ai, int gl, bool grid_mode,
+                                             const NbScratch& nbs, int nb0, int nnb) {
+    if (!args.nb_out || gl >= 16) return;
+    const int v = gl < nnb ? (grid_mode ? nbs.idx[gl] : args.nb_col[nb0 + gl]) : -1;
+    args.nb_out[(size_t)ai * 16 + gl] = v;
+}
+
 __device__ __forceinline__ void write_iteration(const ImpcArgs& args, size_t oi, int gl, int st,
                                                 double obj, int iters,
                                                 double prs = __builtin_nan(""), double drs = __builtin_nan("")) {

@@ -140,6 +140,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     } else {
         nnb = grid_neighbors<64>(args, self, s0[0], s0[1], nb_scratch, lane, s0[2]);
     }
+    write_nb_out(args, ai, lane, grid_mode, nb_scratch, nb0, nnb);
     const bool nb_overflow = nnb < 0 || nnb > (SLACK ? WSL_NB : FOV_NB_CAP);
     if (nb_overflow) nnb = 0;
     if constexpr (SLACK) {

@@ -413,6 +413,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     } else {
         nnb = grid_neighbors<G>(args, self, s0[0], s0[1], nbs, gl);
     }
+    write_nb_out(args, ai, gl, grid_mode, nbs, nb0, nnb);
     if (SLACK && !QUEUE && nnb > G && args.defer) {  // slack mode: beyond one lane per neighbour
         defer_agent(args, ai, gl);
         return;

@@ -65,7 +65,9 @@ class Params(C.Structure):
 class Options(C.Structure):
     _fields_ = [("device", C.c_int32), ("keep_redundant", C.c_int32),
                 ("no_cbf_filter", C.c_int32), ("max_pdip_iters", C.c_int32),
-                ("tolerance", C.c_double), ("warm_delta", C.c_double)]
+                ("tolerance", C.c_double), ("warm_delta", C.c_double),
+                ("dual_as_steps", C.c_int32), ("no_fast_start", C.c_int32), ("early_it", C.c_int32),
+                ("das_warm_steps", C.c_int32), ("lean", C.c_int32)]
 
 
 class Batch(C.Structure):
@@ -78,7 +80,7 @@ class Batch(C.Structure):
         ("stamps", C.c_void_p), ("traj_t", C.c_void_p), ("pos_std", C.c_double),
         ("vel_std", C.c_double), ("noise_seed", C.c_uint64), ("step_index", C.c_int64),
         ("cov", C.c_void_p), ("primal_res", C.c_void_p), ("dual_res", C.c_void_p),
-        ("substeps", C.c_void_p),
+        ("substeps", C.c_void_p), ("nb_out", C.c_void_p),
     ]
 
 
@@ -178,14 +180,19 @@ class Context:
 
     def __init__(self, cfg: dict, device: int = 0, keep_redundant: bool = False,
                  no_cbf_filter: bool = False, max_iters: int = 0, tol: float = 0.0,
-                 warm_delta: float = 0.0):
-        """warm_delta: IMPC iteration-1 warm start floor (0 = default 0.3, < 0 = cold start)."""
+                 warm_delta: float = 0.0, dual_as_steps: int = 0, no_fast_start: bool = False,
+                 early_it: int = 0, das_warm_steps: int = 0, lean: bool = False):
+        """warm_delta: IMPC iteration-1 warm start floor (0 = default 0.3, < 0 = cold start);
+        dual_as_steps: active-set step limit (0 = default, < 0 = the PDIP alone); the other solver
+        options as mpccbf_options (include/mpccbf.h), 0 = default."""
         L = load()
         self.cfg = dict(cfg)
         self.params = Params.from_dict(cfg)
         o = Options(device=device, keep_redundant=int(keep_redundant),
                     no_cbf_filter=int(no_cbf_filter), max_pdip_iters=max_iters, tolerance=tol,
-                    warm_delta=warm_delta)
+                    warm_delta=warm_delta, dual_as_steps=int(dual_as_steps),
+                    no_fast_start=int(no_fast_start), early_it=int(early_it),
+                    das_warm_steps=int(das_warm_steps), lean=int(lean))
         h = C.c_void_p()
         _check(L.mpccbf_create(C.byref(self.params), C.byref(o), C.byref(h)))
         self._h = h
@@ -223,7 +230,7 @@ class Context:
                    agent_first=0, num_agents=None, x=None, status=None, obj=None, iters=None,
                    next_states=None, knn_k=0, knn_radius=0.0, stream=None, stamps=None,
                    traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0, cov=None,
-                   primal_res=None, dual_res=None, substeps=None):
+                   primal_res=None, dual_res=None, substeps=None, nb_out=None):
         """CSR neighbours (nb_row_ptr/nb_col) or, with both None, the knn_k nearest within
         knn_radius found on the device in the same launch sequence. traj_t (float64, one per
         agent, initialised to -1) turns on the closed-loop simulator semantics: x persists the
@@ -238,7 +245,7 @@ class Context:
                   stamps=_ptr(stamps), traj_t=_ptr(traj_t), pos_std=float(pos_std),
                   vel_std=float(vel_std), noise_seed=int(noise_seed), step_index=int(step_index),
                   cov=_ptr(cov), primal_res=_ptr(primal_res), dual_res=_ptr(dual_res),
-                  substeps=_ptr(substeps))
+                  substeps=_ptr(substeps), nb_out=_ptr(nb_out))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
 
     def run_steps(self, states, states_alt, num_steps, targets=None, refs=None, agent_first=0,

@@ -74,7 +74,13 @@ def test_fov_closed_loop_is_deterministic(mpclib, slack):
     """The FoV controller's closed loop (512 agents, 30 steps) run twice from the same swarm,
     with the output buffers pre-filled with different garbage and a different allocation
     history, is bit-identical: no result depends on uninitialised memory or on the order the
-    neighbour table's atomics insert agents."""
+    neighbour table's atomics insert agents. The neighbour lists the kernel built its rows from
+    (mpccbf_batch.nb_out) are compared too, and at step 0 they are the CPU query's (fov_csr: the
+    k nearest inside the cone and range, sorted by index).
+    Round 3's step-0 failures of the slack case (1 vs 7-8 solver steps) were a product with 0 of
+    LDS the active set had not written (das_wave.hpp, the slack patterns' unbounded loops): NaN /
+    Inf left there by an earlier kernel turned the first direction into NaN; reproduced
+    deterministically by a NaN LDS-poison build (profiles/r04_lds_poison_nan.log)."""
     torch = _torch()
     n, steps = 512, 30
     over = dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.9) if slack else {}
@@ -94,16 +100,24 @@ def test_fov_closed_loop_is_deterministic(mpclib, slack):
         cur = torch.tensor(states, device=dev)
         tg = torch.tensor(targets, device=dev)
         log = []
+        nb_out = torch.full((n, 16), -5, dtype=torch.int32, device=dev)
         for s in range(steps):
             ctx.impc_solve(cur, targets=tg, knn_k=8, knn_radius=cfg["fov_Rs"], cov=cov, traj_t=traj_t,
-                           step_index=s, pos_std=0.001, vel_std=0.01, noise_seed=20251015, **out)
-            log.append((out["status"].clone(), out["iters"].clone(), out["obj"].clone(), out["next_states"].clone()))
+                           step_index=s, pos_std=0.001, vel_std=0.01, noise_seed=20251015, nb_out=nb_out, **out)
+            log.append((out["status"].clone(), out["iters"].clone(), out["obj"].clone(), out["next_states"].clone(),
+                        nb_out.clone()))
+            if s == 0:
+                rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
+                nbl = nb_out.cpu().numpy()
+                for a in range(n):
+                    lst = col[rp[a]:rp[a + 1]]
+                    assert list(nbl[a, :len(lst)]) == list(lst) and np.all(nbl[a, len(lst):] == -1), (a, nbl[a], lst)
             cur = out["next_states"].clone()
         torch.cuda.synchronize()
         runs.append(log)
         del junk
     for s in range(steps):
-        for a, b, name in zip(runs[0][s], runs[1][s], ("status", "iters", "obj", "next_states")):
+        for a, b, name in zip(runs[0][s], runs[1][s], ("status", "iters", "obj", "next_states", "nb_out")):
             same = torch.equal(a, b) if name != "obj" else bool(torch.all((a == b) | (torch.isnan(a) & torch.isnan(b))))
             if not same:
                 idx = torch.nonzero(a != b)[:4].tolist()

@@ -26,10 +26,12 @@ def _torch():
     return torch
 
 
-def _run(mpclib, torch, cfg, states, targets, steps, nranks):
+def _run(mpclib, torch, cfg, states, targets, steps, nranks, cov=None):
     dev = torch.device("cuda", 0)
     n = len(states)
     per = n // nranks
+    fov = cfg.get("cbf_mode", 0) == 1
+    radius = cfg["fov_Rs"] if fov else 3.0 * cfg["d_min"]
     comms = mpclib.Comm.local_group(nranks, 0) if nranks > 1 else [None]
     results, errors = [None] * nranks, []
 
@@ -44,12 +46,15 @@ def _run(mpclib, torch, cfg, states, targets, steps, nranks):
                 tg = torch.tensor(targets[r * per:(r + 1) * per], device=dev)
                 traj_t = torch.full((per,), -1.0, dtype=torch.float64, device=dev)
                 slog = torch.empty((steps, per, 2), dtype=torch.int32, device=dev)
+                ilog = torch.empty((steps, per, 2), dtype=torch.int32, device=dev)
+                cv = None if cov is None else torch.tensor(cov, device=dev)
                 res = ctx.run_steps(a, b, steps, targets=tg, agent_first=r * per, num_agents=per,
-                                    knn_k=8, knn_radius=3.0 * cfg["d_min"], x=out["x"], obj=out["obj"],
+                                    knn_k=8, knn_radius=radius, x=out["x"], obj=out["obj"],
                                     traj_t=traj_t, pos_std=0.001, vel_std=0.01, noise_seed=7,
-                                    status_log=slog, comm=comms[r], stream=stream)
+                                    status_log=slog, iters_log=ilog, comm=comms[r], stream=stream, cov=cv)
                 stream.synchronize()
-                results[r] = (res["final"].cpu().numpy(), slog.cpu().numpy(), out["x"].cpu().numpy())
+                results[r] = (res["final"].cpu().numpy(), slog.cpu().numpy(), out["x"].cpu().numpy(),
+                              ilog.cpu().numpy())
         except Exception as e:  # surfaced in the main thread
             errors.append(e)
 
@@ -76,13 +81,37 @@ def test_local_group_matches_single_rank(mpclib, nranks, n_agents):
     single = _run(mpclib, torch, cfg, states, targets, steps, 1)[0]
     multi = _run(mpclib, torch, cfg, states, targets, steps, nranks)
     per = n_agents // nranks
-    for r, (final, slog, x) in enumerate(multi):
+    for r, (final, slog, x, _) in enumerate(multi):
         # every rank ends with the whole gathered table, equal to the single-rank loop
         np.testing.assert_array_equal(final, single[0])
         np.testing.assert_array_equal(slog, single[1][:, r * per:(r + 1) * per])
         np.testing.assert_array_equal(x, single[2][r * per:(r + 1) * per])
     assert not np.array_equal(single[0], states)
     assert np.any(single[1] == 3), "the crowded swarm should produce INFEASIBLE QPs"
+
+
+@pytest.mark.parametrize("slack", [False, True])
+def test_local_group_fov_config5_shape(mpclib, slack):
+    """BASELINE config 5's shape: 4096 FoV agents as 8 ranks x 512 (FovBezierIMPCCBF.cpp:48-223,
+    cone-filtered neighbour query over the gathered table, foreign rows inserted after the
+    exchange), with and without slack variables: bit-identical to the single-rank closed loop,
+    solver-step counts included."""
+    torch = _torch()
+    over = dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=0.9) if slack else {}
+    cfg = swarm.fov_config(20, **over)
+    states, targets = swarm.heading_swarm(4096)
+    cov = np.tile([0.1, 0.0, 0.1], (4096, 1)) if slack else None
+    steps = 8
+    single = _run(mpclib, torch, cfg, states, targets, steps, 1, cov=cov)[0]
+    multi = _run(mpclib, torch, cfg, states, targets, steps, 8, cov=cov)
+    per = 512
+    for r, (final, slog, x, ilog) in enumerate(multi):
+        np.testing.assert_array_equal(final, single[0])
+        np.testing.assert_array_equal(slog, single[1][:, r * per:(r + 1) * per])
+        np.testing.assert_array_equal(ilog, single[3][:, r * per:(r + 1) * per])
+        np.testing.assert_array_equal(x, single[2][r * per:(r + 1) * per])
+    assert not np.array_equal(single[0], states)
+    assert np.any(single[3] > 0), "some QP should need solver steps"
 
 
 def test_local_group_rank_failure_does_not_hang(mpclib):

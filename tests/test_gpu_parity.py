@@ -323,9 +323,9 @@ def test_fov_grid_neighbours_match_csr(mpclib):
 
 
 @pytest.mark.parametrize("scale", [1.0, 0.6, 0.45])
-def test_fov_dual_active_set_matches_pdip(mpclib, scale, monkeypatch):
+def test_fov_dual_active_set_matches_pdip(mpclib, scale):
     """Config 5: the dual active-set solve (default first attempt, das_wave.hpp) and the PDIP alone
-    (MPCCBF_DUAL_AS=0) give the same statuses — INFEASIBLE included (an unreachable candidate
+    (mpccbf_options.dual_as_steps < 0) give the same statuses — INFEASIBLE included (an unreachable candidate
     goes to phase 1 directly) — and the same optima to the PDIP's tolerance, except where the
     PDIP alone fails (UNKNOWN): there the active-set result is checked against the oracle."""
     torch = _torch()
@@ -333,9 +333,7 @@ def test_fov_dual_active_set_matches_pdip(mpclib, scale, monkeypatch):
     states, targets = swarm.heading_swarm(256, seed=4)
     states[:, :2] *= scale
     rp, col = swarm.fov_csr(states, 8, cfg["fov_Rs"], cfg["fov_beta"])
-    monkeypatch.setenv("MPCCBF_DUAL_AS", "0")
-    pdip = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
-    monkeypatch.delenv("MPCCBF_DUAL_AS")
+    pdip = run_gpu(mpclib.Context(cfg, dual_as_steps=-1), states, targets, rp, col, torch)
     das = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
     mism = np.nonzero(np.any(pdip["status"] != das["status"], axis=1))[0]
     assert len(mism) <= 0.02 * len(states), mism
@@ -583,20 +581,19 @@ def test_grid_bucket_overflow_falls_back_to_full_scan(mpclib):
 
 
 @pytest.mark.parametrize("scale", [0.55, 0.42, 0.3])
-def test_iteration1_warm_start_matches_cold_start(mpclib, scale, monkeypatch):
+def test_iteration1_warm_start_matches_cold_start(mpclib, scale):
     """IMPC iteration 1 warm-started from iteration 0's primal-dual point (the default,
     mpccbf_options.warm_delta = 0 -> 0.3) and cold-started (warm_delta < 0) reach the same
     optima: statuses equal (also on the very crowded 0.3 lattice, where breakdowns and infeasible
     QPs occur), objectives within solver tolerance; the warm start saves Newton steps. The PDIP
     path alone (dual active-set solve off), which is the one the warm start feeds."""
     torch = _torch()
-    monkeypatch.setenv("MPCCBF_DUAL_AS", "0")
     cfg = swarm.config(15)
     states, targets = swarm.lattice_swarm(1024, seed=5)
     states[:, :2] *= scale
     rp, col = swarm.knn_csr(states, 8, 6.0)
-    cold = run_gpu(mpclib.Context(cfg, warm_delta=-1.0), states, targets, rp, col, torch)
-    warm = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    cold = run_gpu(mpclib.Context(cfg, warm_delta=-1.0, dual_as_steps=-1), states, targets, rp, col, torch)
+    warm = run_gpu(mpclib.Context(cfg, dual_as_steps=-1), states, targets, rp, col, torch)
     np.testing.assert_array_equal(cold["status"], warm["status"])
     ok = cold["status"] == 0
     if scale < 0.4:  # very crowded: iteration 1 is never reached OPTIMAL; statuses are the check
@@ -611,7 +608,7 @@ def test_iteration1_warm_start_matches_cold_start(mpclib, scale, monkeypatch):
 
 
 @pytest.mark.parametrize("scale", [0.3, 0.45, 0.55, 1.0])
-def test_dual_active_set_matches_pdip(mpclib, scale, monkeypatch):
+def test_dual_active_set_matches_pdip(mpclib, scale):
     """The dual active-set solve (default first attempt) and the PDIP alone (MPCCBF_DUAL_AS=0)
     give the same statuses — INFEASIBLE included: a QP the active-set method finds unreachable is
     certified by phase 1 as before — and the same optima to the PDIP's tolerance; the active-set
@@ -622,9 +619,7 @@ def test_dual_active_set_matches_pdip(mpclib, scale, monkeypatch):
     states, targets = swarm.lattice_swarm(1024, seed=5)
     states[:, :2] *= scale
     rp, col = swarm.knn_csr(states, 8, 6.0)
-    monkeypatch.setenv("MPCCBF_DUAL_AS", "0")
-    pdip = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
-    monkeypatch.delenv("MPCCBF_DUAL_AS")
+    pdip = run_gpu(mpclib.Context(cfg, dual_as_steps=-1), states, targets, rp, col, torch)
     das = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
     np.testing.assert_array_equal(pdip["status"], das["status"])
     ok = pdip["status"] == 0
@@ -640,10 +635,25 @@ def test_dual_active_set_matches_pdip(mpclib, scale, monkeypatch):
         assert das["iters"][hard, 0].mean() < pdip["iters"][hard, 0].mean()
 
 
-def test_invalid_warm_delta_env_rejected(mpclib, monkeypatch):
-    monkeypatch.setenv("MPCCBF_WARM_DELTA", "0.3x")
-    with pytest.raises(mpclib.MpccbfError, match="MPCCBF_WARM_DELTA"):
-        mpclib.Context(swarm.config(15))
+def test_solver_env_vars_have_no_effect(mpclib, monkeypatch):
+    """The release library's solver path comes from mpccbf_options alone: the diagnostics build's
+    tuning variables (MPCCBF_DUAL_AS, ...) set in the caller's environment change nothing, while
+    the same setting through the options does (the PDIP alone takes other solver steps)."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(512, seed=5)
+    states[:, :2] *= 0.55
+    rp, col = swarm.knn_csr(states, 8, 6.0)
+    ref = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    for k, v in (("MPCCBF_DUAL_AS", "0"), ("MPCCBF_EARLY_IT", "1"), ("MPCCBF_FAST_START", "0"),
+                 ("MPCCBF_LEAN", "1"), ("MPCCBF_DAS_WARM", "0"), ("MPCCBF_WARM_DELTA", "0.3x")):
+        monkeypatch.setenv(k, v)
+    env = run_gpu(mpclib.Context(cfg), states, targets, rp, col, torch)
+    for k in ("status", "iters", "obj"):
+        np.testing.assert_array_equal(env[k], ref[k])
+    opt = run_gpu(mpclib.Context(cfg, dual_as_steps=-1), states, targets, rp, col, torch)
+    np.testing.assert_array_equal(opt["status"], ref["status"])
+    assert not np.array_equal(opt["iters"], ref["iters"])
 
 
 @pytest.mark.parametrize("n_ring,radius,v0", [(20, 1.99, (0.2, 0.1)), (40, 1.98, (0.1, 0.3))])

@@ -36,8 +36,18 @@ def test_library_exports_every_declared_symbol(mpclib):
 
 def test_abi_version_and_status_strings(mpclib):
     L = mpclib.load()
-    assert L.mpccbf_abi_version() == 9
+    assert L.mpccbf_abi_version() == 10
     assert [L.mpccbf_status_string(i).decode() for i in range(7)] == mpclib.STATUS_NAMES
+
+
+def test_release_library_reads_no_solver_env_vars(mpclib):
+    """Solver decisions come from mpccbf_options alone: the release library does not even name the
+    diagnostics build's tuning variables (capi.hip, MPCCBF_DIAG_ENV); no getenv call site is
+    compiled in (the GPU-side check: test_gpu_parity.py::test_solver_env_vars_have_no_effect)."""
+    blob = open(mpclib.LIB_PATH, "rb").read()
+    for name in (b"MPCCBF_DUAL_AS", b"MPCCBF_EARLY_IT", b"MPCCBF_FAST_START", b"MPCCBF_LEAN",
+                 b"MPCCBF_DAS_WARM", b"MPCCBF_WARM_DELTA"):
+        assert name not in blob, name
 
 
 def test_param_validation_messages(mpclib):

@@ -1,5 +1,5 @@
 """Re-solve the FoV (config 5) QPs of a `bench.py --workload fov --dump` trace on the GPU, once with
-the default solver and once with the PDIP alone (MPCCBF_DUAL_AS=0), and list the agents whose
+the default solver and once with the PDIP alone (mpccbf_options.dual_as_steps < 0), and list the agents whose
 default solve took many steps: which QPs the dual active set hands to the PDIP.
 
     python tools/fov_diag.py gpurun_out/<tag>/fov.npz [first_step] [last_step] [min_steps] [--slack]
@@ -28,9 +28,7 @@ def main():
     cfg = swarm.fov_config(20, **over)
     _, targets = swarm.heading_swarm(n)
     dev = torch.device("cuda", 0)
-    os.environ["MPCCBF_DUAL_AS"] = "0"
-    ctx_p = Context(cfg)
-    del os.environ["MPCCBF_DUAL_AS"]
+    ctx_p = Context(cfg, dual_as_steps=-1)  # the PDIP alone
     ctx = Context(cfg)
     tg = torch.tensor(targets, device=dev)
     common = dict(targets=tg, knn_k=8, knn_radius=cfg["fov_Rs"])

@@ -1,6 +1,6 @@
 """FoV (config 5) status parity of the dual active-set first attempt: the bench's closed loop with
 the default solver, and at every step the same states solved by a PDIP-only context
-(MPCCBF_DUAL_AS=0, read at context creation); the states of steps whose statuses differ are saved
+(mpccbf_options.dual_as_steps < 0); the states of steps whose statuses differ are saved
 for an offline oracle check (--check).
 
     python tools/fov_status_check.py [steps] [out.npz]          (GPU)
@@ -33,9 +33,7 @@ def run(steps, out):
     cfg = fov_cfg(swarm)
     states, targets = swarm.heading_swarm(512)
     dev = torch.device("cuda", 0)
-    os.environ["MPCCBF_DUAL_AS"] = "0"
-    ctx_p = Context(cfg)
-    del os.environ["MPCCBF_DUAL_AS"]
+    ctx_p = Context(cfg, dual_as_steps=-1)  # the PDIP alone
     ctx = Context(cfg)
     tg = torch.tensor(targets, device=dev)
     cur = torch.tensor(states, device=dev)

@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B timing of bench lines under environment settings (run from the repo root on the GPU box):
 #   bash tools/gpu_ab.sh <tag> "<bench args>" "<env A>" "<env B>" ...
-# e.g.  bash tools/gpu_ab.sh lean "--steps 20 --warmup 5" "MPCCBF_LEAN=1" "MPCCBF_LEAN=0"
+# e.g.  bash tools/gpu_ab.sh lean "--steps 20 --warmup 5" "MPCCBF_LIB=mpc-cbf_amd/build/diag/libmpccbf.so MPCCBF_LEAN=1" "MPCCBF_LIB=mpc-cbf_amd/build/diag/libmpccbf.so MPCCBF_LEAN=0"
+# (the solver-tuning variables are read by the diagnostics build only: make -C mpc-cbf_amd diag)
 # Each setting runs the bench line twice (interleaved A B A B); outputs gpurun_out/<tag>/<i>_<r>.json.
 set -e -o pipefail
 TAG=$1
