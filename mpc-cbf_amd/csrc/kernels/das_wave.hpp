@@ -84,12 +84,18 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
 }
 
 // P and P^-1 (16 x 16, global) into the workspace, once per agent: every das_solve_wave call of
-// the agent reads them there (a per-call copy was a global round trip on each solve's chain)
+// the agent reads them there (a per-call copy was a global round trip on each solve's chain).
+// Also zeroes ws.W: the direction reads row 0 of it while the active set is empty and multiplies
+// it by 0 (the slack patterns' unbounded loops, kk = 16); never written, it holds whatever an
+// earlier kernel left in this LDS — NaN / Inf included, and 0 * NaN is NaN. That was round 3's
+// FoV-slack step-0 nondeterminism (profiles/r04_lds_poison_nan.log). (Zeroed here rather than a
+// select in the loop: the select pushed the FoV kernels from 0 / 76 to 524 / 972 B/lane of scratch.)
 __device__ __forceinline__ void das_load_operators(WaveAS& ws, const double* __restrict__ P,
                                                    const double* __restrict__ Pinv, int lane) {
     for (int e = lane; e < WNZ * WNZ; e += 64) {
         ws.Pi[(e >> 4) * 17 + (e & 15)] = Pinv[e];
         ws.P[(e >> 4) * 17 + (e & 15)] = P[e];
+        ws.W[e] = 0.0;
     }
     wave_lds_sync();
 }
@@ -267,13 +273,8 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
                 for (int a = 0; a < WNZ - 1; a++) {
                     if (a < kk) {
                         const double ra_ = bcast16v(a, rhoi);
-                        // (a select, not a product with 0: rows a >= k of ws.W were never written in
-                        // this block — LDS left by an earlier kernel, NaN / Inf included, and
-                        // 0 * NaN is NaN. The slack patterns' unbounded loops (kk = 16) read them
-                        // on every step from an empty active set: that was the FoV-slack step-0
-                        // nondeterminism of round 3)
-                        const double wa = ws.W[(a < k ? a : 0) * WNZ + i];
-                        zi = a < k ? fma(-ra_, wa, zi) : zi;
+                        // (rows a >= k: ws.W finite, zeroed by das_load_operators, times 0)
+                        zi = fma(a < k ? -ra_ : 0.0, ws.W[(a < k ? a : 0) * WNZ + i], zi);
                     }
                 }
                 yi = fma(-t, zi, yi);
@@ -353,8 +354,7 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         for (int a = 0; a < WNZ - 1; a++) {
             if (a < kk) {
                 const double la = bcast16v(a, lsi);
-                const double ga = Gs[(a < k ? ws.row[a] : 0) * WNZ + i];
-                r = a < k ? fma(la, ga, r) : r;  // (a select: see the direction above)
+                r = fma(a < k ? la : 0.0, Gs[(a < k ? ws.row[a] : 0) * WNZ + i], r);
             }
         }
         double qn = fabs(sc.q[i]);

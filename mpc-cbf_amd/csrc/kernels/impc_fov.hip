@@ -140,7 +140,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     } else {
         nnb = grid_neighbors<64>(args, self, s0[0], s0[1], nb_scratch, lane, s0[2]);
     }
-    write_nb_out(args, ai, lane, grid_mode, nb_scratch, nb0, nnb);
     const bool nb_overflow = nnb < 0 || nnb > (SLACK ? WSL_NB : FOV_NB_CAP);
     if (nb_overflow) nnb = 0;
     if constexpr (SLACK) {
@@ -651,6 +650,8 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
         write_agent_outputs<NZ, 64, !SLACK>(op, buf, args, ai, lane, s0, yk, have_curve);
     }
+    // (diagnostics; here, not after the query: there it pushed the kernel into scratch)
+    write_nb_out(args, ai, lane, grid_mode, nb_scratch, nb0, nnb);
     stamp(args, ai, lane, 7);
 }
 

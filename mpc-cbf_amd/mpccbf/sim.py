@@ -1,12 +1,17 @@
 """Closed-loop swarm simulator with the reference example's outputs.
 
 The loop of MPCCBFFormationControl_example.cpp:131-231 on the device: every control step each
-robot re-plans (ConnectivityIMPCCBF::optimize -> mpccbf_impc_solve, all robots in one batch: a
-Jacobi sweep where the reference updates robots one after another), keeps its last successful
+robot re-plans (ConnectivityIMPCCBF::optimize -> mpccbf_impc_solve), keeps its last successful
 trajectory when a step fails (:150-165), and integrates int(h / Ts) control sub-steps of the kept
 curve with state noise (:188-207), or holds its position at zero velocity when it never had a
-curve (:208-221). The states.json trace is written in the example's shape (:127-129, :166-205,
-:229-231):
+curve (:208-221). Two update orders:
+  order="jacobi" (default, the batched product path): all robots in one launch, every robot
+      re-planning from the states of the previous step;
+  order="gauss_seidel" (the reference's own order, for parity at small N): robots in index order
+      (:140), each solved alone (one launch per robot) from the current table and its next state
+      written back in place (:201) before the next robot plans, so robot i sees robots < i at
+      their new states.
+The states.json trace is written in the example's shape (:127-129, :166-205, :229-231):
 
     {"dt": h, "Ts": Ts, "robots": {"<i>": {"pred_curve": [[[x, y, z], ...]] per step,
                                            "states": [[px, py, pz, vx, vy, vz], ...] per sub-step}}}
@@ -53,8 +58,11 @@ class Simulator:
 
     def __init__(self, cfg: dict, states: np.ndarray, targets: np.ndarray, *, neighbours="knn",
                  knn_k=8, knn_radius=None, pos_std=0.0, vel_std=0.0, noise_seed=0, device=0,
-                 record=True):
+                 record=True, order="jacobi"):
         import torch
+        if order not in ("jacobi", "gauss_seidel"):
+            raise ValueError("order must be 'jacobi' or 'gauss_seidel'")
+        self.order = order
         self.torch = torch
         self.cfg = dict(cfg)
         self.dev = torch.device("cuda", device)
@@ -70,12 +78,14 @@ class Simulator:
         self.nsub = int(cfg["h"] / cfg["Ts"])
         self.substeps = torch.empty((n, self.nsub, 6), dtype=torch.float64, device=self.dev)
         self.nb = {}
-        if neighbours == "all":
+        self.csr = neighbours == "all"
+        if self.csr:
             rp, col = swarm.all_csr(n)
             self.nb = dict(nb_row_ptr=torch.tensor(rp, device=self.dev),
                            nb_col=torch.tensor(col if len(col) else np.zeros(1, np.int32), device=self.dev))
         else:
             self.nb = dict(knn_k=knn_k, knn_radius=knn_radius or 3.0 * cfg["d_min"])
+        self.gs_next = torch.empty((1, 6), dtype=torch.float64, device=self.dev)
         self.noise = dict(pos_std=pos_std, vel_std=vel_std, noise_seed=noise_seed)
         self.step_index = 0
         self.sim_t = 0.0
@@ -88,9 +98,24 @@ class Simulator:
         torch = self.torch
         t_before = self.traj_t.cpu().numpy() if self.record else None
         o = self.out
-        self.ctx.impc_solve(self.states, targets=self.targets, x=o["x"], status=o["status"], obj=o["obj"],
-                            iters=o["iters"], next_states=self.next, traj_t=self.traj_t,
-                            substeps=self.substeps, step_index=self.step_index, **self.nb, **self.noise)
+        if self.order == "jacobi":
+            self.ctx.impc_solve(self.states, targets=self.targets, x=o["x"], status=o["status"], obj=o["obj"],
+                                iters=o["iters"], next_states=self.next, traj_t=self.traj_t,
+                                substeps=self.substeps, step_index=self.step_index, **self.nb, **self.noise)
+        else:
+            # robot by robot (:140), each from the table as the robots before it left it (:201)
+            self.next.copy_(self.states)  # (the states the robots re-plan from, for the record)
+            for i in range(self.n):
+                sl = slice(i, i + 1)
+                nb = dict(self.nb)
+                if self.csr:
+                    nb["nb_row_ptr"] = self.nb["nb_row_ptr"][i:i + 2]
+                self.ctx.impc_solve(self.states, targets=self.targets[sl], agent_first=i, num_agents=1,
+                                    x=o["x"][sl], status=o["status"][sl], obj=o["obj"][sl], iters=o["iters"][sl],
+                                    next_states=self.gs_next, traj_t=self.traj_t[sl], substeps=self.substeps[sl],
+                                    step_index=self.step_index, **nb, **self.noise)
+                self.states[i].copy_(self.gs_next[0])
+            self.states, self.next = self.next, self.states  # (swapped back below)
         torch.cuda.synchronize()
         status = o["status"].cpu().numpy()
         self.status_log.append(status.copy())

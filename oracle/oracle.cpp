@@ -552,7 +552,19 @@ struct Assembler {
                 for (int d = 0; d < DIM; d++) s += a[d] * U[(k * DIM + d) * nc + j];
                 row[j] = -1.0 * s;
             }
-            if (nslack > 0) row[nc + nbi] = -1.0;  // ConnectivityMPCCBFQPGenerator.cpp:33-40
+            if (nslack > 0) {
+                // slack mode: a row that every acceleration of the box at sample k satisfies with
+                // v_i = 0 (b >= max over the box of -a^T u) holds for every v_i >= 0 too, and the
+                // box rows of sample k (addEvalBoundConstraints(2, ...), below) are in every QP —
+                // dropping it leaves the feasible set and the optimum unchanged (the kernel's
+                // filter, impc_kernel.hip lane_cbf_rows). Kept, a distant neighbour's row has a
+                // bound ~1e26 next to a slack weight down to ~1e-9, and the dense PDIP stalls on
+                // its dual residual (round 3: two all-neighbour slack QPs UNKNOWN).
+                double bmax = 0.0;
+                for (int d = 0; d < DIM; d++) bmax += std::max(-a[d] * p->a_min[d], -a[d] * p->a_max[d]);
+                if (b >= bmax) return;
+                row[nc + nbi] = -1.0;  // ConnectivityMPCCBFQPGenerator.cpp:33-40
+            }
             addRow(qp, row, LOWEST, b + 0.0);     // slack_value = 0 (:138, :172)
         };
         if (p->cbf_mode == 1) {
@@ -872,6 +884,25 @@ struct Solver {
                 if (!is_neg_inf(qp->vlo[i])) x[i] = std::max(x[i], qp->vlo[i]);
                 if (!is_pos_inf(qp->vhi[i])) x[i] = std::min(x[i], qp->vhi[i]);
             }
+            // ... and a variable without curvature that relaxes upper-bounded rows (a slack
+            // variable: -1 in its neighbour's CBF rows) starts at the smallest value that satisfies
+            // them at the start point, max(lower bound, max_r (g_r x - hi_r) / -A_ri): its optimum
+            // can be ~1e8 (a neighbour deep inside d_min), which steps limited by the ridge on a
+            // zero-curvature column (dv ~ rd / ridge) never reach (round 3's UNKNOWN slack QPs)
+            for (int i = 0; i < n; i++) {
+                if (P[(size_t)i * n + i] != 0.0 || is_neg_inf(qp->vlo[i])) continue;
+                double v = x[i];
+                for (int r = 0; r < qp->m; r++) {
+                    const double a = qp->A[(size_t)r * n + i];
+                    if (!(a < 0.0) || is_pos_inf(qp->hi[r]) || qp->lo[r] == qp->hi[r]) continue;
+                    double gx = 0.0;
+                    for (int j = 0; j < n; j++)
+                        if (j != i) gx += qp->A[(size_t)r * n + j] * x[j];
+                    v = std::max(v, (gx - qp->hi[r]) / -a);
+                }
+                if (!is_pos_inf(qp->vhi[i])) v = std::min(v, qp->vhi[i]);
+                x[i] = v;
+            }
         }
         std::vector<double> s(ns), z(ns);
         for (int k = 0; k < ns; k++) {
@@ -923,9 +954,13 @@ struct Solver {
             const bool finite = std::isfinite(rpmax) && std::isfinite(rdmax) && std::isfinite(mu) &&
                                 std::isfinite(compmax);
             if (!finite) break;  // diverged: status stays UNKNOWN (phase 1 decides)
-            if (std::getenv("ORC_TRACE"))
-                std::fprintf(stderr, "it %d rp %.3e rd %.3e mu %.3e comp %.3e\n", it, rpmax, rdmax,
-                             mu, compmax);
+            if (std::getenv("ORC_TRACE")) {
+                int ia = 0;
+                for (int i = 0; i < n; i++)
+                    if (std::fabs(rd[i]) > std::fabs(rd[ia])) ia = i;
+                std::fprintf(stderr, "it %d rp %.3e rd %.3e (var %d: x %.3e c %.3e) mu %.3e comp %.3e\n", it,
+                             rpmax, rdmax, ia, x[ia], c[ia], mu, compmax);
+            }
             // duality gap relative to the objective (rows whose bound is astronomically far,
             // e.g. b ~ 1e25 for a distant neighbour's CBF row, must not force mu -> 0 forever)
             double objv = 0;
@@ -993,9 +1028,11 @@ struct Solver {
             }
         }
         R.iters = it;
-        if (R.status != ORC_OPTIMAL && best_merit < 1e-8) {
-            // numerical stall after reaching a near-optimal point: keep the best iterate
-            R.status = ORC_OPTIMAL;
+        if (R.status != ORC_OPTIMAL && !bx.empty()) {
+            // numerical stall after reaching a near-optimal point (best merit < 1e-8): keep the best
+            // iterate as the optimum; otherwise it is still the best start for the caller's
+            // active-set finish (solve(): certified, or UNKNOWN)
+            if (best_merit < 1e-8) R.status = ORC_OPTIMAL;
             x = bx;
             lam = blam;
             z = bz;
@@ -1168,14 +1205,126 @@ static DenseQP scale_huge_rows(const DenseQP& q) {
     return r;
 }
 
-Solution solve(const DenseQP& q_in) {
+// Columns of variables without curvature that relax upper-bounded rows (slack variables, lower
+// bound 0, linear cost only) scaled to the magnitude of the bounds they offset: x_i = sigma_i x'_i
+// with sigma_i = max(1, max_r |hi_r / A_ri| over rows with hi_r < 0). A neighbour deep inside d_min
+// has a CBF bound ~ -1e8
+// (gamma (2 d.dv + gamma h^3)^3), so its slack's optimum is ~1e8 next to a weight ~1e-4; unscaled,
+// the interior point reaches it only in ridge-limited steps (round 3's two UNKNOWN all-neighbour
+// slack QPs). A change of variables: same optimum, sigma_i times the multiplier scale.
+static DenseQP scale_slack_columns(const DenseQP& q, std::vector<double>& sigma) {
+    DenseQP r = q;
+    const int n = q.n;
+    sigma.assign(n, 1.0);
+    for (int i = 0; i < n; i++) {
+        if (q.vlo[i] != 0.0 || !is_pos_inf(q.vhi[i]) || q.c[i] <= 0.0) continue;
+        bool curv = false;
+        for (int j = 0; j < n; j++) curv = curv || q.H[(size_t)i * n + j] != 0.0 || q.H[(size_t)j * n + i] != 0.0;
+        if (curv) continue;
+        double sg = 1.0;
+        for (int k = 0; k < q.m; k++) {
+            const double a = q.A[(size_t)k * n + i];
+            // (rows whose bound is negative: they force the variable up to about -hi / -a; a row
+            // with a large positive bound leaves it at 0 and says nothing about its scale)
+            if (!(a < 0.0) || is_pos_inf(q.hi[k]) || q.lo[k] == q.hi[k] || !(q.hi[k] < 0.0)) continue;
+            sg = std::max(sg, std::fabs(q.hi[k] / a));
+        }
+        sigma[i] = sg;
+        r.c[i] *= sg;
+        for (int k = 0; k < q.m; k++) r.A[(size_t)k * n + i] *= sg;
+    }
+    return r;
+}
+
+Solution solve_kept(const DenseQP& q_in);
+
+// Exact presolve: a variable that appears in no row, has no curvature, a finite lower bound and a
+// positive linear cost sits at that bound at the optimum (a slack variable whose rows the exact
+// box filter removed: v_i = 0). Removed here — left in, its central-path value mu / w_i with a
+// weight down to ~1e-9 keeps the interior point far from the optimum. keep: kept columns.
+static DenseQP drop_idle_columns(const DenseQP& q, std::vector<int>& keep, std::vector<double>& fixed) {
+    const int n = q.n;
+    keep.clear();
+    fixed.assign(n, 0.0);
+    for (int i = 0; i < n; i++) {
+        bool used = false;
+        for (int k = 0; k < q.m && !used; k++) used = q.A[(size_t)k * n + i] != 0.0;
+        for (int j = 0; j < n && !used; j++) used = q.H[(size_t)i * n + j] != 0.0 || q.H[(size_t)j * n + i] != 0.0;
+        if (!used && !is_neg_inf(q.vlo[i]) && q.c[i] > 0.0) {
+            fixed[i] = q.vlo[i];
+            continue;
+        }
+        keep.push_back(i);
+    }
+    DenseQP r;
+    const int nk = (int)keep.size();
+    r.n = nk;
+    r.m = q.m;
+    r.c0 = q.c0;
+    for (int i = 0; i < n; i++) r.c0 += fixed[i] * q.c[i];  // (fixed columns: no rows, no curvature)
+    r.H.assign((size_t)nk * nk, 0.0);
+    r.c.resize(nk);
+    r.vlo.resize(nk);
+    r.vhi.resize(nk);
+    for (int a = 0; a < nk; a++) {
+        r.c[a] = q.c[keep[a]];
+        r.vlo[a] = q.vlo[keep[a]];
+        r.vhi[a] = q.vhi[keep[a]];
+        for (int b = 0; b < nk; b++) r.H[(size_t)a * nk + b] = q.H[(size_t)keep[a] * n + keep[b]];
+    }
+    r.A.resize((size_t)q.m * nk);
+    for (int k = 0; k < q.m; k++)
+        for (int a = 0; a < nk; a++) r.A[(size_t)k * nk + a] = q.A[(size_t)k * n + keep[a]];
+    r.lo = q.lo;
+    r.hi = q.hi;
+    return r;
+}
+
+Solution solve(const DenseQP& q_full) {
+    std::vector<int> keep;
+    std::vector<double> fixed;
+    const DenseQP q_in = drop_idle_columns(q_full, keep, fixed);
+    Solution out = solve_kept(q_in);
+    std::vector<double> x = fixed;
+    for (size_t a = 0; a < keep.size(); a++) x[keep[a]] = out.x[a];
+    out.x = x;
+    if (out.status == ORC_OPTIMAL) {
+        double obj = q_full.c0;
+        const int n = q_full.n;
+        for (int i = 0; i < n; i++) {
+            double hx = 0;
+            for (int j = 0; j < n; j++) hx += q_full.H[(size_t)i * n + j] * x[j];
+            obj += x[i] * hx + q_full.c[i] * x[i];
+        }
+        out.obj = obj;
+    }
+    return out;
+}
+
+Solution solve_kept(const DenseQP& q_in) {
     Solution out;
-    const DenseQP q = scale_huge_rows(q_in);
+    std::vector<double> sigma;
+    const DenseQP q = scale_slack_columns(scale_huge_rows(q_in), sigma);
     Solver s(q);
     Solver::Result r = s.pdip(200, 1e-10);
-    if (r.status == ORC_OPTIMAL) s.polish(r);
+    if (r.status == ORC_OPTIMAL) {
+        s.polish(r);
+    } else if (s.polish(r)) {
+        // the interior point stalled short of the tolerance (slack QPs whose optimal slack is
+        // ~1e8 next to weights ~1e-4: the dual residual floors at ~1e-7): the equality QP on its
+        // active sides, accepted as the optimum only with an exact KKT certificate (stationarity,
+        // primal and dual feasibility, complementarity) at 1e-9
+        double cinf = 0.0, zinf = 0.0, binf = 0.0;
+        for (double v : s.c) cinf = std::max(cinf, std::fabs(v));
+        for (double v : r.z) zinf = std::max(zinf, std::fabs(v));
+        for (const auto& sd : s.sides) binf = std::max(binf, std::fabs(sd.b));
+        if (r.kkt[0] <= 1e-9 * (1.0 + cinf) && r.kkt[1] <= 1e-9 * (1.0 + binf) &&
+            r.kkt[2] <= 1e-9 * (1.0 + zinf) && r.kkt[3] <= 1e-9 * (1.0 + zinf) * (1.0 + binf))
+            r.status = ORC_OPTIMAL;
+    }
     out.iters = r.iters;
     std::memcpy(out.kkt, r.kkt, sizeof(out.kkt));
+    for (int i = 0; i < q.n; i++) r.x[i] *= sigma[i];  // back to the caller's variables
     if (r.status != ORC_OPTIMAL) {
         // CPLEX default feasibility tolerance 1e-6 decides infeasibility
         double t = phase1(q);
@@ -1187,11 +1336,11 @@ Solution solve(const DenseQP& q_in) {
     out.status = ORC_OPTIMAL;
     out.x = r.x;
     const int n = q.n;
-    double obj = q.c0;
+    double obj = q_in.c0;
     for (int i = 0; i < n; i++) {
         double hx = 0;
-        for (int j = 0; j < n; j++) hx += q.H[i * n + j] * r.x[j];
-        obj += r.x[i] * hx + q.c[i] * r.x[i];
+        for (int j = 0; j < n; j++) hx += q_in.H[i * n + j] * r.x[j];
+        obj += r.x[i] * hx + q_in.c[i] * r.x[i];
     }
     out.obj = obj;
     return out;

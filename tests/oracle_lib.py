@@ -339,3 +339,91 @@ def connectivity_control(cfg: dict, states, self_idx, desired_u):
         float(cfg.get("slack_decay_rate", 1.0)), len(st), _d(st), int(self_idx), _d(f(desired_u)),
         _d(u), _d(obj), _d(l2))
     return stt, u, float(obj[0]), float(l2[0])
+
+
+# ---- closed loop in the reference example's order (test infrastructure) -----------------------
+_M64 = (1 << 64) - 1
+
+
+def _mix64(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def normal_sample(seed: int, step: int, agent: int, comp: int, sub: int = 0) -> float:
+    """The counter-based state noise of the product (impc_common.hpp normal_sample: splitmix64 keyed
+    by (seed, step, agent, component, sub-step) + Box-Muller), in place of math::addRandomNoise's
+    std::mt19937 seeded from std::random_device (Random.cpp:7-28), which no two runs share."""
+    k = _mix64(seed & _M64)
+    k = _mix64(k ^ (step & _M64))
+    k = _mix64(k ^ ((agent * 8 + comp) & _M64))
+    if sub > 0:
+        k = _mix64(k ^ ((sub << 40) & _M64))
+    u1 = float((k >> 11) + 1) * 2.0 ** -53
+    u2 = float(_mix64(k) >> 11) * 2.0 ** -53
+    return float(np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2))
+
+
+def knn_list(states, i, k, radius):
+    """Agent i's k nearest others (planar) within radius, ties by index, sorted by index (the
+    device grid query's rule, mpccbf.swarm.knn_csr for one agent)."""
+    p = states[:, :2]
+    d2 = np.sum((p - p[i]) ** 2, axis=1)
+    d2[i] = np.inf
+    cand = np.nonzero(d2 <= radius * radius)[0]
+    order = np.lexsort((cand, d2[cand]))[:k]
+    return np.sort(cand[order]).astype(np.int32)
+
+
+def closed_loop_gauss_seidel(cfg: dict, states, targets, steps, k=8, radius=6.0, pos_std=0.0, vel_std=0.0,
+                             seed=0, neighbours="knn"):
+    """MPCCBFFormationControl_example.cpp:131-226 restated in its own order: per control step the
+    robots in index order (:140), each optimize()d against the current table (robots before it
+    already moved, :201), the kept curve (last successful trajectory, :150-165) evaluated int(h/Ts)
+    sub-steps ahead with the noise (:188-207), or the position held at zero velocity (:208-221).
+    Returns (trace: steps+1 x n x 6 states after each step, status: steps x n x impc_iter)."""
+    p = make_params(cfg)
+    n = len(states)
+    cur = np.array(states, dtype=np.float64)
+    refs = np.tile(np.asarray(targets, dtype=np.float64), (1, cfg["k_hor"]))
+    nsub = int(cfg["h"] / cfg["Ts"])
+    eval_step = cfg["Ts"] * nsub
+    tmax = cfg["num_pieces"] * cfg["piece_max_parameter"]
+    xs = [None] * n
+    traj_t = np.full(n, -1.0)
+    trace = [cur.copy()]
+    stats = []
+    for s in range(steps):
+        st = np.full((n, cfg["impc_iter"]), UNKNOWN, dtype=np.int32)
+        for i in range(n):
+            nb = (np.array([j for j in range(n) if j != i], dtype=np.int32) if neighbours == "all"
+                  else knn_list(cur, i, k, radius))
+            r = impc_optimize(p, cur, i, nb, refs[i])
+            st[i] = r["status"]
+            ok = np.nonzero(r["status"] == OPTIMAL)[0]
+            if len(ok):
+                xs[i] = r["x"][ok[-1]].copy()
+                traj_t[i] = 0.0
+            nxt = np.zeros(6)
+            if xs[i] is not None:
+                t_new = min(traj_t[i] + eval_step, tmax)
+                pos, vel = eval_curve(p, xs[i], t_new, 0), eval_curve(p, xs[i], t_new, 1)
+                for c in range(6):
+                    sd = pos_std if c < 3 else vel_std
+                    v = pos[c] if c < 3 else vel[c - 3]
+                    nxt[c] = v + sd * normal_sample(seed, s, i, c) if sd > 0.0 else v
+                traj_t[i] = t_new
+            else:
+                for c in range(6):
+                    sd = pos_std if c < 3 else vel_std
+                    v = cur[i, c] if c < 3 else 0.0
+                    for kk in range(1, nsub + 1):
+                        dn = sd * normal_sample(seed, s, i, c, nsub - kk) if sd > 0.0 else 0.0
+                        v = v + dn if c < 3 else dn
+                    nxt[c] = v
+            cur[i] = nxt
+        trace.append(cur.copy())
+        stats.append(st)
+    return np.array(trace), np.array(stats)

@@ -58,6 +58,7 @@ def test_regression_cases_match_oracle(mpclib):
     cases = json.load(open(os.path.join(HERE, "golden", "regress_cases.json")))["cases"]
     dev = torch.device("cuda", 0)
     assert any(c.get("controller") == "fov_slack" for c in cases)
+    assert any(c.get("controller") == "collision_slack" for c in cases)
     for case in cases:
         states = np.array(case["states"])
         n = len(states)
@@ -66,6 +67,9 @@ def test_regression_cases_match_oracle(mpclib):
             cfg = swarm.fov_config(case["k_hor"], slack_mode=1, slack_cost=case["slack_cost"],
                                    slack_decay_rate=case["slack_decay_rate"])
             cov = np.tile(np.array(case["cov"]), (n, 1))
+        elif case.get("controller") == "collision_slack":  # ConnectivityIMPCCBF in slack mode
+            cfg = swarm.config(case["k_hor"], slack_mode=1, slack_cost=case["slack_cost"],
+                               slack_decay_rate=case["slack_decay_rate"])
         else:
             cfg = swarm.config(case["k_hor"])
         targets = np.tile(np.array(case["target"]), (n, 1))
