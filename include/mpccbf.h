@@ -368,9 +368,11 @@ int mpccbf_connectivity_control_solve(const mpccbf_connectivity_control_params* 
  *             vlo_i <= x_i <= vhi_i
  * The host validates and packs the nonzeros; the device eliminates the equalities (Householder QR
  * with column pivoting: null space + minimum-norm particular solution) and solves the reduced
- * problem with the interior-point kernel. n <= 64, at most 64 equality rows, reduced dimension
- * <= 8 and 256 reduced rows (MPCCBF_ERR_CAPACITY beyond). x_out is written only if *status_out is
- * OPTIMAL (Solver.h:33-35). */
+ * problem with the interior-point kernel. A QP with more than 64 variables or 64 equality rows
+ * (fixed variables count as equalities) is reduced on the host the same way and solved by the same
+ * device kernel. Inconsistent equalities are INFEASIBLE whatever the sizes; otherwise reduced
+ * dimension <= 8 and 256 reduced rows (MPCCBF_ERR_CAPACITY beyond). x_out is written only if
+ * *status_out is OPTIMAL (Solver.h:33-35). */
 typedef struct mpccbf_dense_qp {
     int32_t n, m;
     const double* H;  /* n x n row-major */

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/mpccbf.h"
+#include "host/dense_qp.hpp"
 #include "host/errors.hpp"
 #include "kernels/group.hpp"
 #include "kernels/pdip.hpp"
@@ -68,6 +69,9 @@ struct DenseBatch {
     int32_t maxit;
     double tol;
     double feas_tol;
+    // count flags: 1 = reduced on the host (beyond the device elimination's 64 variables / 64
+    // equalities; host/dense_qp.cpp), its reduced QP, status, m and pd uploaded, x expanded on the host
+    const int32_t* hostred;
 };
 
 namespace dev {
@@ -91,7 +95,7 @@ __device__ __forceinline__ bool fin_bound(double v) { return isfinite(v) && fabs
 __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int l = threadIdx.x;
-    if (qi >= a.count) return;
+    if (qi >= a.count || a.hostred[qi]) return;  // (reduced on the host)
     __shared__ ReduceLds s;
     const int32_t* ib = a.ints + a.off_i[qi];
     const double* db = a.dbl + a.off_d[qi];
@@ -109,7 +113,9 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     const double* ihi = ilo + mi;
     const double* ival = ihi + mi;
     double* red = a.red + (size_t)qi * DQ_STRIDE;
-    bool infeasible = false;
+    // inconsistent equalities (decided whatever the reduced dimension) / a constant row violated
+    // (decided only within capacity: beyond it the rows' reduced coefficients are not all formed)
+    bool infeasible = false, eq_infeasible = false;
 
     // ---- E^T into LDS (lane c: equality c's row as column c), zero elsewhere
     for (int e = l; e < DENSE_NMAX * LDS_S; e += 64) s.et[e] = 0.0;
@@ -208,18 +214,33 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     if (l < me) {
         double v = 0.0;
         for (int k = eptr[l]; k < eptr[l + 1]; k++) v = fma(eval[k], s.xp[ecol[k]], v);
-        if (fabs(v - erhs[l]) > kFeasTol) infeasible = true;
+        if (fabs(v - erhs[l]) > kFeasTol) eq_infeasible = true;
     }
-    // ---- Hs Z and Hs xp from H's nonzeros (Hs = (H + H^T) / 2; LDS atomics)
-    for (int e = l; e < nh; e += 64) {
-        const int i = hidx[e] / n, j = hidx[e] % n;
-        const double hv = 0.5 * hval[e];
-        atomicAdd(&s.hx[i], hv * s.xp[j]);
-        atomicAdd(&s.hx[j], hv * s.xp[i]);
-        for (int b = 0; b < nz && b < DENSE_NZ; b++) {
-            atomicAdd(&s.hz[i * DENSE_NZ + b], hv * s.z[j * DENSE_NZ + b]);
-            atomicAdd(&s.hz[j * DENSE_NZ + b], hv * s.z[i * DENSE_NZ + b]);
+    // ---- Hs Z and Hs xp from H's nonzeros (Hs = (H + H^T) / 2): lane l sums row l over the
+    // nonzeros in their packed order (every lane scans the list; a fixed summation order, so the
+    // result does not depend on how the hardware orders LDS atomics)
+    if (l < n) {
+        double hxl = 0.0, hzl[DENSE_NZ];
+#pragma unroll
+        for (int b = 0; b < DENSE_NZ; b++) hzl[b] = 0.0;
+        for (int e = 0; e < nh; e++) {
+            const int i = hidx[e] / n, j = hidx[e] - (hidx[e] / n) * n;
+            if (i != l && j != l) continue;
+            const double hv = 0.5 * hval[e];
+            if (i == l) {
+                hxl = fma(hv, s.xp[j], hxl);
+#pragma unroll
+                for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[j * DENSE_NZ + b], hzl[b]);
+            }
+            if (j == l) {
+                hxl = fma(hv, s.xp[i], hxl);
+#pragma unroll
+                for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[i * DENSE_NZ + b], hzl[b]);
+            }
         }
+        s.hx[l] = hxl;
+#pragma unroll
+        for (int b = 0; b < DENSE_NZ; b++) s.hz[l * DENSE_NZ + b] = hzl[b];
     }
     __syncthreads();
     // P = 2 Z^T Hs Z (lane a * 8 + b), q = Z^T (2 Hs xp + c), k0 (objective constant: unused,
@@ -319,6 +340,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         cnt += __popcll(msk);
     }
     infeasible = __ballot(infeasible) != 0ull;
+    eq_infeasible = __ballot(eq_infeasible) != 0ull;
     // ---- expansion data and the decision
     double* zx = a.zx + (size_t)qi * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX);
     for (int e = l; e < DENSE_NMAX * DENSE_NZ; e += 64) zx[e] = s.z[e];
@@ -326,7 +348,8 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     if (l < DENSE_NZ) a.y[(size_t)qi * DENSE_NZ + l] = 0.0;  // (the PDIP overwrites it when it solves)
     if (l == 0) {
         int st = RS_SOLVE;
-        if (nz > DENSE_NZ) st = RS_CAP_NZ;
+        if (eq_infeasible) st = ST_INFEASIBLE;  // (before the capacity checks: as the host path did)
+        else if (nz > DENSE_NZ) st = RS_CAP_NZ;
         else if (cnt > DENSE_ROWS) st = RS_CAP_ROWS;
         else if (infeasible) st = ST_INFEASIBLE;
         else if (nz == 0) st = ST_OPTIMAL;  // x = xp is the only point
@@ -391,7 +414,7 @@ __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
 __global__ void __launch_bounds__(64) dense_expand_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int l = threadIdx.x;
-    if (qi >= a.count || a.status[qi] != ST_OPTIMAL) return;
+    if (qi >= a.count || a.status[qi] != ST_OPTIMAL || a.hostred[qi]) return;  // (host-reduced: host expands)
     __shared__ double xs[DENSE_NMAX];
     const int32_t* ib = a.ints + a.off_i[qi];
     const double* db = a.dbl + a.off_d[qi];
@@ -609,12 +632,25 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     parallel_for(count, [&](int k0, int k1) {
         for (int k = k0; k < k1; k++) plan[k] = plan_qp(qps[k]);
     });
-    for (int k = 0; k < count; k++) {  // the first bad QP's error, as a serial pass would report
+    for (int k = 0; k < count; k++)  // the first bad QP's error, as a serial pass would report
         if (!plan[k].err.empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + plan[k].err);
-        if (plan[k].cap)
-            return set_error(MPCCBF_ERR_CAPACITY, "QP " + std::to_string(k) + ": " + std::to_string(plan[k].n) +
-                                                      " variables / " + std::to_string(plan[k].me) +
-                                                      " equalities exceed the device elimination (64 / 64)");
+    // QPs beyond the device elimination (more than 64 variables or 64 equality rows): the equality
+    // elimination on the host (host/dense_qp.cpp), the reduced QP solved on the device like the rest
+    std::vector<int32_t> hostred(count, 0);
+    std::vector<int> big;
+    std::vector<ReducedQP> hred;
+    for (int k = 0; k < count; k++)
+        if (plan[k].cap) {
+            hostred[k] = 1;
+            big.push_back(k);
+        }
+    hred.resize(big.size());
+    for (size_t b = 0; b < big.size(); b++) {
+        try {
+            hred[b] = reduce_dense_qp(qps[big[b]]);
+        } catch (const std::exception& ex) {
+            return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(big[b]) + ": " + ex.what());
+        }
     }
     std::vector<int64_t> off_d(count), off_i(count);
     size_t nd = 0, ni = 0;
@@ -648,7 +684,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     const size_t b_obj = align16((size_t)count * sizeof(double));
     const size_t b_int = align16((size_t)count * sizeof(int32_t));
     const size_t in_bytes = b_d + b_i + 2 * b_off;
-    const size_t need = in_bytes + b_red + b_zx + b_y + b_x + b_obj + 4 * b_int;
+    const size_t need = in_bytes + b_red + b_zx + b_y + b_x + b_obj + 5 * b_int;
     e = g_dense_buf.reserve(need, device);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP buffers: ") + hipGetErrorString(e));
     char* base = (char*)g_dense_buf.p;
@@ -673,14 +709,58 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     a.m = (int32_t*)(p + b_int);
     a.pd = (int32_t*)(p + 2 * b_int);
     a.iters = (int32_t*)(p + 3 * b_int);
+    int32_t* d_hostred = (int32_t*)(p + 4 * b_int);
+    a.hostred = d_hostred;
     a.maxit = 100;
     a.tol = 1e-9;
     a.feas_tol = 1e-6;
     hipStream_t s = nullptr;
     e = hipMemcpyAsync(base, hb, in_bytes, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_hostred, hostred.data(), count * sizeof(int32_t), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
+    }
+    // host-reduced QPs: their reduced form in the device layout (P, LP padded with the identity, q,
+    // the Newton ridge when P is only semidefinite, rows [g | lo | hi]) and the decision
+    std::vector<std::vector<double>> hblk(big.size());
+    std::vector<int32_t> hst(big.size()), hm(big.size()), hpd(big.size());
+    for (size_t b = 0; b < big.size() && e == hipSuccess; b++) {
+        const ReducedQP& r = hred[b];
+        int st_b = RS_SOLVE;
+        if (r.status == MPCCBF_INFEASIBLE) st_b = MPCCBF_INFEASIBLE;
+        else if (r.nz > DENSE_NZ) st_b = RS_CAP_NZ;
+        else if (r.m > DENSE_ROWS) st_b = RS_CAP_ROWS;
+        else if (r.status >= 0) st_b = r.status;  // (nz = 0: x = xp)
+        std::vector<double>& blk = hblk[b];
+        blk.assign(DQ_STRIDE, 0.0);
+        double pmax = 0.0;
+        if (st_b == RS_SOLVE) {
+            for (int i = 0; i < DENSE_NZ; i++)
+                for (int j = 0; j < DENSE_NZ; j++) {
+                    const bool in = i < r.nz && j < r.nz;
+                    blk[i * DENSE_NZ + j] = in ? r.P(i, j) : (i == j ? 1.0 : 0.0);
+                    blk[DENSE_NZ * DENSE_NZ + i * DENSE_NZ + j] =
+                        (in && r.pd) ? (j <= i ? r.LP(i, j) : 0.0) : (i == j ? 1.0 : 0.0);
+                    if (in) pmax = std::max(pmax, std::fabs(r.P(i, j)));
+                }
+            for (int i = 0; i < r.nz; i++) blk[2 * DENSE_NZ * DENSE_NZ + i] = r.q[i];
+            blk[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ] = r.pd ? 0.0 : 1e-10 * std::max(1.0, pmax);
+            for (int k = 0; k < r.m; k++) {
+                double* row = &blk[DQ_HDR + (size_t)k * DQ_ROW];
+                for (int j = 0; j < r.nz; j++) row[j] = r.G(k, j);
+                row[DENSE_NZ] = r.lo[k];
+                row[DENSE_NZ + 1] = r.hi[k];
+            }
+        }
+        hst[b] = st_b;
+        hm[b] = std::min(r.m, DENSE_ROWS);
+        hpd[b] = r.pd ? 1 : 0;
+        const int k = big[b];
+        e = hipMemcpyAsync(a.red + (size_t)k * DQ_STRIDE, blk.data(), DQ_STRIDE * sizeof(double), hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(a.status + k, &hst[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(a.m + k, &hm[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(a.pd + k, &hpd[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
     }
     if (e == hipSuccess) {
         hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, DQ_R>), dim3(count), dim3(64), 0, s, a);
@@ -695,19 +775,33 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     if (e == hipSuccess) e = hipMemcpyAsync(st.data(), a.status, count * sizeof(int32_t), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(obj.data(), a.obj, count * sizeof(double), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipMemcpyAsync(x.data(), a.x, x.size() * sizeof(double), hipMemcpyDeviceToHost, s);
+    std::vector<double> yb(big.size() * DENSE_NZ);
+    for (size_t b = 0; b < big.size() && e == hipSuccess; b++)
+        e = hipMemcpyAsync(&yb[b * DENSE_NZ], a.y + (size_t)big[b] * DENSE_NZ, DENSE_NZ * sizeof(double),
+                           hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP solve: ") + hipGetErrorString(e));
+    // host-reduced QPs: x = xp + Z y and the full-space objective
+    std::vector<std::vector<double>> xbig(big.size());
+    for (size_t b = 0; b < big.size(); b++) {
+        const int k = big[b];
+        if (st[k] != MPCCBF_OPTIMAL) continue;
+        xbig[b].resize(qps[k].n);
+        expand_solution(hred[b], &yb[b * DENSE_NZ], xbig[b].data(), &obj[k]);
+    }
     for (int k = 0; k < count; k++)
         if (st[k] == RS_CAP_NZ || st[k] == RS_CAP_ROWS)
             return set_error(MPCCBF_ERR_CAPACITY, "QP " + std::to_string(k) +
                                                       (st[k] == RS_CAP_NZ ? ": reduced dimension exceeds 8"
                                                                           : ": reduced rows exceed 256"));
     // outputs: x only for OPTIMAL (Solver.h:33-35)
+    size_t bi = 0;
     for (int k = 0; k < count; k++) {
         status_out[k] = st[k];
         if (obj_out) obj_out[k] = st[k] == MPCCBF_OPTIMAL ? obj[k] : __builtin_nan("");
-        if (st[k] == MPCCBF_OPTIMAL && x_out && x_out[k])
-            std::memcpy(x_out[k], &x[(size_t)k * DENSE_NMAX], (size_t)qps[k].n * sizeof(double));
+        const double* xs = &x[(size_t)k * DENSE_NMAX];
+        if (hostred[k]) xs = xbig[bi++].data();
+        if (st[k] == MPCCBF_OPTIMAL && x_out && x_out[k]) std::memcpy(x_out[k], xs, (size_t)qps[k].n * sizeof(double));
     }
     return MPCCBF_OK;
 }

@@ -321,6 +321,110 @@ __device__ double lane_slack_weight(const DevOps& op, const ImpcArgs& args, cons
     return jn >= 0 ? op.slack_cost * pow(op.slack_decay, (double)rank) : 1.0;
 }
 
+// Slack-pattern active set of the collision slack mode (ConnectivityIMPCCBF.cpp:73-119,
+// MPCCBFQPGeneratorBase.cpp:28-130; the FoV kernel's run_patterns on the separable layout). Lane l
+// owns neighbour l's slack v_l >= 0 (cost w) and its CBF rows g_c y - v_l <= h_c (slots c with
+// ccv = 1). A pattern fixes per lane either v_l = 0 (lead = -1: its rows hard, g_c y <= h_c) or a
+// leader slot l with v_l = g_l y - h_l >= 0: w g_l joins the linear term, the other rows become
+// (g_c - g_l) y <= h_c - h_l and the leader's own row the bound -g_l y <= -h_l. Each pattern is a
+// strictly convex QP in y alone, solved exactly by sep_dual_as; it is the slack QP's optimum when
+// every lane's multipliers are consistent — v_l = 0: the rows' multipliers sum to at most w
+// (stationarity in v, the bound's multiplier w - sum >= 0); led: the leader row's implied
+// multiplier w - sum(others) - mu >= 0 (mu: the bound's). Otherwise a lane over its cost takes its
+// largest-multiplier row as leader, a led lane with a negative leader multiplier its other active
+// row; a pattern without a feasible point lets the unreachable candidate's row lead when that is a
+// CBF row of a lane without a leader. lead: per lane, in (the first pattern) and out. Returns 1 with
+// yo, vo (this lane's slack), the residuals and the summed steps; 0: no consistent pattern found
+// (the caller's PDIP solves). mult: 16 doubles of the group's LDS (sep_dual_as's multipliers).
+template <int G, int SB, int CB>
+__device__ int sep_slack_patterns(const SepRows<SB, CB>& rw, double w, int& lead, const double* __restrict__ P,
+                                  const double* __restrict__ Pinv, const double (&q)[SEP_NZ], double tol,
+                                  int maxstep, int npat, double* pol, double* mult, double (&yo)[SEP_NZ], double& vo,
+                                  double& rp_out, double& rd_out, int& steps) {
+    const int gl = lane_bits_opaque<G - 1>();
+    constexpr int SCBF = 2 * SEP_D * SB;  // first CBF side index (sep_stage_side)
+    steps = 0;
+    for (int pat = 0; pat < npat; pat++) {
+        double g4[4] = {0.0, 0.0, 0.0, 0.0}, hl = 0.0;
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            if (c != lead) continue;
+#pragma unroll
+            for (int j = 0; j < 4; j++) g4[j] = rw.cg[c][j];
+            hl = rw.chi[c];
+        }
+        SepRows<SB, CB> rp = rw;
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            if (lead < 0 || rw.ccv[c] == 0.0) continue;  // (inert slots stay inert)
+            const double keep = c == lead ? 0.0 : 1.0;  // leader: -g_l; others: g_c - g_l
+#pragma unroll
+            for (int j = 0; j < 4; j++) rp.cg[c][j] = fma(keep, rw.cg[c][j], -g4[j]);
+            rp.chi[c] = fma(keep, rw.chi[c], -hl);
+        }
+        double qa[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) qa[j] = lead >= 0 ? w * g4[j] : 0.0;
+        grp_sum_vec<G, 4>(qa);
+        double qp[SEP_NZ], yu[SEP_NZ], yg[SEP_NZ], rpg = 0.0, rdg = 0.0, tl = 0.0;
+#pragma unroll
+        for (int j = 0; j < SEP_NZ; j++) qp[j] = j < 4 ? q[j] + qa[j] : q[j];
+#pragma unroll
+        for (int d = 0; d < SEP_D; d++) {
+            const int o = 2 * d;
+            yu[o] = -fma(Pinv[3 * d], qp[o], Pinv[3 * d + 1] * qp[o + 1]);
+            yu[o + 1] = -fma(Pinv[3 * d + 1], qp[o], Pinv[3 * d + 2] * qp[o + 1]);
+        }
+        int st = 0;
+        const int r = sep_dual_as<G, SB, CB>(rp, true, P, Pinv, qp, yu, tol, maxstep, pol, yg, rpg, rdg, st, nullptr,
+                                             true, tl, nullptr, 0, nullptr, nullptr, mult);
+        steps += st;
+        if (r == 0) return 0;
+        if (r < 0) {
+            // no feasible point with this pattern: the unreachable candidate's row leads its lane
+            const int id = (int)pol[POL_K * 16 + POL_ID];
+            const int s = id >> 4, ln = id & 15;
+            if (s < SCBF || __shfl(lead, ln, G) >= 0) return 0;
+            wave_lds_sync();
+            if (gl == ln) lead = s - SCBF;
+            continue;
+        }
+        // per lane: multipliers of its rows (lam) and of its leader's bound (mu)
+        const int k = (int)mult[7];
+        double lam = 0.0, mu = 0.0, best = -1.0;
+        int pick = -1;
+        for (int a = 0; a < k; a++) {
+            const int id = (int)mult[8 + a];
+            const int s = id >> 4;
+            if ((id & 15) != gl || s < SCBF) continue;
+            const int c = s - SCBF;
+            const double ua = mult[a];
+            if (c == lead) {
+                mu += ua;
+            } else {
+                lam += ua;
+                if (ua > best) best = ua, pick = c;
+            }
+        }
+        const bool bad = lead < 0 ? !(lam <= w) : !(w - lam - mu >= 0.0);
+        wave_lds_sync();  // (mult is rewritten by the next pattern)
+        if (grp_ballot<G>(bad) == 0ull) {
+#pragma unroll
+            for (int j = 0; j < SEP_NZ; j++) yo[j] = yg[j];
+            double t = -hl;
+#pragma unroll
+            for (int j = 0; j < 4; j++) t = fma(g4[j], yg[j], t);
+            vo = lead >= 0 ? fmax(t, 0.0) : 0.0;
+            rp_out = rpg;
+            rd_out = rdg;
+            return 1;
+        }
+        if (grp_ballot<G>(bad && pick < 0) != 0ull) return 0;
+        if (bad) lead = pick;
+    }
+    return 0;
+}
+
 // state row `row` of the batch (re-read where needed instead of held in registers)
 __device__ __forceinline__ void load_state_lds(const double* s0k, double (&s)[6]) {
     wave_lds_sync();  // (written by lanes 0..5 of the group)
@@ -584,7 +688,29 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
             bool certified = false, infeas = false;
             double tstar = 0.0;
             PdipOut po{ST_UNKNOWN, 0};
-            for (;;) {
+            // slack mode: the slack-pattern active set first (every slack at zero, then leader
+            // rows); the PDIP below only when it finds no consistent pattern
+            bool pattern_done = false;
+            double* pat_mult = SLACK ? stage + sep_pol_doubles<SB, CB>() : nullptr;
+            if constexpr (SLACK) {
+                if (op.dual_as > 0 && live) {
+                    int lead = -1, pst = 0;
+                    double yg[NZ], vg = 0.0, rpg = 0.0, rdg = 0.0;
+                    if (sep_slack_patterns<G, SB, CB>(rw, wslack, lead, opp(buf, op.o_Pr), opp(buf, op.o_Pinv), q,
+                                                      op.tol, 2 * op.dual_as, 8, stage, pat_mult, yg, vg, rpg, rdg,
+                                                      pst)) {
+#pragma unroll
+                        for (int j = 0; j < NZ; j++) y[j] = yg[j];
+                        vslack = vg;
+                        po = PdipOut{ST_OPTIMAL, 0};
+                        po.rp = rpg;
+                        po.rd = rdg;
+                        pattern_done = true;
+                    }
+                    total += pst;
+                }
+            }
+            for (; !pattern_done;) {
                 PdipCfg ca = cfg;
                 ca.early_it = attempt == 0 ? op.early_it : 0;
                 ca.fast_start = op.fast_start != 0;
@@ -632,6 +758,38 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 else if (attempt < 2) attempt = 2;
                 else break;
             }
+            if constexpr (SLACK) {
+                // the slack PDIP's point fixes a pattern — a lane with v > 0 leads with its row of
+                // largest excess g y - h — and one active-set solve of it (plus one exchange)
+                // returns the exact optimum, which replaces the interior point's when consistent
+                // (also a PDIP that stalled short of its tolerance: round 3's UNKNOWN all-neighbour
+                // slack QPs)
+                if (!pattern_done && !infeas && op.dual_as > 0 && live) {
+                    int lead = -1;
+                    double best = -1e300;
+#pragma unroll
+                    for (int c = 0; c < CB; c++) {
+                        double t = -rw.chi[c];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
+                        if (rw.ccv[c] != 0.0 && t > best) best = t, lead = c;
+                    }
+                    if (!(vslack > 1e-9)) lead = -1;
+                    int pst = 0;
+                    double yg[NZ], vg = 0.0, rpg = 0.0, rdg = 0.0;
+                    if (sep_slack_patterns<G, SB, CB>(rw, wslack, lead, opp(buf, op.o_Pr), opp(buf, op.o_Pinv), q,
+                                                      op.tol, 2 * op.dual_as, 2, stage, pat_mult, yg, vg, rpg, rdg,
+                                                      pst)) {
+#pragma unroll
+                        for (int j = 0; j < NZ; j++) y[j] = yg[j];
+                        vslack = vg;
+                        po.status = ST_OPTIMAL;
+                        po.rp = rpg;
+                        po.rd = rdg;
+                    }
+                    total += pst;
+                }
+            }
             st = po.status;
             nit = total + tr_p1;  // active-set, PDIP and phase-1 steps
             prs = st == ST_INFEASIBLE ? tstar : po.rp;
@@ -675,7 +833,8 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     // CBF-row staging, reused as the dual active set's scratch (sep_pol_doubles)
     constexpr int STAGE = CB * 16 * (SEP_NZ + 1) > sep_pol_doubles<SB, CB>() ? CB * 16 * (SEP_NZ + 1)
                                                                              : sep_pol_doubles<SB, CB>();
-    __shared__ double stage_all[GPB][SLACK ? 1 : STAGE];
+    // (slack mode: the slack-pattern active set's scratch + its multipliers, sep_slack_patterns)
+    __shared__ double stage_all[GPB][SLACK ? sep_pol_doubles<SB, CB>() + 16 : STAGE];
     __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
     // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
@@ -758,8 +917,9 @@ bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k) { return csr ||
 // Whether launch_impc defers agents (so launch_impc_fallback must follow): the lean main launch
 // always may; the full separable kernel when its 16 CBF row slots can be exceeded.
 bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k) {
-    if (op.slack_mode)
-        return op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2 && (csr || knn_k > 16);
+    // slack mode: more than 16 neighbours only from caller lists (grid mode takes knn_k <= 16,
+    // impc_enqueue)
+    if (op.slack_mode) return op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2 && csr;
     if (sep_lean(op, variant)) return true;
     if (!(variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)) return false;
     return impc_rows_may_exceed(op, csr, knn_k);

@@ -152,7 +152,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
                                const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], int k,
                                const double* __restrict__ pol, const double (&sc)[2 * SEP_D * SB + CB],
                                double tol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
-                               SepWarm<SB>* warm) {
+                               SepWarm<SB>* warm, double* __restrict__ mult = nullptr) {
     const int gl = lane_bits_opaque<G - 1>();
     using S6 = Sym<POL_K>;
     double K[S6::P], rhs[POL_K], dk[POL_K], lam[POL_K];
@@ -244,6 +244,16 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
                     warm->zl(d, kk) = fmax(ml, 0.0);
                     warm->zu(d, kk) = fmax(mu, 0.0);
                 }
+        }
+        if (mult != nullptr) {  // the active sides' multipliers (>= 0) and ids (sep_dual_as)
+            double ui = 0.0;
+#pragma unroll
+            for (int i = 0; i < POL_K; i++) ui = gl == i ? pol[(i < k ? i : 0) * 16 + POL_SGN] * lam[i] : ui;
+            if (gl < k) {
+                mult[gl] = ui;
+                mult[8 + gl] = pol[gl * 16 + POL_ID];
+            }
+            if (gl == 0) mult[7] = (double)k;
         }
     }
     wave_lds_sync();  // the scratch is reused
@@ -369,7 +379,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                            double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
                            int& steps, SepWarm<SB>* warm, bool want_rd, double& tlow,
                            long long* dbg = nullptr, int k0 = 0, const double* __restrict__ warm_ids = nullptr,
-                           double* __restrict__ save = nullptr) {
+                           double* __restrict__ save = nullptr, double* __restrict__ mult = nullptr) {
     static_assert(G == 16, "rows of pol are copied one column per lane");
     (void)dbg;
     GSTAMP(0, true);
@@ -767,7 +777,8 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     };
     if (!(rd <= tol)) {
         // rounding accumulated over the steps: the active set's equality QP, re-solved exactly
-        const bool ok = sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm);
+        const bool ok = sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm,
+                                                        mult);
         if (ok) save_sides();
         wave_lds_sync();
         return ok ? 1 : 0;
@@ -794,6 +805,17 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             }
     }
     save_sides();
+    if (mult != nullptr) {  // mult[0 .. k): the active sides' multipliers (>= 0), mult[7] = k,
+                            // mult[8 .. 8 + k): their side ids (POL_ID)
+        double ui = 0.0;
+#pragma unroll
+        for (int i = 0; i < POL_K; i++) ui = gl == i ? u[i] : ui;
+        if (gl < k) {
+            mult[gl] = ui;
+            mult[8 + gl] = pol[gl * 16 + POL_ID];
+        }
+        if (gl == 0) mult[7] = (double)k;
+    }
     wave_lds_sync();  // the scratch is reused
     GSTAMP(10, true);
     return 1;

@@ -378,12 +378,16 @@ def knn_list(states, i, k, radius):
 
 
 def closed_loop_gauss_seidel(cfg: dict, states, targets, steps, k=8, radius=6.0, pos_std=0.0, vel_std=0.0,
-                             seed=0, neighbours="knn"):
+                             seed=0, neighbours="knn", inputs=None):
     """MPCCBFFormationControl_example.cpp:131-226 restated in its own order: per control step the
     robots in index order (:140), each optimize()d against the current table (robots before it
     already moved, :201), the kept curve (last successful trajectory, :150-165) evaluated int(h/Ts)
     sub-steps ahead with the noise (:188-207), or the position held at zero velocity (:208-221).
-    Returns (trace: steps+1 x n x 6 states after each step, status: steps x n x impc_iter)."""
+    Returns (trace: steps+1 x n x 6 states after each step, status: steps x n x impc_iter).
+    inputs (a trace of another run, steps+1 x n x 6): robot i of step s plans from that run's table
+    as it stood at its turn — robots < i at inputs[s+1], the others at inputs[s] — instead of this
+    loop's own: every update checked on the same inputs, without the amplification a free-running
+    comparison accumulates through the CBF rows (Bc is cubic in the distance margin)."""
     p = make_params(cfg)
     n = len(states)
     cur = np.array(states, dtype=np.float64)
@@ -394,10 +398,13 @@ def closed_loop_gauss_seidel(cfg: dict, states, targets, steps, k=8, radius=6.0,
     xs = [None] * n
     traj_t = np.full(n, -1.0)
     trace = [cur.copy()]
+    own = cur.copy()
     stats = []
     for s in range(steps):
         st = np.full((n, cfg["impc_iter"]), UNKNOWN, dtype=np.int32)
         for i in range(n):
+            if inputs is not None:
+                cur = np.concatenate([inputs[s + 1][:i], inputs[s][i:]]).astype(np.float64)
             nb = (np.array([j for j in range(n) if j != i], dtype=np.int32) if neighbours == "all"
                   else knn_list(cur, i, k, radius))
             r = impc_optimize(p, cur, i, nb, refs[i])
@@ -424,6 +431,11 @@ def closed_loop_gauss_seidel(cfg: dict, states, targets, steps, k=8, radius=6.0,
                         v = v + dn if c < 3 else dn
                     nxt[c] = v
             cur[i] = nxt
-        trace.append(cur.copy())
+            if inputs is not None:
+                own[i] = nxt
+        if inputs is not None:
+            trace.append(own.copy())
+        else:
+            trace.append(cur.copy())
         stats.append(st)
     return np.array(trace), np.array(stats)

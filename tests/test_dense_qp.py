@@ -165,3 +165,41 @@ def test_dense_inconsistent_and_dependent_equalities(mpclib):
     np.testing.assert_allclose([x[0] + x[1], x[1] + x[2]], [1.0, 1.0], atol=1e-10)
     # min |x|^2 on the two planes: x = (1/3, 2/3, 1/3)
     np.testing.assert_allclose(x, [1 / 3, 2 / 3, 1 / 3], atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_dense_beyond_device_elimination_capacity(mpclib, oracle):
+    """QPs beyond the device elimination's 64 variables / 64 equality rows are reduced on the host
+    (host/dense_qp.cpp) and solved by the same device interior-point kernel, in one batch with a
+    device-reduced QP: 80 variables with 74 equality rows and 2 fixed variables (reduced dimension
+    4), and 40 variables with 70 equality rows of rank 34 (36 consistent combinations: reduced
+    dimension 6, the same optimum as its 34 independent rows), against the oracle. Inconsistent
+    equalities with a reduced dimension above 8 are INFEASIBLE, not a capacity error (the equality
+    decision precedes the capacity checks), on the device path (30 variables) and the host path (90)."""
+    rng = np.random.default_rng(29)
+    big = _random_qp(rng, 80, 74, 40, 0, 2)
+    small = _random_qp(rng, 12, 5, 20, 0, 1)
+    indep = _random_qp(rng, 40, 34, 30, 0, 0)
+    eq = indep["lo"] == indep["hi"]
+    E, b = indep["A"][eq], indep["lo"][eq]
+    W = rng.normal(size=(36, E.shape[0]))
+    dep = dict(indep, A=np.vstack([indep["A"], W @ E]), lo=np.concatenate([indep["lo"], W @ b]),
+               hi=np.concatenate([indep["hi"], W @ b]))
+    st, xs, obj = mpclib.dense_qp_solve_batch([big, small, dep])
+    for k, q in enumerate((big, small, indep)):
+        r = oracle.solve_dense_qp(dict(n=q["c"].shape[0], H=q["H"], c=q["c"], c0=q["c0"], A=q["A"], lo=q["lo"],
+                                       hi=q["hi"], vlo=q["vlo"], vhi=q["vhi"]))
+        assert st[k] == r["status"] == mpclib.OPTIMAL, (k, st[k], r["status"])
+        assert abs(obj[k] - r["obj"]) <= 1e-6 * max(1.0, abs(r["obj"])), (k, obj[k], r["obj"])
+        np.testing.assert_allclose(xs[k], r["x"], atol=1e-5)
+    # inconsistent equalities (a row repeated with its right-hand side + 1), reduced dimension 20
+    for n in (30, 90):
+        q = _random_qp(rng, n, 10, 5, 0, 0)
+        eqm = q["lo"] == q["hi"]
+        row, rhs = q["A"][eqm][0], q["lo"][eqm][0] + 1.0
+        extra = 1 if n <= 64 else 60  # (beyond 64 equality rows too on the host path)
+        q["A"] = np.vstack([q["A"]] + [row[None, :]] * extra)
+        q["lo"] = np.concatenate([q["lo"], np.full(extra, rhs)])
+        q["hi"] = np.concatenate([q["hi"], np.full(extra, rhs)])
+        st, xs, _ = mpclib.dense_qp_solve_batch([q])
+        assert st[0] == mpclib.INFEASIBLE and xs[0] is None, (n, st[0])
