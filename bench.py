@@ -66,6 +66,8 @@ def parse():
                          "BezierIMPCCBFPFXYYaw_example.cpp:138-142,201-202)")
     ap.add_argument("--slack-decay", type=float, default=0.9)
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--das-warm", type=int, default=0,
+                    help="mpccbf_options.das_warm_steps (0 = default 3; < 0 = no IMPC iteration-1 warm start)")
     ap.add_argument("--cpu-baseline-agents", type=int, default=-1,
                     help="agents in the CPU-oracle sample (default: sized for ~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -254,7 +256,7 @@ def main():
     # neighbour-estimate covariances (FoV slack weights): the FoV example's 0.1 I for everyone
     cov_h = np.tile([0.1, 0.0, 0.1], (total, 1)) if (fov and args.slack) else None
     cov = None if cov_h is None else torch.tensor(cov_h, dtype=torch.float64, device=dev)
-    ctx = Context(cfg, device=local)
+    ctx = Context(cfg, device=local, das_warm_steps=args.das_warm)
     ctx.set_variant(args.variant)
 
     targets = torch.tensor(targets_h[first:first + per], dtype=torch.float64, device=dev)

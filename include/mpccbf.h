@@ -163,9 +163,10 @@ int mpccbf_num_shared_rows(const mpccbf_ctx* ctx);
  *   next_states num_agents x 6: position/velocity of the kept curve at t = h (Jacobi update of
  *               the closed-loop driver, example :188-207, without noise); unchanged input if no
  *               curve was found.
- *   stamps      diagnostics, normally NULL: num_agents x 8 int64 shader-clock stamps (s_memtime)
+ *   stamps      diagnostics, normally NULL: num_agents x 8 int64 wall-clock stamps (s_memrealtime)
  *               at the kernel's phase boundaries (start, setup, neighbours, CBF rows 0, solve 0,
- *               CBF rows 1, solve 1, end).
+ *               CBF rows 1, solve 1, end) — written by the diagnostics builds only (make stamps /
+ *               prof); the release library compiles the stamp code out and ignores the pointer.
  *   nb_out      diagnostics, normally NULL (ABI 10): num_agents x 16 int32, the neighbour list each
  *               agent's QPs were built from, in the kernel's order (grid mode: the in-kernel query's
  *               k nearest, sorted by index; CSR: the given list), -1 after the last; lists longer

@@ -42,7 +42,6 @@ constexpr int DENSE_EMAX = 64;     // equalities per QP (lane = equality)
 constexpr int DQ_R = DENSE_ROWS / 64;
 constexpr int DQ_HDR = 2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 2;  // P, LP, q, reg, pad
 constexpr int DQ_ROW = DENSE_NZ + 2;                            // g, lo, hi
-constexpr int DQ_STRIDE = DQ_HDR + DENSE_ROWS * DQ_ROW;        // reduced QP, doubles
 constexpr double kInf = 1e300;     // |bound| >= 1e300 means "absent" (numeric_limits lowest/max)
 constexpr double kFeasTol = 1e-6;  // CPLEX default feasibility tolerance (CPLEX.cpp:8 default ctor)
 // reduce-kernel statuses beyond qpcpp::SolveStatus: -1 = the PDIP solves it; capacity errors
@@ -57,7 +56,8 @@ struct DenseBatch {
     const int64_t* off_d;  // per QP
     const int64_t* off_i;
     int32_t count;
-    double* red;      // count x DQ_STRIDE reduced QPs (the PDIP's input)
+    double* red;      // reduced QPs (the PDIP's input), QP k at red + red_off[k]: header + its rows
+    const int64_t* red_off;  // per QP, sized by its inequality-row count (<= DENSE_ROWS rows)
     double* zx;       // count x (DENSE_NMAX x DENSE_NZ + DENSE_NMAX): Z row-major, then xp
     int32_t* status;  // count: decided status or RS_*
     int32_t* m;       // count: reduced rows
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     const double* ilo = eval + eptr[me];
     const double* ihi = ilo + mi;
     const double* ival = ihi + mi;
-    double* red = a.red + (size_t)qi * DQ_STRIDE;
+    double* red = a.red + a.red_off[qi];
     // inconsistent equalities (decided whatever the reduced dimension) / a constant row violated
     // (decided only within capacity: beyond it the rows' reduced coefficients are not all formed)
     bool infeasible = false, eq_infeasible = false;
@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int gl = threadIdx.x;
     if (qi >= a.count || a.status[qi] != RS_SOLVE) return;  // decided by the reduction
-    const double* base = a.red + (size_t)qi * DQ_STRIDE;
+    const double* base = a.red + a.red_off[qi];
     const double* P = base;
     const double* LP = base + NZ * NZ;
     const double* qv = base + 2 * NZ * NZ;
@@ -599,6 +599,13 @@ void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, int32_t*
     }
 }
 
+// reduced row count of host-reduced QP k (its index in `big`)
+int hred_rows(const std::vector<ReducedQP>& hred, const std::vector<int>& big, int k) {
+    for (size_t b = 0; b < big.size(); b++)
+        if (big[b] == k) return hred[b].m;
+    return 0;
+}
+
 template <typename F>
 void parallel_for(int count, F f) {
     const int nthr = count >= 64 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
@@ -677,14 +684,24 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         for (int k = k0; k < k1; k++) pack_qp(qps[k], plan[k], h_d + off_d[k], h_i + off_i[k]);
     });
     // ---- device buffers: packed input | reduced QPs | Z, xp | y | x | obj | int outputs
-    const size_t b_red = align16((size_t)count * DQ_STRIDE * sizeof(double));
+    // reduced QPs sized by their inequality rows (the reduced rows are a subset of them; a QP with
+    // more than DENSE_ROWS is a capacity error before its rows are read): header + rows each
+    std::vector<int64_t> red_off(count);
+    size_t nred = 0;
+    for (int k = 0; k < count; k++) {
+        red_off[k] = (int64_t)nred;
+        const int rows_k = hostred[k] ? std::min(hred_rows(hred, big, k), DENSE_ROWS) : std::min(plan[k].mi, DENSE_ROWS);
+        nred += (size_t)DQ_HDR + (size_t)std::max(rows_k, 1) * DQ_ROW;  // (>= 1 row: the kernel reads row 0)
+    }
+    const size_t b_red = align16(nred * sizeof(double));
+    const size_t b_redoff = align16((size_t)count * sizeof(int64_t));
     const size_t b_zx = align16((size_t)count * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX) * sizeof(double));
     const size_t b_y = align16((size_t)count * DENSE_NZ * sizeof(double));
     const size_t b_x = align16((size_t)count * DENSE_NMAX * sizeof(double));
     const size_t b_obj = align16((size_t)count * sizeof(double));
     const size_t b_int = align16((size_t)count * sizeof(int32_t));
     const size_t in_bytes = b_d + b_i + 2 * b_off;
-    const size_t need = in_bytes + b_red + b_zx + b_y + b_x + b_obj + 5 * b_int;
+    const size_t need = in_bytes + b_red + b_redoff + b_zx + b_y + b_x + b_obj + 5 * b_int;
     e = g_dense_buf.reserve(need, device);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP buffers: ") + hipGetErrorString(e));
     char* base = (char*)g_dense_buf.p;
@@ -697,6 +714,9 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     char* p = base + in_bytes;
     a.red = (double*)p;
     p += b_red;
+    int64_t* d_redoff = (int64_t*)p;
+    a.red_off = d_redoff;
+    p += b_redoff;
     a.zx = (double*)p;
     p += b_zx;
     a.y = (double*)p;
@@ -717,6 +737,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     hipStream_t s = nullptr;
     e = hipMemcpyAsync(base, hb, in_bytes, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_hostred, hostred.data(), count * sizeof(int32_t), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_redoff, red_off.data(), count * sizeof(int64_t), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
@@ -733,7 +754,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         else if (r.m > DENSE_ROWS) st_b = RS_CAP_ROWS;
         else if (r.status >= 0) st_b = r.status;  // (nz = 0: x = xp)
         std::vector<double>& blk = hblk[b];
-        blk.assign(DQ_STRIDE, 0.0);
+        blk.assign((size_t)DQ_HDR + (size_t)std::min(r.m, DENSE_ROWS) * DQ_ROW, 0.0);
         double pmax = 0.0;
         if (st_b == RS_SOLVE) {
             for (int i = 0; i < DENSE_NZ; i++)
@@ -746,7 +767,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
                 }
             for (int i = 0; i < r.nz; i++) blk[2 * DENSE_NZ * DENSE_NZ + i] = r.q[i];
             blk[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ] = r.pd ? 0.0 : 1e-10 * std::max(1.0, pmax);
-            for (int k = 0; k < r.m; k++) {
+            for (int k = 0; k < r.m && k < DENSE_ROWS; k++) {
                 double* row = &blk[DQ_HDR + (size_t)k * DQ_ROW];
                 for (int j = 0; j < r.nz; j++) row[j] = r.G(k, j);
                 row[DENSE_NZ] = r.lo[k];
@@ -757,7 +778,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         hm[b] = std::min(r.m, DENSE_ROWS);
         hpd[b] = r.pd ? 1 : 0;
         const int k = big[b];
-        e = hipMemcpyAsync(a.red + (size_t)k * DQ_STRIDE, blk.data(), DQ_STRIDE * sizeof(double), hipMemcpyHostToDevice, s);
+        e = hipMemcpyAsync(a.red + red_off[k], blk.data(), blk.size() * sizeof(double), hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(a.status + k, &hst[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(a.m + k, &hm[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(a.pd + k, &hpd[b], sizeof(int32_t), hipMemcpyHostToDevice, s);

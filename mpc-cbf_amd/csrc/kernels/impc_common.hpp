@@ -731,12 +731,18 @@ __device__ __forceinline__ void grid_clear(const ImpcArgs& args) {
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < T; e += nthr) args.grid.clr_cnt[e] = 0u;
 }
 
-// diagnostics: wall-clock stamp (s_memrealtime, 100 MHz, chip-wide) of phase `k` of agent ai
+// diagnostics: wall-clock stamp (s_memrealtime, 100 MHz, chip-wide) of phase `k` of agent ai —
+// compiled in the diagnostics builds only (make stamps / prof: MPCCBF_STAMPS); in the release
+// kernels the stamp code kept the agent index live across the kernel and cost a 4-byte spill
 __device__ __forceinline__ void stamp(const ImpcArgs& args, int ai, int gl, int k) {
+#if defined(MPCCBF_STAMPS) || defined(MPCCBF_PDIP_STAMPS)
     if (args.stamps) {
         const long long t = (long long)__builtin_amdgcn_s_memrealtime();
         if (gl == 0) args.stamps[(size_t)ai * NSTAMP + k] = t;
     }
+#else
+    (void)args, (void)ai, (void)gl, (void)k;
+#endif
 }
 
 // diagnostics (args.nb_out): the first 16 entries of the agent's neighbour list as the kernel built

@@ -75,10 +75,10 @@ prof fov --workload fov
 prof fov_slack --workload fov --slack
 prof dense --workload dense --steps 10 --warmup 2
 step pytest; (cd $ROOT && timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/${TAG}_pytest_gpu.log 2>&1)
-step fovs status; MPCCBF_CHECK_SLACK=1 timeout -k 10 300 python3 $ROOT/tools/fov_status_check.py 1000 $OUT/${TAG}_fovs_status.npz > $OUT/${TAG}_fovs_status.log 2>&1
-step stamps; (cd $ROOT && timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1)
+step fovs status; (cd $ROOT && MPCCBF_CHECK_SLACK=1 timeout -k 10 300 python3 $ROOT/tools/fov_status_check.py 1000 $OUT/${TAG}_fovs_status.npz > $OUT/${TAG}_fovs_status.log 2>&1)
+step stamps; (cd $ROOT && MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/stamps/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1)
 step stamps pdip; (cd $ROOT && MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision_das.log 2>&1)
-step stamps fov; (cd $ROOT && WORKLOAD=fov timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov.log 2>&1)
+step stamps fov; (cd $ROOT && WORKLOAD=fov MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/stamps/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov.log 2>&1)
 step stamps fov das; (cd $ROOT && WORKLOAD=fov MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov_das.log 2>&1)
 step determinism; (cd $ROOT && timeout -k 10 200 python3 tools/determinism_loop.py 6 1 30 > $OUT/${TAG}_determinism_fovs.log 2>&1)
 echo done
