@@ -90,11 +90,32 @@ __device__ __forceinline__ double bwd_rows(const double* __restrict__ Lm, double
 // earlier kernel left in this LDS — NaN / Inf included, and 0 * NaN is NaN. That was round 3's
 // FoV-slack step-0 nondeterminism (profiles/r04_lds_poison_nan.log). (Zeroed here rather than a
 // select in the loop: the select pushed the FoV kernels from 0 / 76 to 524 / 972 B/lane of scratch.)
+// BATCH: every load first (as a loop, each element's two loads were waited for before the next's;
+// off in the FoV slack kernel, where the batch costs scratch).
+template <bool BATCH = true>
 __device__ __forceinline__ void das_load_operators(WaveAS& ws, const double* __restrict__ P,
                                                    const double* __restrict__ Pinv, int lane) {
-    for (int e = lane; e < WNZ * WNZ; e += 64) {
-        ws.Pi[(e >> 4) * 17 + (e & 15)] = Pinv[e];
-        ws.P[(e >> 4) * 17 + (e & 15)] = P[e];
+    if constexpr (!BATCH) {
+        for (int e = lane; e < WNZ * WNZ; e += 64) {
+            ws.Pi[(e >> 4) * 17 + (e & 15)] = Pinv[e];
+            ws.P[(e >> 4) * 17 + (e & 15)] = P[e];
+            ws.W[e] = 0.0;
+        }
+        wave_lds_sync();
+        return;
+    }
+    constexpr int NE = WNZ * WNZ / 64;
+    double pi[NE], pp[NE];
+#pragma unroll
+    for (int k = 0; k < NE; k++) {
+        pi[k] = Pinv[lane + 64 * k];
+        pp[k] = P[lane + 64 * k];
+    }
+#pragma unroll
+    for (int k = 0; k < NE; k++) {
+        const int e = lane + 64 * k;
+        ws.Pi[(e >> 4) * 17 + (e & 15)] = pi[k];
+        ws.P[(e >> 4) * 17 + (e & 15)] = pp[k];
         ws.W[e] = 0.0;
     }
     wave_lds_sync();

@@ -176,73 +176,114 @@ __device__ __forceinline__ int grid_neighbors_stream(const ImpcArgs& args, int s
     return nk;
 }
 
-// k nearest other agents (planar distance, ties by index) within the radius, found through the
-// spatial hash; the result is left in sc.idx sorted by agent index (sc.src: each one's slot in
-// sc.cst). Returns the count. Up to NB_CAP candidates within the radius are gathered and ranked at
-// once; beyond, grid_neighbors_stream re-runs the query without a cap. Distance-only test: agents
-// of a colliding cell that share a bucket are still filtered by distance, and a bucket reached
-// from two of the 9 cells is scanned once.
+// The neighbour query in stages, so that its dependent global round trips (the 9 cells' bucket
+// counts, then the first pass's bucket slots, then those candidates' states) can be issued between
+// the setup's own loads instead of after them: gq_begin (counts), gq_slots (the candidate list and
+// the first pass's slots), gq_states (the first pass's states), then grid_neighbors_finish.
+// The first pass covers candidates gl and G + gl (G = 16) or gl (G = 64).
 template <int G>
-__device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double py, NbScratch& sc,
-                              int gl, double yaw = 0.0) {
+struct GridQuery {
+    static constexpr int NP = G == 16 ? 2 : 1;
+    uint32_t hs[9], nc[9], off[9], total;
+    bool full;
+    int j[NP];           // first pass: raw slot entry (gq_slots), then the candidate agent (-1: none)
+    double st[NP][4];    // its (px, py, vx, vy)
+};
+
+template <int G>
+__device__ __forceinline__ void gq_begin(const ImpcArgs& args, double px, double py, GridQuery<G>& q) {
     const GridArgs& gr = args.grid;
     const long long cx = (long long)floor(px * gr.inv_cell), cy = (long long)floor(py * gr.inv_cell);
-    const double r2 = gr.radius * gr.radius;
-    // the 9 cells' buckets (a bucket reached from two cells is scanned once), concatenated: lane
-    // gl takes candidates gl, gl + G, ... of the whole list, so the dependent loads (bucket entry,
-    // then the agent's position) of all cells are in flight together
-    uint32_t hs[9], nc[9];
-    bool full = false;
 #pragma unroll
     for (int c = 0; c < 9; c++) {
-        hs[c] = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
-        nc[c] = gr.cnt[hs[c]];
-        full = full || nc[c] > (uint32_t)GRID_CAP;
+        q.hs[c] = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
+        q.nc[c] = gr.cnt[q.hs[c]];
     }
-    // a bucket that overflowed its slots: scan the whole state table instead (same result)
-    uint32_t off[9], total = 0;
+}
+
+// candidate t's entry in the slot table (entry 0 when unused: the slot loads are unconditional —
+// behind a branch, the join waited for them)
+template <int G>
+__device__ __forceinline__ uint32_t gq_entry(const GridArgs& gr, const GridQuery<G>& q, uint32_t t) {
+    uint32_t e = 0;
+#pragma unroll
+    for (int c = 0; c < 9; c++) {  // the cell whose range holds t
+        const uint32_t u = t - q.off[c];
+        e = ((q.off[c] <= t) & (u < q.nc[c])) ? u * (gr.mask + 1u) + q.hs[c] : e;
+    }
+    return (t < q.total && !q.full) ? e : 0u;
+}
+
+// candidate t's agent from its raw slot entry: the entry, or t itself when scanning the whole
+// table (-1: none)
+template <int G>
+__device__ __forceinline__ int gq_agent(const GridQuery<G>& q, uint32_t t, int raw) {
+    return t >= q.total ? -1 : (q.full ? (int)t : raw);
+}
+
+template <int G>
+__device__ __forceinline__ void gq_slots(const ImpcArgs& args, GridQuery<G>& q, int gl) {
+    // a bucket that overflowed its slots: scan the whole state table instead (same result); a
+    // bucket reached from two of the 9 cells is scanned once
+    bool full = false;
+    uint32_t total = 0;
 #pragma unroll
     for (int c = 0; c < 9; c++) {
+        full = full || q.nc[c] > (uint32_t)GRID_CAP;
         bool dup = false;
 #pragma unroll
-        for (int p = 0; p < c; p++) dup = dup || (hs[p] == hs[c]);
-        if (dup) nc[c] = 0;
-        off[c] = total;
-        total += nc[c];
+        for (int p = 0; p < c; p++) dup = dup || (q.hs[p] == q.hs[c]);
+        if (dup) q.nc[c] = 0;
+        q.off[c] = total;
+        total += q.nc[c];
     }
-    if (full) total = (uint32_t)args.num_states;
-    int cnt = 0;
-    // candidate t: its agent index (bucket slot, or t itself when scanning the whole table), state,
-    // squared distance and whether it is a neighbour (within the radius and, for the FoV
-    // controller, the cone)
-    auto load_cand = [&](uint32_t t, int& j, double& d2, double& nx, double& ny, double& nvx, double& nvy) -> bool {
-        bool keep = false;
-        j = -1;
-        d2 = 0.0;
-        nx = ny = nvx = nvy = 0.0;
-        if (t < total) {
-            if (full) {
-                j = (int)t;
-            } else {
-                uint32_t e = 0;
+    q.full = full;
+    q.total = full ? (uint32_t)args.num_states : total;
+    // every pass's entry first, then the loads (their results stay in flight until gq_states)
+    uint32_t e[GridQuery<G>::NP];
 #pragma unroll
-                for (int c = 0; c < 9; c++)  // the cell whose range holds t
-                    if (off[c] <= t && t - off[c] < nc[c]) e = (t - off[c]) * (gr.mask + 1u) + hs[c];
-                j = (int)gr.slots[e];
-            }
-            nx = args.states[(size_t)j * 6];
-            ny = args.states[(size_t)j * 6 + 1];
-            nvx = args.states[(size_t)j * 6 + 3];
-            nvy = args.states[(size_t)j * 6 + 4];
-            const double ex = nx - px;
-            const double ey = ny - py;
-            d2 = ex * ex + ey * ey;
-            keep = (j != self) && (d2 <= r2);
-            if (keep && gr.cone > 0.0) {  // inside the field of view (strict)
-                double offa = atan2(ey, ex) - yaw;
-                offa -= 6.283185307179586 * rint(offa * 0.15915494309189535);
-                keep = fabs(offa) < gr.cone;
-            }
+    for (int p = 0; p < GridQuery<G>::NP; p++) e[p] = gq_entry<G>(args.grid, q, (uint32_t)(p * G + gl));
+#pragma unroll
+    for (int p = 0; p < GridQuery<G>::NP; p++) q.j[p] = (int)args.grid.slots[e[p]];
+}
+
+template <int G>
+__device__ __forceinline__ void gq_states(const ImpcArgs& args, GridQuery<G>& q, int gl) {
+#pragma unroll
+    for (int p = 0; p < GridQuery<G>::NP; p++) {
+        q.j[p] = gq_agent<G>(q, (uint32_t)(p * G + gl), q.j[p]);
+        const size_t r = (size_t)(q.j[p] >= 0 ? q.j[p] : 0) * 6;
+        q.st[p][0] = args.states[r];
+        q.st[p][1] = args.states[r + 1];
+        q.st[p][2] = args.states[r + 3];
+        q.st[p][3] = args.states[r + 4];
+    }
+}
+
+// k nearest other agents (planar distance, ties by index) within the radius, found through the
+// spatial hash (q: the staged query's first pass, gq_*); the result is left in sc.idx sorted by
+// agent index (sc.src: each one's slot in sc.cst). Returns the count. Up to NB_CAP candidates
+// within the radius are gathered and ranked at once; beyond, grid_neighbors_stream re-runs the
+// query without a cap. Distance-only test: agents of a colliding cell that share a bucket are
+// still filtered by distance.
+template <int G>
+__device__ int grid_neighbors_finish(const ImpcArgs& args, int self, double px, double py, NbScratch& sc,
+                                     int gl, double yaw, GridQuery<G>& q) {
+    const GridArgs& gr = args.grid;
+    const double r2 = gr.radius * gr.radius;
+    const uint32_t total = q.total;
+    int cnt = 0;
+    // whether candidate j at (nx, ny) is a neighbour (within the radius and, for the FoV
+    // controller, the cone); d2: its squared distance
+    auto is_nb = [&](int j, double nx, double ny, double& d2) -> bool {
+        const double ex = nx - px;
+        const double ey = ny - py;
+        d2 = ex * ex + ey * ey;
+        bool keep = j >= 0 && (j != self) && (d2 <= r2);
+        if (keep && gr.cone > 0.0) {  // inside the field of view (strict)
+            double offa = atan2(ey, ex) - yaw;
+            offa -= 6.283185307179586 * rint(offa * 0.15915494309189535);
+            keep = fabs(offa) < gr.cone;
         }
         return keep;
     };
@@ -260,27 +301,42 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
         }
         cnt += __popcll(msk);
     };
-    if constexpr (G == 16) {
-        // two chunks per pass (candidates gl and G + gl): both chunks' dependent loads (bucket slot,
-        // then the agent's state) are in flight together — the 9 cells typically hold 17-32
-        // candidates, which took two serial round-trip pairs chunk by chunk
-        for (uint32_t t0 = 0; t0 < total; t0 += 2 * G) {
-            int ja, jb;
-            double da, xa, ya, vxa, vya, db, xb, yb, vxb, vyb;
-            const bool ka = load_cand(t0 + gl, ja, da, xa, ya, vxa, vya);
-            const bool kb = load_cand(t0 + G + gl, jb, db, xb, yb, vxb, vyb);
-            put_chunk(ka, ja, da, xa, ya, vxa, vya);
-            put_chunk(kb, jb, db, xb, yb, vxb, vyb);
+    constexpr int NP = GridQuery<G>::NP;
+    // the first pass from the staged loads
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        double d2;
+        const bool keep = is_nb(q.j[p], q.st[p][0], q.st[p][1], d2);
+        put_chunk(keep, q.j[p], d2, q.st[p][0], q.st[p][1], q.st[p][2], q.st[p][3]);
+    }
+    // the rest, NP chunks per pass: the chunks' dependent loads (bucket slot, then the agent's
+    // state) are in flight together
+    for (uint32_t t0 = NP * G; t0 < total; t0 += NP * G) {
+        int j[NP];
+        double st[NP][4];
+#pragma unroll
+        for (int p = 0; p < NP; p++) j[p] = (int)gq_entry<G>(gr, q, t0 + p * G + gl);
+#pragma unroll
+        for (int p = 0; p < NP; p++) j[p] = (int)gr.slots[(uint32_t)j[p]];
+#pragma unroll
+        for (int p = 0; p < NP; p++) j[p] = gq_agent<G>(q, t0 + p * G + gl, j[p]);
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            const size_t r = (size_t)(j[p] >= 0 ? j[p] : 0) * 6;
+            st[p][0] = args.states[r];
+            st[p][1] = args.states[r + 1];
+            st[p][2] = args.states[r + 3];
+            st[p][3] = args.states[r + 4];
         }
-    } else {
-        for (uint32_t t0 = 0; t0 < total; t0 += G) {
-            int j;
-            double d2, nx, ny, nvx, nvy;
-            const bool keep = load_cand(t0 + gl, j, d2, nx, ny, nvx, nvy);
-            put_chunk(keep, j, d2, nx, ny, nvx, nvy);
+#pragma unroll
+        for (int p = 0; p < NP; p++) {
+            double d2;
+            const bool keep = is_nb(j[p], st[p][0], st[p][1], d2);
+            put_chunk(keep, j[p], d2, st[p][0], st[p][1], st[p][2], st[p][3]);
         }
     }
-    if (cnt > NB_CAP) return grid_neighbors_stream<G>(args, self, px, py, sc, gl, yaw, hs, nc, off, total, full);
+    if (cnt > NB_CAP)
+        return grid_neighbors_stream<G>(args, self, px, py, sc, gl, yaw, q.hs, q.nc, q.off, total, q.full);
     wave_lds_sync();
     // rank by (d2, index): keep the k nearest
     const int k = gr.k;
@@ -359,6 +415,17 @@ __device__ int grid_neighbors(const ImpcArgs& args, int self, double px, double 
     return nk;
 }
 
+// the whole query in one call (no setup loads to overlap)
+template <int G>
+__device__ __forceinline__ int grid_neighbors(const ImpcArgs& args, int self, double px, double py, NbScratch& sc,
+                                              int gl, double yaw = 0.0) {
+    GridQuery<G> q;
+    gq_begin<G>(args, px, py, q);
+    gq_slots<G>(args, q, gl);
+    gq_states<G>(args, q, gl);
+    return grid_neighbors_finish<G>(args, self, px, py, sc, gl, yaw, q);
+}
+
 // ---------------------------------------------------------------------------------------------
 // Steps shared by both layouts
 // ---------------------------------------------------------------------------------------------
@@ -419,6 +486,81 @@ __device__ __forceinline__ void agent_linear_term(const DevOps& op, const double
     }
 }
 
+// agent_linear_term spread over the group's lanes: lane i < NZ forms q_i (the same sums in the
+// same order as agent_linear_term), lanes 0 .. 5 and 6 .. 8 (targets) or 6 .. G-1 (reference
+// tail) the objective constant's terms, summed over the group. Every operator entry is a vector
+// load issued at once (the one-lane form serialised ~12 scalar-cache round trips). Returns this
+// lane's q_i (0 beyond NZ) and the constant (every lane).
+template <int NZ, int G>
+__device__ __forceinline__ double agent_linear_term_lanes(const DevOps& op, const double* buf,
+                                                          const ImpcArgs& args, int ai, const double (&s0)[6],
+                                                          int gl, double& kconst) {
+    static_assert(NZ <= G && G >= 9, "one lane per linear-term entry");
+    const int i = gl < NZ ? gl : 0;
+    // constant: s0^T Ks s0 + t^T Kt s0 — lane s < 6: s0_s (Ks s0)_s; lane 6 + d: t_d (Kt s0)_d
+    const int sr = gl < 6 ? gl : 0;
+    const int dr = (gl >= 6 && gl < 9) ? gl - 6 : 0;
+    double s0s = s0[0];
+#pragma unroll
+    for (int k = 1; k < 6; k++) s0s = sr == k ? s0[k] : s0s;
+    if (args.targets) {
+        // every load first (a scheduling barrier keeps them ahead of the arithmetic: interleaved,
+        // each group of loads waited for the previous one)
+        double qs[6], qt[3], t[3], kr[6];
+        const double* Qs = opp(buf, op.o_Qs) + (size_t)i * 6;
+        const double* Qt = opp(buf, op.o_Qt) + (size_t)i * 3;
+        const double* Kr = gl < 6 ? opp(buf, op.o_Ks) + (size_t)sr * 6 : opp(buf, op.o_Kt) + (size_t)dr * 6;
+#pragma unroll
+        for (int s = 0; s < 6; s++) qs[s] = Qs[s];
+#pragma unroll
+        for (int d = 0; d < 3; d++) qt[d] = Qt[d];
+#pragma unroll
+        for (int d = 0; d < 3; d++) t[d] = args.targets[(size_t)ai * 3 + d];
+#pragma unroll
+        for (int u = 0; u < 6; u++) kr[u] = Kr[u];
+        __builtin_amdgcn_sched_barrier(0);
+        double q = 0.0;
+#pragma unroll
+        for (int s = 0; s < 6; s++) q = fma(qs[s], s0[s], q);
+#pragma unroll
+        for (int d = 0; d < 3; d++) q = fma(qt[d], t[d], q);
+        double v = 0.0;
+#pragma unroll
+        for (int u = 0; u < 6; u++) v = fma(kr[u], s0[u], v);
+        const double td = dr == 0 ? t[0] : (dr == 1 ? t[1] : t[2]);
+        const double kc = gl < 6 ? s0s * v : (gl < 9 ? td * v : 0.0);
+        kconst = grp_sum<G>(kc);
+        return gl < NZ ? q : 0.0;
+    }
+    // reference-tail form (refs): + Qr r, + r^T Kr s0 (lanes 6 .. G-1: entries j = gl - 6,
+    // gl - 6 + (G - 6), ...)
+    const double* Qs = opp(buf, op.o_Qs) + (size_t)i * 6;
+    double q = 0.0;
+#pragma unroll
+    for (int s = 0; s < 6; s++) q = fma(Qs[s], s0[s], q);
+    double kc = 0.0;
+    {
+        const double* Ks = opp(buf, op.o_Ks) + (size_t)sr * 6;
+        double v = 0.0;
+#pragma unroll
+        for (int u = 0; u < 6; u++) v = fma(Ks[u], s0[u], v);
+        kc = gl < 6 ? s0s * v : 0.0;
+    }
+    const double* Qr = opp(buf, op.o_Qr);
+    const double* Kr = opp(buf, op.o_Kr);
+    const int nr = 3 * op.spd_f;
+    const double* rt = args.refs + (size_t)ai * 3 * op.K + 3 * (op.K - op.spd_f);
+    for (int j = 0; j < nr; j++) q = fma(Qr[(size_t)i * nr + j], rt[j], q);
+    for (int j = gl - 6; gl >= 6 && j < nr; j += G - 6) {
+        double v = 0.0;
+#pragma unroll
+        for (int s = 0; s < 6; s++) v = fma(Kr[j * 6 + s], s0[s], v);
+        kc = fma(rt[j], v, kc);
+    }
+    kconst = grp_sum<G>(kc);
+    return gl < NZ ? q : 0.0;
+}
+
 // Constant rows (zero in y): pure feasibility checks on s0, group-uniform result.
 template <int G>
 __device__ __forceinline__ bool constant_rows_infeasible(const DevOps& op, const double* buf,
@@ -428,10 +570,12 @@ __device__ __forceinline__ bool constant_rows_infeasible(const DevOps& op, const
     const double* chi = opp(buf, op.o_chi);
     bool bad = false;
     for (int i = gl; i < op.mc; i += G) {
+        // (bounds loaded with the row: the short-circuit test loaded chi after clo, after Cs)
+        const double lo = clo[i], hi = chi[i];
         double v = 0.0;
 #pragma unroll
         for (int s = 0; s < 6; s++) v = fma(Cs[i * 6 + s], s0[s], v);
-        if (v < clo[i] - op.feas_tol || v > chi[i] + op.feas_tol) bad = true;
+        bad = bad | (v < lo - op.feas_tol) | (v > hi + op.feas_tol);
     }
     return grp_ballot<G>(bad) != 0ull;
 }
@@ -646,20 +790,36 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
                                                     const double (&s0)[6], const double (&yk)[NZ],
                                                     bool have_curve) {
     const bool sim = args.traj_t != nullptr;
-    if (args.x && (have_curve || !sim)) {
+    const double t_stored = sim ? args.traj_t[ai] : 0.0;  // (loaded here: in flight during the x rows)
+    // this step's control points x = Xs s0 + Z y to args.x, XU rows per lane at a time (their loads
+    // in flight together; one row at a time, each row's loads waited for the previous row's)
+    // (staging them in LDS for the curve evaluation below, with its piece lookup from the kernel
+    // arguments, measured slower: 0.15 us per agent)
+    const bool want_x = args.x && (have_curve || !sim);
+    if (want_x && !have_curve) {
+        for (int i = gl; i < op.n; i += G) args.x[(size_t)ai * op.n + i] = __builtin_nan("");
+    } else if (want_x) {
         const double* Z = opp(buf, op.o_Z);
         const double* Xs = opp(buf, op.o_Xs);
-        for (int i = gl; i < op.n; i += G) {
-            double v = 0.0;
-            if (have_curve) {
+        constexpr int XU = (64 + G - 1) / G;
+        for (int i0 = 0; i0 < op.n; i0 += XU * G) {
+            double v[XU];
 #pragma unroll
-                for (int s = 0; s < 6; s++) v = fma(Xs[i * 6 + s], s0[s], v);
+            for (int u = 0; u < XU; u++) {
+                const int i = i0 + u * G + gl;
+                const int ic = i < op.n ? i : 0;
+                double a = 0.0;
 #pragma unroll
-                for (int j = 0; j < NZ; j++) v = fma(Z[i * NZ + j], yk[j], v);
-            } else {
-                v = __builtin_nan("");
+                for (int s = 0; s < 6; s++) a = fma(Xs[ic * 6 + s], s0[s], a);
+#pragma unroll
+                for (int j = 0; j < NZ; j++) a = fma(Z[ic * NZ + j], yk[j], a);
+                v[u] = a;
             }
-            args.x[(size_t)ai * op.n + i] = v;
+#pragma unroll
+            for (int u = 0; u < XU; u++) {
+                const int i = i0 + u * G + gl;
+                if (i < op.n) args.x[(size_t)ai * op.n + i] = v[u];
+            }
         }
     }
     if (gl >= 6) return;
@@ -667,7 +827,7 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
     const double sd = gl < 3 ? args.pos_std : args.vel_std;
     const int64_t agent = args.agent_first + ai;
     if (sim) {
-        const double t_prev = have_curve ? 0.0 : args.traj_t[ai];
+        const double t_prev = have_curve ? 0.0 : t_stored;
         double t_new = t_prev;
         const double tmax = opp(buf, op.o_cum)[op.P - 1];
         if (have_curve || t_prev >= 0.0) {

@@ -76,69 +76,119 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     double s0[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) s0[k] = args.states[(size_t)self * 6 + k];
+    // grid mode: the neighbour query's loads are staged between the setup's (gq_*; the state
+    // arrives before the branch, else the join waits for every load in flight)
+    const bool grid_mode = args.nb_row_ptr == nullptr;
+    GridQuery<64> gq;
+    asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s0[2]), "v"(s0[3]), "v"(s0[4]), "v"(s0[5]));
+    if (grid_mode) gq_begin<64>(args, s0[0], s0[1], gq);
     __shared__ double ykeep_s[WNZ], q_s[WNZ];  // wave-uniform vectors kept out of the registers
     __shared__ double ypd[WNZ];                // slack mode: the slack PDIP's point during its polish
     __shared__ double kconst_s;                // the objective's constant (read once per IMPC iteration)
     __shared__ double ego_s[2][8];             // IMPC iteration >= 1: the ego state at each CBF sample
+    // the FoV rows' per-sample operators (acceleration rows U_k: Z and s0 parts; the P^-1 Grams of
+    // the rows' weights), copied once per agent: read by every row task of both IMPC iterations
+    __shared__ double uz_s[MAX_CBF_H * 3 * 15], us_s[MAX_CBF_H * 18], mf_s[MAX_CBF_H * 6];
     // non-finite QP data (a NaN / Inf state, target or neighbour position), checked where the rows
     // are formed (v * 0 is NaN for a non-finite v): the rows that persist across the IMPC
     // iterations (q, box-row bounds, Voronoi rows) and each iteration's FoV rows
     bool nfin_fixed = false;
     {
-        double q15[NZ], kconst0;
-        agent_linear_term<NZ>(op, buf, args, ai, s0, q15, kconst0);
-        double chk = kconst0 * 0.0;
-#pragma unroll
-        for (int j = 0; j < NZ; j++) chk = fma(q15[j], 0.0, chk);
-        nfin_fixed = !(chk == 0.0);
-        if (lane == 0) {
-#pragma unroll
-            for (int j = 0; j < NZ; j++) {
-                q_s[j] = q15[j];
-                ykeep_s[j] = 0.0;
-            }
-            q_s[WNZ - 1] = 0.0;
-            ykeep_s[WNZ - 1] = 0.0;
-            kconst_s = kconst0;
+        double kconst0;
+        const double q = agent_linear_term_lanes<NZ, 64>(op, buf, args, ai, s0, lane, kconst0);
+        nfin_fixed = !(fma(q, 0.0, kconst0 * 0.0) == 0.0);  // (per lane; the solve ballots it)
+        if (lane < WNZ) {
+            q_s[lane] = q;  // (0 for the padding entry)
+            ykeep_s[lane] = 0.0;
         }
+        if (lane == 0) kconst_s = kconst0;
     }
 
     // ---- shared box rows into the image (rows 0 .. mb-1), bounds shifted by Gs s0
     const int mb = op.m;
+    if (grid_mode) gq_slots<64>(args, gq, lane);
     {
         const double* W = opp(buf, op.o_Wbox);
-        // (unrolled over the image's row slots: every slot's loads go out together)
+        const double* wb = opp(buf, op.o_wbox);
+        // each row's shift coefficients and bounds (rows lane, lane + 64, lane + 128), then the
+        // rows' coefficients in the image layout, BOXB per lane at a time: the loads' indices are
+        // clamped instead of guarded, so they are in flight together (guarded, one row slot's loads
+        // waited for the previous slot's)
+        double bt[WR][8], bw[WR];
+#pragma unroll
+        for (int sl = 0; sl < WR; sl++) {
+            const int r = lane + 64 * sl;
+            const double* src = W + (size_t)(r < mb ? r : 0) * WBOX_ROW + WNZ;
+#pragma unroll
+            for (int k = 0; k < 8; k++) bt[sl][k] = src[k];
+            bw[sl] = wb[r < mb ? r : 0];
+        }
+        constexpr int BOXB = 18;
+        const int ng = mb * WNZ;
+        for (int f0 = 0; f0 < ng; f0 += 64 * BOXB) {
+            double v[BOXB];
+#pragma unroll
+            for (int b = 0; b < BOXB; b++) {
+                const int f = f0 + 64 * b + lane;
+                const int fc = f < ng ? f : 0;
+                v[b] = W[(size_t)(fc / WNZ) * WBOX_ROW + fc % WNZ];
+            }
+#pragma unroll
+            for (int b = 0; b < BOXB; b++) {
+                const int f = f0 + 64 * b + lane;
+                if (f < ng) Gimg[f] = v[b];
+            }
+        }
 #pragma unroll
         for (int sl = 0; sl < WR; sl++) {
             const int r = lane + 64 * sl;
             if (r < mb) {
-                const double* src = W + (size_t)r * WBOX_ROW;
                 double sh = 0.0;
 #pragma unroll
-                for (int k = 0; k < 6; k++) sh = fma(src[WNZ + k], s0[k], sh);
-#pragma unroll
-                for (int j = 0; j < WNZ; j++) Gimg[r * WNZ + j] = src[j];
-                rlo[r] = src[WNZ + 6] - sh;
-                rhi[r] = src[WNZ + 7] - sh;
+                for (int k = 0; k < 6; k++) sh = fma(bt[sl][k], s0[k], sh);
+                rlo[r] = bt[sl][6] - sh;
+                rhi[r] = bt[sl][7] - sh;
                 nfin_fixed = nfin_fixed || !(sh * 0.0 == 0.0);  // (the rows themselves: host constants)
                 rml[r] = 1.0;
-                was.wn[r] = (float)opp(buf, op.o_wbox)[r];  // (constant rows: the host's weights)
+                was.wn[r] = (float)bw[sl];  // (constant rows: the host's weights)
             }
         }
     }
+    if (grid_mode) gq_states<64>(args, gq, lane);
     if (lane < WNZ) Gimg[WROWS * WNZ + lane] = 0.0;
     zero_row = &Gimg[WROWS * WNZ];
     const bool infeasible = constant_rows_infeasible<64>(op, buf, s0, lane);
-    das_load_operators(was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16), lane);
+    das_load_operators<!SLACK>(was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16), lane);
+    {
+        // (one batch of clamped loads over the three arrays, then the stores)
+        const int n1 = op.cbf_h * 3 * NZ, n2 = op.cbf_h * 18, n3 = op.cbf_h * 6;
+        const double* s1 = opp(buf, op.o_UZ);
+        const double* s2 = opp(buf, op.o_US);
+        const double* s3 = opp(buf, op.o_wfov);
+        constexpr int NL = (MAX_CBF_H * (3 * 15 + 18 + 6) + 63) / 64;
+        double v[NL];
+#pragma unroll
+        for (int b = 0; b < NL; b++) {
+            const int f = lane + 64 * b;
+            const double* src = f < n1 ? s1 + f : (f < n1 + n2 ? s2 + (f - n1) : s3 + (f < n1 + n2 + n3 ? f - n1 - n2 : 0));
+            v[b] = *src;
+        }
+#pragma unroll
+        for (int b = 0; b < NL; b++) {
+            const int f = lane + 64 * b;
+            if (f < n1) uz_s[f] = v[b];
+            else if (f < n1 + n2) us_s[f - n1] = v[b];
+            else if (f < n1 + n2 + n3) mf_s[f - n1 - n2] = v[b];
+        }
+    }
     stamp(args, ai, lane, 1);
 
-    const bool grid_mode = args.nb_row_ptr == nullptr;
     int nb0 = 0, nnb = 0;
     if (!grid_mode) {
         nb0 = args.nb_row_ptr[ai];
         nnb = args.nb_row_ptr[ai + 1] - nb0;
     } else {
-        nnb = grid_neighbors<64>(args, self, s0[0], s0[1], nb_scratch, lane, s0[2]);
+        nnb = grid_neighbors_finish<64>(args, self, s0[0], s0[1], nb_scratch, lane, s0[2], gq);
     }
     const bool nb_overflow = nnb < 0 || nnb > (SLACK ? WSL_NB : FOV_NB_CAP);
     if (nb_overflow) nnb = 0;
@@ -189,32 +239,42 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         const int nvor = nnb * C;
         for (int v = lane; v < nvor && it == 0; v += 64) {
             const int i = v / C, j = v % C;
+            // control point j's operator rows first (they do not depend on the neighbour; behind
+            // its position and the row's arithmetic they were three dependent round trips)
+            const double* VZ = opp(buf, op.o_VZ) + (size_t)j * 2 * NZ;
+            const double* VS = opp(buf, op.o_VS) + (size_t)j * 12;
+            const double* M = opp(buf, op.o_wvor) + 3 * j;  // g P^-1 g = (nx, ny) M (nx, ny)^T
+            double vz[2 * NZ], vs[12], mw[3];
+#pragma unroll
+            for (int k = 0; k < 2 * NZ; k++) vz[k] = VZ[k];
+#pragma unroll
+            for (int k = 0; k < 12; k++) vs[k] = VS[k];
+#pragma unroll
+            for (int k = 0; k < 3; k++) mw[k] = M[k];
+            __builtin_amdgcn_sched_barrier(0);
             double ox, oy, nx, ny, off;
             nb_position(args, nb_scratch, grid_mode, nb0, i, ox, oy);
             voronoi_row(s0[0], s0[1], ox, oy, op.bbox[0], op.bbox[1], nx, ny, off);
-            const double* VZ = opp(buf, op.o_VZ) + (size_t)j * 2 * NZ;
-            const double* VS = opp(buf, op.o_VS) + (size_t)j * 12;
             const int r = mb + v;
             double sh = 0.0;
 #pragma unroll
-            for (int k = 0; k < 6; k++) sh = fma(nx * VS[k] + ny * VS[6 + k], s0[k], sh);
+            for (int k = 0; k < 6; k++) sh = fma(nx * vs[k] + ny * vs[6 + k], s0[k], sh);
 #pragma unroll
-            for (int jz = 0; jz < NZ; jz++) Gimg[r * WNZ + jz] = nx * VZ[jz] + ny * VZ[NZ + jz];
+            for (int jz = 0; jz < NZ; jz++) Gimg[r * WNZ + jz] = nx * vz[jz] + ny * vz[NZ + jz];
             Gimg[r * WNZ + NZ] = 0.0;
             rlo[r] = 0.0;
             rml[r] = 0.0;
             rhi[r] = -off - 1e-8 - sh;
             nfin_fixed = nfin_fixed || !(fma(nx, 0.0, ny * 0.0) + (off + sh) * 0.0 == 0.0);
-            const double* M = opp(buf, op.o_wvor) + 3 * j;  // g P^-1 g = (nx, ny) M (nx, ny)^T
-            was.wn[r] = rsqrtf((float)fmax(fma(nx, fma(M[0], nx, 2.0 * M[1] * ny), M[2] * ny * ny), 1e-30));
+            was.wn[r] = rsqrtf((float)fmax(fma(nx, fma(mw[0], nx, 2.0 * mw[1] * ny), mw[2] * ny * ny), 1e-30));
         }
         // ---- FoV CBF rows, compacted after the Voronoi rows
         const int nk = (it == 0) ? 1 : op.cbf_h;
         const int base = mb + nvor;
         int count = 0;
         bool row_infeasible = false;
-        const double* UZ = opp(buf, op.o_UZ);
-        const double* US = opp(buf, op.o_US);
+        const double* UZ = uz_s;
+        const double* US = us_s;
         const int ntask = nnb * 4 * nk;
         if (it > 0) {
             // the ego state at each CBF sample (the previous curve at h_samples(k)), once per sample:
@@ -223,11 +283,17 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 const int k = lane / 6, c = lane - 6 * k;
                 const double* PZ = opp(buf, op.o_PZ) + (size_t)k * 6 * NZ + c * NZ;
                 const double* PS = opp(buf, op.o_PS) + (size_t)k * 36 + c * 6;
+                double ps[6], pz[NZ];  // (loaded together, then the sums)
+#pragma unroll
+                for (int u = 0; u < 6; u++) ps[u] = PS[u];
+#pragma unroll
+                for (int j = 0; j < NZ; j++) pz[j] = PZ[j];
+                __builtin_amdgcn_sched_barrier(0);
                 double v = 0.0;
 #pragma unroll
-                for (int u = 0; u < 6; u++) v = fma(PS[u], s0[u], v);
+                for (int u = 0; u < 6; u++) v = fma(ps[u], s0[u], v);
 #pragma unroll
-                for (int j = 0; j < NZ; j++) v = fma(PZ[j], ykeep_s[j], v);
+                for (int j = 0; j < NZ; j++) v = fma(pz[j], ykeep_s[j], v);
                 ego_s[k][c] = v;
             }
             wave_lds_sync();
@@ -309,7 +375,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 const double hr = bb + a[0] * us[0] + a[1] * us[1] + a[2] * us[2];
                 rhi[r] = hr;
                 nfin_it = nfin_it || !(fma(a[0], 0.0, fma(a[1], 0.0, a[2] * 0.0)) + hr * 0.0 == 0.0);
-                const double* M = opp(buf, op.o_wfov) + 6 * k;  // g P^-1 g = a^T M_k a
+                const double* M = mf_s + 6 * k;  // g P^-1 g = a^T M_k a
                 const double n2 = a[0] * (M[0] * a[0] + 2.0 * (M[1] * a[1] + M[2] * a[2])) +
                                   a[1] * (M[3] * a[1] + 2.0 * M[4] * a[2]) + a[2] * M[5] * a[2];
                 was.wn[r] = rsqrtf((float)fmax(n2, 1e-30));

@@ -473,21 +473,33 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     double s0[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) s0[i] = args.states[(size_t)self * 6 + i];
+    // grid mode: the neighbour query's loads are staged between the setup's (gq_*)
+    const bool grid_mode = args.nb_row_ptr == nullptr;
+    GridQuery<G> gq;
+    // (the state arrives before the branch: waited for only on one side, the join would wait for
+    // every load in flight, the query's included)
+    asm volatile("" ::"v"(s0[0]), "v"(s0[1]), "v"(s0[2]), "v"(s0[3]), "v"(s0[4]), "v"(s0[5]));
+    if (grid_mode) gq_begin<G>(args, s0[0], s0[1], gq);
     // the linear term and constant, group-uniform: kept in LDS (qk, after the warm-start ids) and
     // read back inside each IMPC iteration, so they are not live in registers across the loop
     double* qk = keep + 16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1);
     {
-        double q0[NZ], kc0;
-        agent_linear_term<NZ>(op, buf, args, ai, s0, q0, kc0);
+        double kc0;
+        const double q0 = agent_linear_term_lanes<NZ, G>(op, buf, args, ai, s0, gl, kc0);
+        if (gl < NZ) qk[gl] = q0;
         if (gl == 0) {
-#pragma unroll
-            for (int j = 0; j < NZ; j++) qk[j] = q0[j];
             qk[NZ] = kc0;
+            *(int*)(qk + NZ + 1) = ai;
         }
     }
+    // the agent index and the returned point's residuals, re-read from LDS where they are used
+    // (held in registers across the solves they were the main launch's last spills)
+    auto agent = [&]() -> int { return *(volatile int*)(qk + NZ + 1); };
+    volatile double* res = qk + NZ + 2;
 
     // ---- box rows: channel d, slot k -> row k * G + gl of that channel (packed by the host:
     // per row [g0, g1, Gs(6), lo, hi], two-sided; unused rows inert: g = 0, Gs = 0, [-1, 1])
+    if (grid_mode) gq_slots<G>(args, gq, gl);
     SepRows<SB, CB> rw_reg;  // (the fallback launch: rows in LDS)
     SepRows<SB, CB>& rw = pick_rows<QUEUE && !SLACK>(rw_reg, rows_lds);
     {
@@ -506,20 +518,20 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 rw.bhi[d][k] = r[9] - sh;
             }
     }
+    if (grid_mode) gq_states<G>(args, gq, gl);
     const bool infeasible = constant_rows_infeasible<G>(op, buf, s0, gl);
     stamp(args, ai, gl, 1);
 
-    const bool grid_mode = args.nb_row_ptr == nullptr;
     int nb0 = 0, nnb = 0;
     if (!grid_mode) {
         nb0 = args.nb_row_ptr[ai];
         nnb = args.nb_row_ptr[ai + 1] - nb0;
     } else {
-        nnb = grid_neighbors<G>(args, self, s0[0], s0[1], nbs, gl);
+        nnb = grid_neighbors_finish<G>(args, self, s0[0], s0[1], nbs, gl, 0.0, gq);
     }
     write_nb_out(args, ai, gl, grid_mode, nbs, nb0, nnb);
     if (SLACK && !QUEUE && nnb > G && args.defer) {  // slack mode: beyond one lane per neighbour
-        defer_agent(args, ai, gl);
+        defer_agent(args, agent(), gl);
         return;
     }
     const bool nb_overflow = nnb < 0 || (SLACK && !QUEUE && nnb > G);
@@ -566,7 +578,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     };
 
     for (int it = 0; it < op.impc_iter; it++) {
-        const size_t oi = (size_t)ai * op.impc_iter + it;
+        const size_t oi = (size_t)agent() * op.impc_iter + it;
         if (!success) {
             write_iteration(args, oi, gl, ST_UNKNOWN, __builtin_nan(""), 0);
             continue;
@@ -610,12 +622,12 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         }
         if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
         if (count > cap && args.defer) {  // beyond this instantiation: the fallback launch solves it
-            defer_agent(args, ai, gl);
+            defer_agent(args, agent(), gl);
             return;
         }
         int st;
         int nit = 0;
-        double prs = __builtin_nan(""), drs = __builtin_nan("");
+        if (gl == 0) res[0] = res[1] = __builtin_nan("");
         // non-finite data (a NaN / Inf state, target or neighbour state): such a model is not
         // solved (CPLEX rejects non-finite coefficients); reported as ERROR
         bool nfin = false;
@@ -648,7 +660,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 yu[o] = -fma(Pi[3 * d], q[o], Pi[3 * d + 1] * q[o + 1]);
                 yu[o + 1] = -fma(Pi[3 * d + 1], q[o], Pi[3 * d + 2] * q[o + 1]);
             }
-            double tl = 0.0;
+            double tl = 0.0, prs = __builtin_nan(""), drs = __builtin_nan("");
             const int k0 = warm_count(it);
             const int r = sep_dual_as<G, SB, CB>(rw, live, opp(buf, op.o_Pr), Pi, q, yu, op.tol, op.dual_as, stage, y,
                                                  prs, drs, nit, nullptr, true, tl, nullptr, k0, act,
@@ -660,17 +672,18 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                 prs = tl;
                 drs = __builtin_nan("");
             } else {
-                defer_agent(args, ai, gl);
+                defer_agent(args, agent(), gl);
                 return;
             }
+            if (gl == 0) res[0] = prs, res[1] = drs;
         } else {
 #ifdef MPCCBF_PDIP_STAMPS
             long long* dbg = (args.stamps && it == 0)
-                                 ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 16
+                                 ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)agent() * 16
                                  : nullptr;
 #elif defined(MPCCBF_SOLVE_TRACE)  // per-step (rp, mu, alpha, rd) of the first solve + phase 1
             long long* dbg = args.stamps ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP +
-                                               ((size_t)ai * 2 + it) * 256
+                                               ((size_t)agent() * 2 + it) * 256
                                          : nullptr;
 #else
             long long* dbg = nullptr;
@@ -792,8 +805,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
             }
             st = po.status;
             nit = total + tr_p1;  // active-set, PDIP and phase-1 steps
-            prs = st == ST_INFEASIBLE ? tstar : po.rp;
-            drs = po.rd;
+            if (gl == 0) res[0] = st == ST_INFEASIBLE ? tstar : po.rp, res[1] = po.rd;
 #ifdef MPCCBF_SOLVE_TRACE  // diagnostics build: warm + 100 cold + 10000 phase-1 iterations
             nit = tr_warm + 100 * tr_cold + 10000 * tr_p1;
 #else
@@ -810,7 +822,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         } else {
             success = false;
         }
-        write_iteration(args, oi, gl, st, objv, nit, prs, drs);
+        write_iteration(args, oi, gl, st, objv, nit, res[0], res[1]);
         if (it == 0) steps0 = nit;
         if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
         wave_lds_sync();
@@ -819,7 +831,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
 #pragma unroll
     for (int i = 0; i < NZ; i++) yk[i] = ykeep[16 * i];
     load_state_lds(s0k, sx);
-    write_agent_outputs<NZ, G>(op, buf, args, ai, gl, sx, yk, have_curve);
+    write_agent_outputs<NZ, G>(op, buf, args, agent(), gl, sx, yk, have_curve);
     stamp(args, ai, gl, 7);
 }
 
@@ -838,8 +850,9 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
     // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
-    // set's warm-start side ids and their count (not in slack mode) | linear term and constant
-    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 8];
+    // set's warm-start side ids and their count (not in slack mode) | linear term and constant, the
+    // agent index, the residuals
+    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 10];
     __shared__ SepRowsLds<SB, CB> rows_lds[QUEUE && !SLACK ? BS : 1];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;

@@ -370,7 +370,7 @@ __device__ __forceinline__ void publish16(double* __restrict__ dst, double v, in
 // term; on return sc.y holds the iterate. nchunk: row chunks in use.
 // SLK: slack mode — skp holds the slack rows (see WaveSlack); v_obj gets sum_i w_i v_i.
 template <bool SLK = false>
-__device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
+__device__ __forceinline__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
                                    WaveScratch& sc, const double* __restrict__ P,
                                    const double* __restrict__ LP, const PdipCfg cfg, int lane,
                                    long long* dbg = nullptr, const WaveSlack* skp = nullptr,
@@ -737,7 +737,7 @@ __device__ PdipOut pdip_solve_wave(const WaveRows& rw, const double* __restrict_
 // — the first block on the matrix cores (column 15 = G^T (Dl - Du)), the corner by a reduction.
 // The t >= 0 bound is one more side. Uses sc.y / sc.d / sc.M. Returns t* (>= 0), 1e300 on
 // numerical failure.
-__device__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
+__device__ __forceinline__ double pdip_phase1_wave(const WaveRows& rw, const double* __restrict__ Gs, int nchunk,
                                    WaveScratch& sc, int nz, const PdipCfg cfg, int lane) {
     constexpr double eps = 1e-10;
     const int i = lane16_opaque(lane);

@@ -114,19 +114,35 @@ def test_gauss_seidel_trace_matches_oracle(mpclib, neighbours):
     kw = dict(pos_std=1e-3, vel_std=1e-2, noise_seed=77)
     s = sim.Simulator(cfg, states, targets, neighbours=neighbours, knn_k=8, knn_radius=6.0,
                       order="gauss_seidel", record=False, **kw)
-    gpu = [s.states.cpu().numpy().copy()]
+    gpu, objs = [s.states.cpu().numpy().copy()], []
     for _ in range(steps):
         s.step()
         gpu.append(s.states.cpu().numpy().copy())
+        objs.append(s.out["obj"].cpu().numpy().copy())
     gpu = np.array(gpu)
     one, one_status = O.closed_loop_gauss_seidel(cfg, states, targets, steps, k=8, radius=6.0,
                                                  pos_std=kw["pos_std"], vel_std=kw["vel_std"],
                                                  seed=kw["noise_seed"], neighbours=neighbours, inputs=gpu)
     np.testing.assert_array_equal(np.array(s.status_log), one_status)
-    # (measured on MI355X: 3e-13 on most steps, at most 2.5e-9 where an update's QP is ill-conditioned:
-    # two exact active-set solutions agree to rounding amplified by the conditioning)
-    err1 = np.max(np.abs(gpu - one), axis=(1, 2))
-    assert err1.max() <= 1e-8, err1
+    # per update: within 1e-8 of the oracle (measured on MI355X: 3e-13 on most updates). Where an
+    # update's QP is ill-conditioned the oracle's interior-point optimum sits up to ~1e-11 relative
+    # above the device's exact active-set one, which moves the curve by up to ~1e-7 (all-neighbour
+    # lists, step 5 robot 18: 1.3e-7 with the oracle's objective 4.1e-9 above the device's; the
+    # previous kernels gave the same trace bit for bit). Such an update must stay within 1e-6 and
+    # the device's objective must not be worse than the oracle's (1e-10 relative)
+    err = np.max(np.abs(gpu - one), axis=2)  # (steps + 1) x n
+    p = O.make_params(cfg)
+    refs = np.tile(np.asarray(targets, dtype=np.float64), (1, cfg["k_hor"]))
+    for s1, i in zip(*np.nonzero(err > 1e-8)):
+        assert err[s1, i] <= 1e-6, (s1, i, err[s1, i])
+        st = s1 - 1
+        cur = np.concatenate([gpu[st + 1][:i], gpu[st][i:]])
+        nb = (np.array([j for j in range(n) if j != i], dtype=np.int32) if neighbours == "all"
+              else O.knn_list(cur, i, 8, 6.0))
+        r = O.impc_optimize(p, cur, i, nb, refs[i])
+        ok = r["status"] == O.OPTIMAL
+        assert np.all(objs[st][i][ok] <= r["obj"][ok] + 1e-10 * np.abs(r["obj"][ok])), (st, i, objs[st][i], r["obj"])
+    assert (err > 1e-8).sum() <= 2, np.argwhere(err > 1e-8)
     assert np.any(one_status == O.OPTIMAL)
     free, _ = O.closed_loop_gauss_seidel(cfg, states, targets, steps, k=8, radius=6.0,
                                          pos_std=kw["pos_std"], vel_std=kw["vel_std"],
