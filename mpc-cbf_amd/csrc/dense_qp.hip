@@ -216,27 +216,28 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         for (int k = eptr[l]; k < eptr[l + 1]; k++) v = fma(eval[k], s.xp[ecol[k]], v);
         if (fabs(v - erhs[l]) > kFeasTol) eq_infeasible = true;
     }
-    // ---- Hs Z and Hs xp from H's nonzeros (Hs = (H + H^T) / 2): lane l sums row l over the
-    // nonzeros in their packed order (every lane scans the list; a fixed summation order, so the
-    // result does not depend on how the hardware orders LDS atomics)
+    // ---- Hs Z and Hs xp, Hs = (H + H^T) / 2: H's nonzeros scattered into a dense n x n image in
+    // LDS (E^T's space, free from here; each entry written once, so no atomics), then lane l forms
+    // row l over j = 0 .. n-1 — a fixed summation order (no dependence on how the hardware orders
+    // LDS atomics), and no lane walks the whole nonzero list (that serial scan of global loads and
+    // divisions cost ~1.7 ms per 4096-QP call)
+    for (int e = l; e < n * LDS_S; e += 64) s.et[e] = 0.0;
+    __syncthreads();
+    for (int e = l; e < nh; e += 64) {
+        const int k = hidx[e];
+        const int i = k / n, j = k - i * n;
+        s.et[i * LDS_S + j] = hval[e];
+    }
+    __syncthreads();
     if (l < n) {
         double hxl = 0.0, hzl[DENSE_NZ];
 #pragma unroll
         for (int b = 0; b < DENSE_NZ; b++) hzl[b] = 0.0;
-        for (int e = 0; e < nh; e++) {
-            const int i = hidx[e] / n, j = hidx[e] - (hidx[e] / n) * n;
-            if (i != l && j != l) continue;
-            const double hv = 0.5 * hval[e];
-            if (i == l) {
-                hxl = fma(hv, s.xp[j], hxl);
+        for (int j = 0; j < n; j++) {
+            const double hv = 0.5 * (s.et[l * LDS_S + j] + s.et[j * LDS_S + l]);
+            hxl = fma(hv, s.xp[j], hxl);
 #pragma unroll
-                for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[j * DENSE_NZ + b], hzl[b]);
-            }
-            if (j == l) {
-                hxl = fma(hv, s.xp[i], hxl);
-#pragma unroll
-                for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[i * DENSE_NZ + b], hzl[b]);
-            }
+            for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[j * DENSE_NZ + b], hzl[b]);
         }
         s.hx[l] = hxl;
 #pragma unroll

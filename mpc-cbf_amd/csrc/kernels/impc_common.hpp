@@ -882,6 +882,18 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
     }
 }
 
+// XCD-aware block order: workgroups are dispatched round-robin over the 8 XCDs (block b runs on
+// XCD b % 8), each with its own L2. Block b takes logical block xcd_block(b) so that every XCD
+// gets one contiguous range of the batch: consecutive agents are spatial neighbours (the swarms are
+// laid out in lattice / heading order and the hash table by cell), so an XCD's neighbour-state and
+// bucket reads stay mostly inside its own range instead of every XCD's L2 fetching the whole state
+// table each step. A bijection of [0, gridDim.x).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7;
+    const int x = b & 7, k = b >> 3;
+    return x * q + (x < r ? x : r) + k;
+}
+
 // the bucket counts of the table two steps ahead are zeroed by the launch's threads (called by
 // every thread before any early exit)
 __device__ __forceinline__ void grid_clear(const ImpcArgs& args) {

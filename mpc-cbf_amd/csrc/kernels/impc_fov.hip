@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                                                        const ImpcArgs args) {
     constexpr int NZ = 15;
     const int lane = threadIdx.x;
-    const int ai = blockIdx.x;
+    const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x);
     lds_poison();
     grid_clear(args);
     if (ai >= args.num_agents) return;

@@ -494,8 +494,13 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     }
     // the agent index and the returned point's residuals, re-read from LDS where they are used
     // (held in registers across the solves they were the main launch's last spills)
+#ifdef MPCCBF_V_REGAI  // (A/B variant: both in registers)
+    auto agent = [&]() -> int { return ai; };
+    double res[2];
+#else
     auto agent = [&]() -> int { return *(volatile int*)(qk + NZ + 1); };
     volatile double* res = qk + NZ + 2;
+#endif
 
     // ---- box rows: channel d, slot k -> row k * G + gl of that channel (packed by the host:
     // per row [g0, g1, Gs(6), lo, hi], two-sided; unused rows inert: g = 0, Gs = 0, [-1, 1])
@@ -859,7 +864,7 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     lds_poison();
     if constexpr (!QUEUE) {
         grid_clear(args);
-        const int ai = blockIdx.x * GPB + gib;
+        const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * GPB + gib;
         if (ai >= args.num_agents) return;
         impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
                                                    nb_scratch[gib], keep_all[gib]);
