@@ -445,9 +445,10 @@ __device__ __forceinline__ void defer_agent(const ImpcArgs& args, int ai, int gl
 // The (non-slack) fallback launch keeps a lane's rows (SepRows, e.g. 8 CBF slots: 60 doubles) in
 // LDS instead of registers: its occupancy is one wave per SIMD either way, and in registers they
 // spilled (1236 -> 424 B/lane for 8 slots, 44 -> 0 for 1). Padded to an odd number of doubles per
-// lane (bank spread of the per-lane struct reads). The slack fallback keeps them in registers: in
-// LDS its results changed in the last bits and one all-neighbour slack QP of the stress line
-// (255 slacks, weights down to 1e-9) flipped to UNKNOWN.
+// lane (bank spread of the per-lane struct reads). The slack fallback too since round 4 (156 -> 0
+// B/lane; round 3 had kept them in registers because in LDS one all-neighbour slack QP of the
+// stress line flipped to UNKNOWN in the last bits — with the slack-pattern active set the 1000-step
+// stress line stays at 0 UNKNOWN either way, `profiles/r04_slack_fallback_lds.log`).
 template <int SB, int CB>
 struct SepRowsLds {
     SepRows<SB, CB> r;
@@ -506,7 +507,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     // per row [g0, g1, Gs(6), lo, hi], two-sided; unused rows inert: g = 0, Gs = 0, [-1, 1])
     if (grid_mode) gq_slots<G>(args, gq, gl);
     SepRows<SB, CB> rw_reg;  // (the fallback launch: rows in LDS)
-    SepRows<SB, CB>& rw = pick_rows<QUEUE && !SLACK>(rw_reg, rows_lds);
+    SepRows<SB, CB>& rw = pick_rows<QUEUE>(rw_reg, rows_lds);
     {
         const double* B = opp(buf, op.o_Gsep);
 #pragma unroll
@@ -858,7 +859,7 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     // set's warm-start side ids and their count (not in slack mode) | linear term and constant, the
     // agent index, the residuals
     __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 10];
-    __shared__ SepRowsLds<SB, CB> rows_lds[QUEUE && !SLACK ? BS : 1];
+    __shared__ SepRowsLds<SB, CB> rows_lds[QUEUE ? BS : 1];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     lds_poison();
