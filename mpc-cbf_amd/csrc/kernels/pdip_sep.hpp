@@ -122,13 +122,25 @@ __device__ __forceinline__ void sep_stage_side(const SepRows<SB, CB>& rw, const 
                 b = side ? rw.bhi[d][kk] : rw.blo[d][kk];
                 sg = side ? 1.0 : -1.0;
             }
+    if constexpr (CB > 2) {
+        // (the wide capacity fallback: its rows live in LDS, so the slot is indexed directly — the
+        // unrolled compares over 8 slots kept every slot's row in registers and spilled)
+        const int c = s - i;
+        if (c >= 0 && c < CB) {
 #pragma unroll
-    for (int c = 0; c < CB; c++, i++) {
-        if (i != s) continue;
+            for (int j = 0; j < 4; j++) g[j] = rw.cg[c][j];
+            b = rw.chi[c];
+            sg = 1.0;
+        }
+    } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) g[j] = rw.cg[c][j];
-        b = rw.chi[c];
-        sg = 1.0;
+        for (int c = 0; c < CB; c++, i++) {
+            if (i != s) continue;
+#pragma unroll
+            for (int j = 0; j < 4; j++) g[j] = rw.cg[c][j];
+            b = rw.chi[c];
+            sg = 1.0;
+        }
     }
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) r[j] = g[j];
