@@ -42,6 +42,44 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __longlong_as_double(((long long)hi << 32) | (long long)lo);
 }
 
+// row i of a 16 x 16 LDS matrix stored with row stride 17 times a 16-vector (LDS): every load first
+// (interleaved with the FMAs the compiler waited for each pair of loads in turn), then the same
+// sequential FMA chain
+__device__ __forceinline__ double rowdot17(const double* M, int i, const double* v, double init = 0.0) {
+    double m[WNZ], x[WNZ];
+#pragma unroll
+    for (int j = 0; j < WNZ; j++) {
+        m[j] = M[i * 17 + j];
+        x[j] = v[j];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double a = init;
+#pragma unroll
+    for (int j = 0; j < WNZ; j++) a = fma(m[j], x[j], a);
+    return a;
+}
+
+// dotl with every load first, then the same two FMA chains (BATCH; the FoV slack kernel keeps the
+// interleaved form, where the batch costs scratch)
+template <bool BATCH>
+__device__ __forceinline__ double dotl_b(const double* a, const double* b) {
+    if constexpr (!BATCH) return dotl(a, b);
+    double x[WNZ], z[WNZ];
+#pragma unroll
+    for (int j = 0; j < WNZ; j++) {
+        x[j] = a[j];
+        z[j] = b[j];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < WNZ; j += 2) {
+        s0 = fma(x[j], z[j], s0);
+        s1 = fma(x[j + 1], z[j + 1], s1);
+    }
+    return s0 + s1;
+}
+
 // a row (LDS) times a vector of scalar operands
 __device__ __forceinline__ double dot_rows_s(const double* a, const double (&ys)[WNZ]) {
     double s0 = 0.0, s1 = 0.0;
@@ -167,9 +205,7 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
     // y = -P^-1 q
     double yi;
     {
-        double a = 0.0;
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) a = fma(ws.Pi[i * 17 + j], sc.q[j], a);
+        const double a = rowdot17(ws.Pi, i, sc.q);
         yi = -a;
     }
     publish16(sc.y, yi, lane);
@@ -191,9 +227,7 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         for (int r0 = nfirst; r0 < nrows; r0 += 4) {
             const int r = r0 + grp;
             const double* g = Gs + (r < nrows ? r : 0) * WNZ;
-            double w = 0.0;
-#pragma unroll
-            for (int j = 0; j < WNZ; j++) w = fma(ws.Pi[i * 17 + j], g[j], w);
+            const double w = rowdot17(ws.Pi, i, g);
             const double n2 = grp_sum<16>(g[i] * w);
             if (i == 0 && r < nrows) ws.wn[r] = rsqrtf((float)fmax(n2, 1e-30));
         }
@@ -212,9 +246,30 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         double ys[WNZ];
 #pragma unroll
         for (int j = 0; j < WNZ; j++) ys[j] = readlane_d(yi, j);
+        // every slot's row first (24 LDS reads in flight together; slot by slot, each slot's reads
+        // waited for the previous slot's arithmetic)
+        double ts[WR];
+        {
+            double rr[WR][WNZ];
+#pragma unroll
+            for (int s = 0; s < WR; s++)
+#pragma unroll
+                for (int j = 0; j < WNZ; j++) rr[s][j] = rw.g[s][j];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < WR; s++) {
+                double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+                for (int j = 0; j < WNZ; j += 2) {
+                    s0 = fma(rr[s][j], ys[j], s0);
+                    s1 = fma(rr[s][j + 1], ys[j + 1], s1);
+                }
+                ts[s] = s0 + s1;
+            }
+        }
 #pragma unroll
         for (int s = 0; s < WR; s++) {
-            const double t = dot_rows_s(rw.g[s], ys);
+            const double t = ts[s];
             const double al = rw.lo[s] - t, au = t - rw.hi[s];
             const double vl = rw.ml[s] > 0.0 ? al * pl[s] : -1.0;
             const double vu = au * pu[s];
@@ -245,11 +300,9 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         const double bp = __shfl(bb, owner, 64);
         const double* gp = Gs + rp * WNZ;
         // the candidate's P^-1 g on the row layout, published
-        double wi = 0.0;
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) wi = fma(ws.Pi[i * 17 + j], gp[j], wi);
+        const double wi = rowdot17(ws.Pi, i, gp);
         publish16(ws.w, wi, lane);
-        const double nw = dotl(gp, ws.w);
+        const double nw = dotl_b<BOUND>(gp, ws.w);
         WSTAMP(3, steps == 0);
         double up = 0.0;  // the candidate's multiplier
         for (;;) {
@@ -262,13 +315,13 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
             double ci = 0.0, sgi = 0.0;
             if (kk > 0) {
                 const int ra = i < k ? ws.row[i] : rp;
-                ci = i < k ? sp * dotl(Gs + ra * WNZ, ws.w) : 0.0;
+                ci = i < k ? sp * dotl_b<BOUND>(Gs + ra * WNZ, ws.w) : 0.0;
                 sgi = i < k ? ws.sg[i] : 0.0;
             }
             const double vi = fwd_rows(L, inv_i, ci, i, kk);
             const double rhoi = bwd_rows(sc.M, inv_i, vi, i, kk);
             const double zn = nw - grp_sum<16>(vi * vi);
-            const double vp = sp * (dotl(gp, sc.y) - bp);
+            const double vp = sp * (dotl_b<BOUND>(gp, sc.y) - bp);
             WSTAMP(4, steps == 1);
             // dual step: the first active multiplier to reach zero
             const double r_i = sgi * rhoi;
@@ -350,7 +403,7 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
                 const double* gi_ = Gs + (i < k ? ws.row[i] : 0) * WNZ;
 #pragma unroll
                 for (int b = 0; b < WNZ; b++)
-                    Kr[b] = (i < k && b < k) ? dotl(gi_, ws.W + b * WNZ) : (i == b ? 1.0 : 0.0);
+                    Kr[b] = (i < k && b < k) ? dotl_b<BOUND>(gi_, ws.W + b * WNZ) : (i == b ? 1.0 : 0.0);
             }
             if (!chol_rows(Kr, L, inv_i, sc.M, lane)) return 0;
         }
@@ -367,9 +420,7 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
     double rd = 0.0;
     const int kk = BOUND ? __builtin_amdgcn_readfirstlane(k) : WNZ;
     if (kk > 0 || want_rd) {
-        double r = sc.q[i];
-#pragma unroll
-        for (int j = 0; j < WNZ; j++) r = fma(ws.P[i * 17 + j], sc.y[j], r);
+        double r = rowdot17(ws.P, i, sc.y, sc.q[i]);
         const double lsi = ui * (i < k ? ws.sg[i < k ? i : 0] : 0.0);
 #pragma unroll
         for (int a = 0; a < WNZ - 1; a++) {
