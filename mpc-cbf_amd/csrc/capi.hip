@@ -295,6 +295,10 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     pack(v, d.o_EB1, o.EB1);
     pack(v, d.o_cum, o.cum);
     d.eval_step = o.eval_step;
+    {
+        const double tend = o.cum.empty() ? 0.0 : o.cum.back();
+        d.az_at_eval = (!o.cum.empty() && std::min(o.eval_step, tend) == std::min(p->h, tend)) ? 1 : 0;
+    }
     d.Ts = p->Ts;
     d.nsub = (int)(p->h / p->Ts);
     // separable layout: box rows regrouped by channel, 16 per channel (lanes of a group)

@@ -60,6 +60,10 @@ struct DevOps {
     // dual active set: IMPC iteration 1 starts from iteration 0's final active set when iteration 0
     // took at least this many steps (0: always cold)
     int32_t das_warm;
+    // closed-loop simulator: 1 when AZ / AS (the curve at t = min(h, T_end)) are also the curve at
+    // a fresh curve's evaluation time min(eval_step, T_end), so the next state of an agent with a new
+    // curve is one operator product (no piece lookup and Bernstein evaluation on the device)
+    int32_t az_at_eval;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;

@@ -783,8 +783,9 @@ __device__ __forceinline__ double curve_component_any(const DevOps& op, const do
 //   args.traj_t set (closed-loop simulator, MPCCBFFormationControl_example.cpp:150-221): x is
 //            the persistent last successful curve, next state = it at the advanced time.
 // FIXED: the curve evaluation's compile-time control-point count (C = 4) when it applies (off for the
-// FoV slack kernel, whose registers it pushes into scratch)
-template <int NZ, int G, bool FIXED = true>
+// FoV slack kernel, whose registers it pushes into scratch); AZE: a fresh curve's next state from the
+// AZ / AS rows when DevOps::az_at_eval (off in the FoV kernels, where it costs scratch)
+template <int NZ, int G, bool FIXED = true, bool AZE = true>
 __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const double* buf,
                                                     const ImpcArgs& args, int ai, int gl,
                                                     const double (&s0)[6], const double (&yk)[NZ],
@@ -833,7 +834,17 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
         if (have_curve || t_prev >= 0.0) {
             t_new = fmin(t_prev + op.eval_step, tmax);  // example :190-193
             const double* xr = have_curve ? nullptr : args.x + (size_t)ai * op.n;
-            v = curve_component_any<NZ, FIXED>(op, buf, xr, s0, yk, t_new, gl);
+            if (AZE && have_curve && op.az_at_eval && !args.substeps) {
+                // a fresh curve at min(eval_step, T_end) = min(h, T_end): the AZ / AS rows
+                const double* AZ = opp(buf, op.o_AZ);
+                const double* AS = opp(buf, op.o_AS);
+#pragma unroll
+                for (int s = 0; s < 6; s++) v = fma(AS[gl * 6 + s], s0[s], v);
+#pragma unroll
+                for (int j = 0; j < NZ; j++) v = fma(AZ[gl * NZ + j], yk[j], v);
+            } else {
+                v = curve_component_any<NZ, FIXED>(op, buf, xr, s0, yk, t_new, gl);
+            }
             if (args.substeps) {  // sub-steps 1 .. nsub - 1: the curve at t_prev + Ts k, own draws
                 for (int k = 1; k < op.nsub; k++) {
                     double u = curve_component_any<NZ, FIXED>(op, buf, xr, s0, yk, fmin(t_prev + op.Ts * k, tmax), gl);
@@ -888,7 +899,7 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
 // laid out in lattice / heading order and the hash table by cell), so an XCD's neighbour-state and
 // bucket reads stay mostly inside its own range instead of every XCD's L2 fetching the whole state
 // table each step. A bijection of [0, gridDim.x).
-__device__ __forceinline__ int xcd_block(int b, int nb) {
+__host__ __device__ __forceinline__ int xcd_block(int b, int nb) {
     const int q = nb >> 3, r = nb & 7;
     const int x = b & 7, k = b >> 3;
     return x * q + (x < r ? x : r) + k;

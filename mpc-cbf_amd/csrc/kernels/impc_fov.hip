@@ -714,7 +714,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         double yk[NZ];
 #pragma unroll
         for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
-        write_agent_outputs<NZ, 64, !SLACK>(op, buf, args, ai, lane, s0, yk, have_curve);
+        write_agent_outputs<NZ, 64, !SLACK, false>(op, buf, args, ai, lane, s0, yk, have_curve);
     }
     // (diagnostics; here, not after the query: there it pushed the kernel into scratch)
     write_nb_out(args, ai, lane, grid_mode, nb_scratch, nb0, nnb);
