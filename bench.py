@@ -38,7 +38,7 @@ HBM_PEAK_GBS = 8000.0
 VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 4  # wave64 VALU instructions / s: 1024 SIMDs, one per 4 cycles at 2.4 GHz
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -84,7 +84,7 @@ def parse():
                     help="skip the closed-loop safety metrics pass (collision_check.py on the trace)")
     ap.add_argument("--dump", default="",
                     help="write the timed pass's per-step status / solver-step logs (rank 0) to this .npz")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def flops_per_qp(iters: np.ndarray, rows: np.ndarray, nz: int) -> float:
@@ -207,6 +207,30 @@ def run_dense(args) -> None:
     print(json.dumps(line), flush=True)
 
 
+def workload_sizes(args, world: int, rank: int) -> tuple[int, int, int]:
+    """Agents in total, agents per rank and this rank's first agent; fills in the defaults of
+    --agents-total / --agents-per-gpu / --k-hor on args. N = 1: config 3 (4096 agents, horizon 15)
+    or config 5's 512-agent per-GPU share (FoV, horizon 20). N > 1: config 4 (8192 agents in total)
+    / config 5 (4096 FoV agents) sharded evenly over the ranks, unless --weak (per-GPU size kept)
+    or an explicit size is given. --rank-share S times one rank's 1/S share on one GPU."""
+    fov = args.workload == "fov"
+    if world > 1 and not args.weak and args.agents_total <= 0 and args.agents_per_gpu <= 0:
+        # BASELINE config 4 (8192 agents sharded over the node's GPUs) / config 5 (4096 FoV agents)
+        args.agents_total = 4096 if fov else 8192
+    if args.agents_per_gpu <= 0:
+        args.agents_per_gpu = 512 if fov else 4096
+    if args.k_hor <= 0:
+        args.k_hor = 20 if fov else 15
+    total = args.agents_total if args.agents_total > 0 else args.agents_per_gpu * world
+    shares = world
+    if args.rank_share > 0:
+        assert world == 1, "--rank-share runs on one GPU"
+        shares = args.rank_share
+    per = total // shares
+    assert per * shares == total, "agents must divide evenly over ranks"
+    return total, per, rank * per
+
+
 def main():
     args = parse()
     spawn_ranks(args)
@@ -228,21 +252,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     fov = args.workload == "fov"
-    if world > 1 and not args.weak and args.agents_total <= 0 and args.agents_per_gpu <= 0:
-        # BASELINE config 4 (8192 agents sharded over the node's GPUs) / config 5 (4096 FoV agents)
-        args.agents_total = 4096 if fov else 8192
-    if args.agents_per_gpu <= 0:
-        args.agents_per_gpu = 512 if fov else 4096
-    if args.k_hor <= 0:
-        args.k_hor = 20 if fov else 15
-    total = args.agents_total if args.agents_total > 0 else args.agents_per_gpu * world
-    shares = world
-    if args.rank_share > 0:
-        assert world == 1, "--rank-share runs on one GPU"
-        shares = args.rank_share
-    per = total // shares
-    assert per * shares == total, "agents must divide evenly over ranks"
-    first = rank * per
+    total, per, first = workload_sizes(args, world, rank)
     slack = dict(slack_mode=1, slack_cost=1000.0, slack_decay_rate=args.slack_decay) if args.slack else {}
     if fov:
         cfg = swarm.fov_config(args.k_hor, **slack)
@@ -496,7 +506,7 @@ def main():
                     + (f", slack_mode (cost 1000, decay {args.slack_decay:g})" if args.slack else "")
                     + ", base_config.json; 2 IMPC QPs/agent/step"
                     + ("" if world == 1 else f"; {per}/GPU, RCCL all-gather of states")
-                    + (f"; rank 0's share of {shares} ranks ({per} of {total} agents; the other rows carried "
+                    + (f"; rank 0's share of {args.rank_share} ranks ({per} of {total} agents; the other rows carried "
                        "over and inserted into the neighbour table every step, the all-gather excluded)"
                        if args.rank_share > 0 else "")),
                 "agents_total": total,
