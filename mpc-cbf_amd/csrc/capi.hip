@@ -25,13 +25,14 @@ namespace mpccbf {
 
 hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
                        hipStream_t s);
-const char* impc_kernel_name(const DevOps& op, int variant);
+const char* impc_kernel_name(const DevOps& op, int variant, int n);
+void impc_set_device_simds(int simds);
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
 hipError_t launch_fov_rows_eval(int count, const double* ego, const double* nb, double fov, double Ds, double Rs,
                                 double bbx, double bby, double* vor, double* rows, hipStream_t s);
 hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide,
                                 hipStream_t s);
-bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k);
+bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k, int n);
 bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k);
 int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
                      double radius, int32_t* row_ptr, int32_t* col, void* scratch,
@@ -72,9 +73,13 @@ struct mpccbf_ctx {
     size_t scratch_bytes = 0;
     void* grid_scratch = nullptr;  // three neighbour tables (see GridArgs)
     size_t grid_bytes = 0;
-    int32_t* defer = nullptr;      // capacity-fallback queue [count, blocks done, agents...] (zeroed)
+    // fallback queues [count, -, agents...], two (alternating by enqueue parity: the main launch
+    // zeroes the other one's header), zero-initialised
+    int32_t* defer = nullptr;
     int defer_cap = 0;
+    int defer_parity = 0;
     int variant = 0;
+    int last_n = 0;  // agents of the last IMPC launch (the kernel name depends on it: share-adaptive)
 };
 
 using namespace mpccbf;
@@ -184,27 +189,34 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     // fallback launch: agents the main launch defers (the lean launch: QPs that need the PDIP or
     // phase 1; beyond the separable kernel's 16 CBF row slots) are solved by a second launch of
     // the full separable pipeline (128 slots when the 16 can be exceeded)
-    const bool fb = c->dev.cbf_mode != 1 && impc_may_defer(c->dev, c->variant, !grid, b->knn_k);
+    const bool fb = c->dev.cbf_mode != 1 && impc_may_defer(c->dev, c->variant, !grid, b->knn_k, b->num_agents);
+    c->last_n = b->num_agents;
     if (fb && c->defer_cap < b->num_agents) {
         if (c->defer) (void)hipFree(c->defer);
         c->defer = nullptr;
         c->defer_cap = 0;
-        HIP_TRY(hipMalloc(&c->defer, (size_t)(b->num_agents + 2) * sizeof(int32_t)));
-        HIP_TRY(hipMemsetAsync(c->defer, 0, (size_t)(b->num_agents + 2) * sizeof(int32_t), stream));
+        HIP_TRY(hipMalloc(&c->defer, 2 * (size_t)(b->num_agents + 2) * sizeof(int32_t)));
+        HIP_TRY(hipMemsetAsync(c->defer, 0, 2 * (size_t)(b->num_agents + 2) * sizeof(int32_t), stream));
         c->defer_cap = b->num_agents;
+        c->defer_parity = 0;
     }
-    a.defer = fb ? c->defer : nullptr;
+    int32_t* q_this = nullptr;
+    if (fb) {
+        q_this = c->defer + (size_t)c->defer_parity * (c->defer_cap + 2);
+        a.defer_clear = c->defer + (size_t)(c->defer_parity ^ 1) * (c->defer_cap + 2);
+        c->defer_parity ^= 1;
+    }
+    a.defer = q_this;
     if (ev0) HIP_TRY(hipEventRecord(ev0, stream));
     hipError_t e = c->dev.cbf_mode == 1 ? launch_impc_fov(c->dev, c->dbuf, a, stream)
                                         : launch_impc(c->dev, c->dbuf, a, c->variant, stream);
     if (e == hipSuccess && fb) {
         ImpcArgs f = a;
         f.defer = nullptr;
-        f.queue = c->defer;
+        f.defer_clear = nullptr;
+        f.queue = q_this;
         e = launch_impc_fallback(c->dev, c->dbuf, f, impc_rows_may_exceed(c->dev, !grid, b->knn_k), stream);
-        // the fallback's last block empties the queue; if it never ran, the agents the main
-        // launch appended are dropped here, so the next main launch starts from an empty queue
-        if (e != hipSuccess) (void)hipMemsetAsync(c->defer, 0, 2 * sizeof(int32_t), stream);
+        // (a queue the fallback never read is zeroed by the main launch after next)
     }
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, stream);
     if (e == hipErrorInvalidValue)
@@ -458,6 +470,11 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
 #endif
     c->variant = 0;
     hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) {
+        // share-adaptive layout: one agent per wave up to one agent per SIMD (4 per CU)
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) impc_set_device_simds(4 * prop.multiProcessorCount);
+    }
     if (e == hipSuccess) e = hipMalloc(&c->dbuf, v.size() * sizeof(double));
     if (e == hipSuccess) e = hipMemcpy(c->dbuf, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
@@ -491,7 +508,7 @@ int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
 const char* mpccbf_kernel_name(const mpccbf_ctx* c) {
     if (!c) return "";
     if (c->dev.cbf_mode == 1) return c->dev.slack_mode ? "impc_fov_kernel<true>" : "impc_fov_kernel<false>";
-    const char* n = impc_kernel_name(c->dev, c->variant);
+    const char* n = impc_kernel_name(c->dev, c->variant, c->last_n);
     return n ? n : "";
 }
 

@@ -145,11 +145,14 @@ struct ImpcArgs {
     // minimal violation t* and NaN), num_agents x impc_iter, or nullptr
     double* primal_res;
     double* dual_res;
-    // capacity fallback (impc_sep_kernel): the main launch appends agents beyond its row capacity
-    // to defer ([count, blocks done, agent...], device) and leaves their outputs to the fallback
-    // launch, which solves exactly the agents in queue (the same buffer) with a wider instantiation
+    // capacity fallback (impc_sep_kernel / impc_wide_kernel): the main launch appends agents it does
+    // not finish to defer ([count, -, agent...], device) and leaves their outputs to the fallback
+    // launch, which solves exactly the agents in queue (the same buffer) with the full pipeline
     int32_t* defer;
     int32_t* queue;
+    // the other step parity's queue header, zeroed by the main launch (block 0): the queues are
+    // double-buffered by step parity, so the fallback launch never has to reset its own
+    int32_t* defer_clear;
     // closed-loop simulator: the state after every control sub-step (num_agents x nsub x 6), the
     // records the example writes to states.json, or nullptr
     double* substeps;

@@ -905,9 +905,10 @@ __host__ __device__ __forceinline__ int xcd_block(int b, int nb) {
     return x * q + (x < r ? x : r) + k;
 }
 
-// the bucket counts of the table two steps ahead are zeroed by the launch's threads (called by
-// every thread before any early exit)
+// the bucket counts of the table two steps ahead are zeroed by the launch's threads, and the other
+// step parity's defer-queue header by block 0 (called by every thread before any early exit)
 __device__ __forceinline__ void grid_clear(const ImpcArgs& args) {
+    if (args.defer_clear && blockIdx.x == 0 && threadIdx.x == 0) args.defer_clear[0] = 0;
     if (!args.grid.clr_cnt) return;
     const uint32_t T = args.grid.mask + 1u;
     const uint32_t nthr = gridDim.x * blockDim.x;

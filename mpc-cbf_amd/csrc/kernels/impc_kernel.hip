@@ -25,6 +25,7 @@
 
 #include "impc.hpp"
 #include "impc_common.hpp"
+#include "impc_wide.hpp"
 #include "pdip.hpp"
 #include "pdip_sep.hpp"
 
@@ -871,20 +872,198 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
                                                    nb_scratch[gib], keep_all[gib]);
     } else {
         // one queue entry per group (no grid-stride loop: carried across iterations the agent's
-        // state spills); groups beyond the queue's length leave at once
+        // state spills, 0 -> 352 B/lane); groups beyond the queue's length leave at once. The
+        // queue's header is zeroed by the main launch after next (the queues alternate by step
+        // parity), so no block has to find out that it is the last one
         const int k = blockIdx.x * GPB + gib;
         if (k < args.queue[0])
             impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
                                                 nb_scratch[gib], keep_all[gib], rows_lds);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            if (atomicAdd(&args.queue[1], 1) == (int)gridDim.x - 1) {
-                args.queue[0] = 0;
-                args.queue[1] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// One agent per wave (impc_wide.hpp)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wide_defer(const ImpcArgs& args, int ai, int gl) {
+    if (gl == 0) {
+        const int slot = atomicAdd(&args.defer[0], 1);
+        args.defer[2 + slot] = ai;
+    }
+}
+
+__device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
+                                const int ai, WideLds& L) {
+    constexpr int NZ = SEP_NZ;
+    const int gl = (int)(threadIdx.x & 63u);
+    stamp(args, ai, gl, 0);
+    const int self = args.agent_first + ai;
+    double s0[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) s0[i] = args.states[(size_t)self * 6 + i];
+    const bool grid_mode = args.nb_row_ptr == nullptr;
+    WideQuery gq;
+    WideCells gc;
+    if (grid_mode) wn_begin(args, s0[0], s0[1], gl, gq);
+    double kconst;
+    const double qlane = agent_linear_term_lanes<NZ, 64>(op, buf, args, ai, s0, gl, kconst);
+    // this lane's box row: channel d = gl / 16, slot gl % 16 (host layout [channel][16][SEP_ROW])
+    WRow rw;
+    {
+        const int lb = gl < W_BOX ? gl : 0;
+        const double* r = opp(buf, op.o_Gsep) + (size_t)lb * SEP_ROW;
+        double rv[SEP_ROW];
+#pragma unroll
+        for (int i = 0; i < SEP_ROW; i++) rv[i] = r[i];
+        double sh = 0.0;
+#pragma unroll
+        for (int s = 0; s < 6; s++) sh = fma(rv[2 + s], s0[s], sh);
+        const int d = gl >> 4;
+#pragma unroll
+        for (int j = 0; j < NZ; j++) rw.g[j] = 0.0;
+        if (gl < W_BOX) {
+#pragma unroll
+            for (int dd = 0; dd < SEP_D; dd++)
+                if (dd == d) {
+                    rw.g[2 * dd] = rv[0];
+                    rw.g[2 * dd + 1] = rv[1];
+                }
+        }
+        rw.lo = gl < W_BOX ? rv[8] - sh : -1e300;
+        rw.hi = gl < W_BOX ? rv[9] - sh : 1.0;
+        const double* pd = opp(buf, op.o_Pinv) + 3 * (d < SEP_D ? d : 0);
+        rw.w = wide_weight(wide_n2(pd[0], pd[1], pd[2], rv[0], rv[1]));
+    }
+    if (grid_mode) {
+        wn_cells(args, gq, gc);
+        wn_slots(args, gc, gl, gq);
+    }
+    if (grid_mode) wn_states(args, gc, gl, gq);
+    const bool infeasible = constant_rows_infeasible<64>(op, buf, s0, gl);
+    stamp(args, ai, gl, 1);
+
+    int nb0 = 0, nnb = 0;
+    if (!grid_mode) {
+        nb0 = args.nb_row_ptr[ai];
+        nnb = args.nb_row_ptr[ai + 1] - nb0;
+    } else {
+        nnb = wn_finish(args, self, s0[0], s0[1], gc, gq, L, gl);
+    }
+    nnb = uni_i(nnb);
+    if (args.nb_out && gl < 16)  // diagnostics: the list the rows are built from
+        args.nb_out[(size_t)ai * 16 + gl] = gl < nnb ? (grid_mode ? L.nbi[gl] : args.nb_col[nb0 + gl]) : -1;
+    const bool nb_overflow = nnb < 0;
+    if (nb_overflow) nnb = 0;
+    stamp(args, ai, gl, 2);
+
+    double q[NZ];
+#pragma unroll
+    for (int j = 0; j < NZ; j++) q[j] = lane_of(qlane, j);
+    kconst = uni(kconst);
+    double y[NZ], yk[NZ];
+#pragma unroll
+    for (int j = 0; j < NZ; j++) y[j] = yk[j] = 0.0;
+    bool have_curve = false, success = true;
+    if (gl == 0) L.act[POL_K] = 0.0;
+    int steps0 = 0;
+    const double* Pinv = opp(buf, op.o_Pinv);
+
+    for (int it = 0; it < op.impc_iter; it++) {
+        const size_t oi = (size_t)ai * op.impc_iter + it;
+        if (!success) {  // the reference breaks out of the IMPC loop (:208-211)
+            write_iteration(args, oi, gl, ST_UNKNOWN, __builtin_nan(""), 0);
+            continue;
+        }
+        bool row_infeasible = false;
+        const int count = uni_i(wide_cbf_rows(op, buf, args, it, s0, y, grid_mode, L, nb0, nnb, gl, row_infeasible));
+        if (gl >= W_BOX) {  // this iteration's CBF rows into the CBF lanes (unused: inert 0 <= 1)
+            const int c = gl - W_BOX;
+            const bool on = c < count;
+            const double* src = L.stage + (on ? c : 0) * W_ROW;
+#pragma unroll
+            for (int j = 0; j < 4; j++) rw.g[j] = on ? src[j] : 0.0;
+            rw.hi = on ? src[4] : 1.0;
+            const double* Pi = opp(buf, op.o_Pinv);
+            rw.w = wide_weight(wide_n2(Pi[0], Pi[1], Pi[2], rw.g[0], rw.g[1]) +
+                               wide_n2(Pi[3], Pi[4], Pi[5], rw.g[2], rw.g[3]));
+        }
+        if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
+        if (count > W_CBF) {  // beyond the 16 CBF lanes: the fallback launch (8 slots per lane)
+            if (args.defer) {
+                wide_defer(args, ai, gl);
+                return;
             }
         }
+        bool nfin = false;
+#pragma unroll
+        for (int j = 0; j < NZ; j++) nfin = nfin || !isfinite(q[j]) || !isfinite(rw.g[j]);
+        nfin = nfin || !isfinite(rw.hi) || (gl < W_BOX && !isfinite(rw.lo));
+        const bool nonfinite = __ballot(nfin) != 0ull;
+        int st, nit = 0;
+        double prs = __builtin_nan(""), drs = __builtin_nan("");
+        if (count > W_CBF || nb_overflow || nonfinite) {
+            st = ST_ERROR;
+        } else if (infeasible || row_infeasible) {
+            st = ST_INFEASIBLE;
+        } else {
+            double yu[NZ];
+#pragma unroll
+            for (int d = 0; d < SEP_D; d++) {
+                const int o = 2 * d;
+                yu[o] = -fma(Pinv[3 * d], q[o], Pinv[3 * d + 1] * q[o + 1]);
+                yu[o + 1] = -fma(Pinv[3 * d + 1], q[o], Pinv[3 * d + 2] * q[o + 1]);
+            }
+            int k0 = 0;
+            if (it > 0 && op.das_warm > 0 && steps0 >= op.das_warm) {
+                wave_lds_sync();
+                k0 = uni_i((int)L.act[POL_K]);
+            }
+            double tl = 0.0;
+            const int r = wide_dual_as(rw, opp(buf, op.o_Pr), Pinv, q, yu, op.tol, op.dual_as, L.pol, y, prs, drs,
+                                       nit, tl, k0, L.act, it == 0 ? L.act : nullptr);
+            if (r > 0) {
+                st = ST_OPTIMAL;
+            } else if (r < 0 && tl > 10.0 * op.feas_tol) {
+                st = ST_INFEASIBLE;
+                prs = tl;
+                drs = __builtin_nan("");
+            } else {
+                if (args.defer) {
+                    wide_defer(args, ai, gl);
+                    return;
+                }
+                st = ST_UNKNOWN;
+            }
+        }
+        double objv = __builtin_nan("");
+        if (st == ST_OPTIMAL) {
+            objv = reduced_objective<NZ>(op, buf, q, y, kconst);
+#pragma unroll
+            for (int i = 0; i < NZ; i++) yk[i] = y[i];
+            have_curve = true;
+        } else {
+            success = false;
+        }
+        write_iteration(args, oi, gl, st, objv, nit, prs, drs);
+        if (it == 0) steps0 = nit;
+        if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
     }
+    write_agent_outputs<NZ, 64>(op, buf, args, ai, gl, s0, yk, have_curve);
+    stamp(args, ai, gl, 7);
+    return;
+}
+
+template <int BS>
+__global__ void __launch_bounds__(BS) impc_wide_kernel(const DevOps op, const double* __restrict__ buf,
+                                                        const ImpcArgs args) {
+    constexpr int WPB = BS / 64;
+    __shared__ WideLds lds_all[WPB];
+    lds_poison();
+    grid_clear(args);
+    const int wv = uni_i((int)(threadIdx.x >> 6));
+    const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * WPB + wv;
+    if (ai >= args.num_agents) return;
+    impc_wide_agent(op, buf, args, ai, lds_all[wv]);
 }
 
 }  // namespace dev
@@ -909,10 +1088,41 @@ static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const I
     return hipGetLastError();
 }
 
+// Whether the one-agent-per-wave kernel applies: the separable collision controller (no slack
+// variables) with the dual active set on; CBF samples <= MAX_CBF_H.
+static bool impc_wide_ok(const DevOps& op) {
+    return op.cbf_mode == 0 && !op.slack_mode && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 &&
+           op.dual_as > 0 && op.cbf_h <= MAX_CBF_H;
+}
+
+// Agents per launch up to which the default layout is the wide kernel: one wave per agent at one
+// wave per SIMD fills the chip once at 4 x CUs agents
+static int g_wide_max = 1024;
+void impc_set_device_simds(int simds) { g_wide_max = simds > 0 ? simds : 1024; }
+
+static hipError_t launch_impc_wide(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
+    constexpr int BS = 256, WPB = BS / 64;
+    const int blocks = (a.num_agents + WPB - 1) / WPB;
+    hipLaunchKernelGGL((dev::impc_wide_kernel<BS>), dim3(blocks), dim3(BS), 0, s, op, buf, a);
+    return hipGetLastError();
+}
+
+// Layouts of the separable collision controller (mpccbf_set_variant):
+//   0 (default) — share-adaptive: up to one agent per SIMD of the device (1,024 on MI355X: config
+//       4's rank share) the one-agent-per-wave kernel (its fallback as a second launch); beyond,
+//       the 16-lane kernel (4 agents per wave: one wave per SIMD covers 4 x as many agents);
+//   VARIANT_SEP16 — the 16-lane kernel at any count (the layout of rounds 1-4);
+//   VARIANT_WIDE — the one-agent-per-wave kernel at any count.
+constexpr int VARIANT_SEP16 = 4, VARIANT_WIDE = 5;
+static bool sep_variant(int variant) { return variant == 0 || variant == VARIANT_SEP16; }
+static bool use_wide(const DevOps& op, int variant, int n) {
+    return impc_wide_ok(op) && (variant == VARIANT_WIDE || (variant == 0 && n <= g_wide_max));
+}
+
 // The separable layout's lean main launch (fast start + dual active set; everything else deferred)
-static bool sep_lean(const DevOps& op, int variant) {
-    return variant == 0 && !op.slack_mode && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 &&
-           op.lean && op.dual_as > 0;
+static bool sep_lean(const DevOps& op, int variant, int n) {
+    return sep_variant(variant) && !use_wide(op, variant, n) && !op.slack_mode && op.sep && op.nzd == SEP_NZD_HOST &&
+           op.sep_rows_per_dim <= 16 && op.lean && op.dual_as > 0;
 }
 
 // Agents the main launch deferred are solved by this launch (the queue in a.queue):
@@ -933,24 +1143,26 @@ hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcA
 // or k nearest x CBF samples > 16).
 bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k) { return csr || knn_k * op.cbf_h > 16; }
 
-// Whether launch_impc defers agents (so launch_impc_fallback must follow): the lean main launch
-// always may; the full separable kernel when its 16 CBF row slots can be exceeded.
-bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k) {
+// Whether launch_impc defers agents (so launch_impc_fallback must follow): the lean main launches
+// always may; the full separable kernel and the wide kernel with the inline fallback when their 16
+// CBF row slots can be exceeded.
+bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k, int n) {
     // slack mode: more than 16 neighbours only from caller lists (grid mode takes knn_k <= 16,
     // impc_enqueue)
     if (op.slack_mode) return op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2 && csr;
-    if (sep_lean(op, variant)) return true;
-    if (!(variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)) return false;
+    if (use_wide(op, variant, n) || sep_lean(op, variant, n)) return true;
+    if (!(sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)) return false;
     return impc_rows_may_exceed(op, csr, knn_k);
 }
 
-// Instantiation launch_impc picks for (operators, variant); nullptr if none fits.
-const char* impc_kernel_name(const DevOps& op, int variant) {
+// Instantiation launch_impc picks for (operators, variant, agents per launch); nullptr if none fits.
+const char* impc_kernel_name(const DevOps& op, int variant, int n) {
     if (op.slack_mode)  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2
         return (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
                    ? "impc_sep_kernel<1,2,true,256>" : nullptr;
-    if (sep_lean(op, variant)) return "impc_sep_kernel<1,1,false,256,false,true>";
-    if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false,256>";
+    if (use_wide(op, variant, n)) return "impc_wide_kernel<256>";
+    if (sep_lean(op, variant, n)) return "impc_sep_kernel<1,1,false,256,false,true>";
+    if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false,256>";
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
         if (variant == 1 && op.m < 64) return "impc_kernel<6,64,1>";
@@ -967,8 +1179,9 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
             return launch_impc_sep_t<1, 2, true>(op, buf, a, s);
         return hipErrorInvalidValue;
     }
-    if (sep_lean(op, variant)) return launch_impc_sep_t<1, 1, false, 256, false, true>(op, buf, a, s);
-    if (variant == 0 && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)
+    if (use_wide(op, variant, a.num_agents)) return launch_impc_wide(op, buf, a, s);
+    if (sep_lean(op, variant, a.num_agents)) return launch_impc_sep_t<1, 1, false, 256, false, true>(op, buf, a, s);
+    if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)
         return launch_impc_sep_t<1, 1, false>(op, buf, a, s);
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return launch_impc_t<6, 16, 4>(op, buf, a, s);
