@@ -215,8 +215,14 @@ def workload_sizes(args, world: int, rank: int) -> tuple[int, int, int]:
     or an explicit size is given. --rank-share S times one rank's 1/S share on one GPU."""
     fov = args.workload == "fov"
     if world > 1 and not args.weak and args.agents_total <= 0 and args.agents_per_gpu <= 0:
-        # BASELINE config 4 (8192 agents sharded over the node's GPUs) / config 5 (4096 FoV agents)
-        args.agents_total = 4096 if fov else 8192
+        # BASELINE config 4 (8192 agents sharded over the node's GPUs) / config 5 (4096 FoV agents);
+        # a rank count that does not divide it (3, 5, 6, 7) runs weak scaling at the per-GPU size
+        cfg_total = 4096 if fov else 8192
+        if cfg_total % world == 0:
+            args.agents_total = cfg_total
+        else:
+            print(f"bench: {cfg_total} agents do not divide over {world} ranks; weak scaling at the "
+                  "per-GPU size (give --agents-total for a strong-scaling line)", file=sys.stderr)
     if args.agents_per_gpu <= 0:
         args.agents_per_gpu = 512 if fov else 4096
     if args.k_hor <= 0:
@@ -303,6 +309,8 @@ def main():
             dist.broadcast(uid, 0)
             comm = Comm(bytes(uid.cpu().tolist()), world, rank, local)
 
+        kclock = torch.zeros((nsteps, 2), dtype=torch.int64, device=dev)
+
         def closed_loop(log, timing):
             """warm-up + nsteps control steps from the initial swarm; returns (seconds, run dict).
             timing=False: nothing but the steps on the stream (the throughput pass);
@@ -324,7 +332,8 @@ def main():
             t0 = time.perf_counter()
             e0.record()  # torch's current stream: the one run_steps launches on
             r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=log[0], iters_log=log[1],
-                              timing=timing, solve_stride=1, step_index=args.warmup, **common)
+                              timing=timing, solve_stride=1, step_index=args.warmup,
+                              kernel_clock=None if timing else kclock, **common)
             e1.record()
             barrier_sync()
             return time.perf_counter() - t0, r
@@ -333,6 +342,10 @@ def main():
         elapsed, _ = closed_loop(logs[0], timing=False)
         # device time of the timed region by HIP events at its two ends (no event between launches)
         region_ms = e0.elapsed_time(e1)
+        # each IMPC launch's own duration in the timed pass: the kernel's first-wave start to its
+        # last-wave end on the device clock (s_memrealtime, 100 MHz; mpccbf_run::kernel_clock)
+        kc = kclock.cpu().numpy().view(np.uint64)
+        launch_us = ((kc[:, 1] - ~kc[:, 0]).astype(np.float64)) * 1e-2
         # replay of the identical steps (same initial swarm, counter-based noise keyed by the step
         # index) with HIP events on the launch stream: per-step device time (p99) and the IMPC
         # kernel's duration on every step (roofline), without perturbing the throughput pass
@@ -408,6 +421,7 @@ def main():
         step_ms = np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(nsteps)])
         kern_ms = np.array([a.elapsed_time(b) for a, b in kev])
         region_ms = None
+        launch_us = None
 
     status = logs[0][0].cpu().numpy()
     iters = logs[0][1].cpu().numpy()
@@ -421,7 +435,7 @@ def main():
     hist["not_attempted"] = int(np.sum(~attempted))
     rows = ctx.shared_rows  # CBF rows are few (filtered); counted as shared rows only
     kname = ctx.kernel_name
-    if kname.startswith("impc_sep_kernel"):
+    if kname.startswith("impc_sep_kernel") or kname.startswith("impc_wide_kernel"):
         flops = flops_per_qp_sep(iters.reshape(-1), rows)
     else:
         flops = flops_per_qp(iters.reshape(-1), np.full(iters.size, rows), ctx.nz)
@@ -432,7 +446,9 @@ def main():
 
     vals = [elapsed, float(hist["OPTIMAL"]), float(hist["INFEASIBLE"]), float(hist["UNKNOWN"]),
             float(hist["ERROR"]), float(hist["not_attempted"]), flops, float(np.mean(kern_ms)),
-            float(np.percentile(step_ms, 99)), float(np.max(kern_ms)), float(bool(replay_same) or replay_same is None)]
+            float(np.percentile(step_ms, 99)), float(np.max(kern_ms)), float(bool(replay_same) or replay_same is None),
+            float(np.mean(launch_us)) if launch_us is not None else -1.0,
+            float(np.max(launch_us)) if launch_us is not None else -1.0]
     t = torch.tensor(vals, dtype=torch.float64, device=dev)
     if world > 1:
         mx = t.clone()
@@ -442,22 +458,23 @@ def main():
         mn = t.clone()
         dist.all_reduce(mn, op=dist.ReduceOp.MIN)
         elapsed, kern_avg, p99, kern_max = float(mx[0]), float(mx[7]), float(mx[8]), float(mx[9])
+        launch_avg, launch_max = float(mx[11]), float(mx[12])
         for i, k in enumerate(("OPTIMAL", "INFEASIBLE", "UNKNOWN", "ERROR", "not_attempted")):
             hist[k] = int(sm[1 + i])
         flops_rank0 = float(t[6])
         replay_same = bool(mn[10] > 0.5) if replay_same is not None else None
     else:
         kern_avg, p99, kern_max = vals[7], vals[8], vals[9]
+        launch_avg, launch_max = vals[11], vals[12]
         flops_rank0 = flops
     kern_bracket = kern_avg
-    # one rank, the native loop: a step is the IMPC launch alone (plus the capacity fallback's
-    # launch when its slots can be exceeded), so the timed region's events divided by the steps
-    # are the kernel's average duration without the dispatch gap that per-launch events add
     nbk = total - 1 if args.neighbours == "all" else args.knn  # neighbours per agent (at most)
-    fallback = kname.startswith("impc_sep_kernel") and nbk * cfg["cbf_horizon"] > 16
-    kernel_only = world == 1 and region_ms is not None and not fallback and args.rank_share <= 0
-    if kernel_only:
-        kern_avg = region_ms / nsteps
+    # the dominant kernel's average duration: the device clock of every IMPC launch of the timed
+    # pass (first-wave start to last-wave end; rocprof's kernel time); the host-loop form has no
+    # such clock and keeps the HIP-event brackets
+    region_avg = (region_ms / nsteps) if region_ms is not None else None
+    if launch_avg > 0:
+        kern_avg, kern_max = launch_avg * 1e-3, launch_max * 1e-3
 
     if rank == 0:
         solved = hist["OPTIMAL"] + hist["INFEASIBLE"]
@@ -474,7 +491,9 @@ def main():
         # issue peak (every SIMD one wave64 VALU op per 4 cycles: 1024 SIMDs x 2.4 GHz / 4)
         valu_insts, valu_src = pmc_lookup(kname, wl, "SQ_INSTS_VALU")
         abytes = algorithmic_bytes_per_agent(ctx.n, nbk, cfg["impc_iter"], cov is not None) * per
-        bound = "mfma" if kname.startswith("impc_fov") else "valu"
+        # every IMPC kernel is bound by its agents' dependent instruction chains (latency at one or
+        # a few waves per SIMD), not by MFMA, VALU throughput or HBM (the fractions below say how far)
+        bound = "latency"
         res = {
             "metric": "QP solves/sec (whole node) + p99 step latency, N-agent horizon-15 MPC-CBF",
             "value": qps,
@@ -539,13 +558,17 @@ def main():
                 "kernel": kname,
                 "kernel_avg_us": kern_avg * 1e3,
                 "kernel_max_us": kern_max * 1e3,
-                "kernel_timing": (("HIP events at the two ends of the timed region (the launch stream), "
-                                   "divided by the launches: every step is one IMPC launch; max from ")
-                                  if kernel_only else "average and max from ")
-                                 + "HIP events around the IMPC kernel, every step of an identical replay of "
-                                   "the timed steps" + (
-                                     " (statuses bit-identical to the timed pass)" if replay_same else ""),
+                "kernel_timing": ("the device clock of every IMPC launch of the timed pass: first-wave start "
+                                  "to last-wave end (s_memrealtime, mpccbf_run::kernel_clock), the kernel's own "
+                                  "duration as rocprof reports it" if launch_avg > 0 else
+                                  "HIP events around every IMPC launch (host-driven loop)"),
+                "step_region_avg_us": None if region_avg is None else region_avg * 1e3,
+                "step_region_timing": "HIP events at the two ends of the timed region divided by the steps "
+                                      "(kernel + fallback / insert launches + dispatch gaps)",
                 "kernel_event_bracket_avg_us": kern_bracket * 1e3,
+                "kernel_event_bracket_timing": "HIP events around the IMPC launch(es) of every step of an "
+                                               "identical replay of the timed steps" + (
+                                                   " (statuses bit-identical to the timed pass)" if replay_same else ""),
                 "flops_per_launch": flops_per_launch,
                 "flops_model": "executed solver steps (dual active-set + PDIP Newton) x the FP64 flops "
                                "of an active-set step (bench.py flops_per_qp_sep, a lower bound); QPs "
@@ -572,6 +595,22 @@ def main():
         res["roofline"]["occupancy_source"] = occ_src
         res["roofline"]["sq_wait_frac"] = (sq_wait / sq_cyc) if (sq_wait is not None and sq_cyc) else None
         res["roofline"]["sq_wait_source"] = sq_src
+        # FP64 the kernel issued (PMC: FMA x 2 + MUL + ADD + TRANS wave instructions x 64 lanes per
+        # launch) against the vector FP64 peak over the launch: what the hardware executed,
+        # assembly and outputs included, where `frac` counts the solver's algorithmic flops only
+        f64 = [pmc_lookup(kname, wl, c)[0] for c in ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64",
+                                                      "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_TRANS_F64")]
+        if all(v is not None for v in f64):
+            issued = (2 * f64[0] + f64[1] + f64[2] + f64[3]) * 64
+            res["roofline"]["fp64_issued"] = {
+                "flops_per_launch": issued, "achieved_tflops": issued / (kern_avg * 1e-3) / 1e12,
+                "frac": issued / (kern_avg * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                "source": pmc_lookup(kname, wl, "SQ_INSTS_VALU_FMA_F64")[1]}
+        # the launch against its longest agent chain (stamps build: setup .. outputs of the slowest
+        # agent, tools/stamp_profile.py): what a latency-bound launch cannot go below
+        cp = critical_path_lookup(kname, wl, per)
+        if cp is not None:
+            res["roofline"]["critical_path"] = cp
         if trace_res is not None:
             res["closed_loop"] = closed_loop_metrics(trace_res, targets_h, cfg, fov)
         if not args.no_cpu_baseline and world == 1:
@@ -656,6 +695,24 @@ def closed_loop_metrics(tr, targets_h, cfg, fov):
         "last_step_agents_within_dmin": int(within.sum()),
         "shape": "box [0.2, 0.2] (base_config.json robot_params.collision_shape), goal radius 1 m",
     }
+
+
+def critical_path_lookup(kname: str, workload: str, agents: int):
+    """The slowest agent's stamped chain and the span of the stamped launch for `kname` at this
+    agent count, from the newest committed profiles/r*_critical_path.json (tools/stamp_profile.py
+    --json). None if absent."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_critical_path.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for e in d.get("entries", []):
+            if e.get("kernel") == kname and e.get("workload", "collision") == workload and e.get("agents") == agents:
+                return {"slowest_agent_chain_us": e["agent_wall_max_us"], "stamped_span_us": e["span_us"],
+                        "agent_chain_mean_us": e["agent_wall_mean_us"], "phases_mean_us": e.get("phases_mean_us"),
+                        "source": os.path.relpath(f, REPO)}
+    return None
 
 
 def pmc_traffic(kname: str, workload: str):

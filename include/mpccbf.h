@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 10
+#define MPCCBF_ABI_VERSION 11
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -260,12 +260,21 @@ typedef struct mpccbf_run {
     int32_t solve_stride;   /* time the IMPC kernel on every solve_stride-th step only (<= 1: all);
                                solve_ms of untimed steps is set to -1 */
     int32_t final_table;    /* out: 0 = batch->states holds the final states, 1 = states_alt */
+    /* ABI 11: device clock of every step's IMPC launch, or NULL: 2 x num_steps uint64 (device,
+     * zero-filled by the call): per step the bitwise complement of the s_memrealtime counter
+     * (100 MHz) when the launch's first wave started, and the counter when its last wave finished
+     * — the kernel's own duration (end - ~start), without the dispatch gaps that events around it
+     * include */
+    uint64_t* kernel_clock;
 } mpccbf_run;
 
 int mpccbf_run_steps(mpccbf_ctx* ctx, const mpccbf_batch* batch, mpccbf_run* run, void* hip_stream);
 
-/* Tuning knob: kernel geometry for mpccbf_impc_solve. 0 (default): 16 lanes per agent,
- * 4 row slots per lane; 1: 64 lanes per agent, 1 slot; 2: 64 lanes, 4 slots (wide rows). */
+/* Tuning knob: kernel layout for mpccbf_impc_solve. 0 (default): share-adaptive — the separable
+ * collision controller runs one agent per wave64 (impc_wide_kernel) up to one agent per SIMD of the
+ * device (1,024 on MI355X) and 16 lanes per agent (impc_sep_kernel, 4 agents per wave) beyond;
+ * 4: the 16-lane kernel at any count; 5: the one-agent-per-wave kernel at any count; 1 / 3: the
+ * dense 6 x 6 layouts (64 / 16 lanes per agent). */
 int mpccbf_set_variant(mpccbf_ctx* ctx, int variant);
 /* Name of the IMPC kernel instantiation the current variant launches (diagnostics). */
 const char* mpccbf_kernel_name(const mpccbf_ctx* ctx);

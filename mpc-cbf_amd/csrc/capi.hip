@@ -39,9 +39,9 @@ int launch_neighbors(const double* states, int num_states, int first, int num_ag
                      size_t scratch_bytes, hipStream_t s);
 size_t neighbors_scratch_bytes(int num_states, int num_agents, int k);
 size_t grid_table_bytes(int num_states);
-void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots);
+void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots, double** sst);
 hipError_t launch_grid_insert(const double* states, int n, int skip0, int skip1, double radius,
-                              uint32_t* cnt, uint32_t* slots, hipStream_t s);
+                              uint32_t* cnt, uint32_t* slots, double* sst, hipStream_t s);
 
 static thread_local std::string g_err;
 
@@ -98,7 +98,8 @@ static void pack(std::vector<double>& v, int32_t& off, const std::vector<Mat>& m
 }
 
 // The three neighbour tables of grid mode in ctx scratch (grown on demand).
-static int grid_tables(mpccbf_ctx* c, int num_states, uint32_t* (&cnt)[3], uint32_t* (&slots)[3]) {
+static int grid_tables(mpccbf_ctx* c, int num_states, uint32_t* (&cnt)[3], uint32_t* (&slots)[3],
+                       double* (&sst)[3]) {
     const size_t tb = grid_table_bytes(num_states);
     if (3 * tb > c->grid_bytes) {
         if (c->grid_scratch) (void)hipFree(c->grid_scratch);
@@ -107,7 +108,8 @@ static int grid_tables(mpccbf_ctx* c, int num_states, uint32_t* (&cnt)[3], uint3
         HIP_TRY(hipMalloc(&c->grid_scratch, 3 * tb));
         c->grid_bytes = 3 * tb;
     }
-    for (int t = 0; t < 3; t++) grid_table_carve((char*)c->grid_scratch + t * tb, num_states, &cnt[t], &slots[t]);
+    for (int t = 0; t < 3; t++)
+        grid_table_carve((char*)c->grid_scratch + t * tb, num_states, &cnt[t], &slots[t], &sst[t]);
     return MPCCBF_OK;
 }
 
@@ -116,7 +118,7 @@ static int grid_tables(mpccbf_ctx* c, int num_states, uint32_t* (&cnt)[3], uint3
 // kernel); gstep >= 0 (mpccbf_run_steps) reads table gstep % 3, which the previous step filled,
 // has the kernel insert its next states into table (gstep + 1) % 3 and zero table (gstep + 2) % 3.
 int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEvent_t ev0, hipEvent_t ev1,
-                 int gstep = -1) {
+                 int gstep = -1, unsigned long long* kclock = nullptr) {
     if (!c || !b) return fail(MPCCBF_ERR_INVALID_ARGUMENT, "null argument");
     if (b->num_agents < 0 || b->agent_first < 0 || b->agent_first + b->num_agents > b->num_states)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "agent range outside states");
@@ -138,21 +140,25 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     HIP_TRY(hipSetDevice(c->device));
     if (grid) {
         uint32_t *cnt[3], *slots[3];
-        const int rc = grid_tables(c, b->num_states, cnt, slots);
+        double* sst[3];
+        const int rc = grid_tables(c, b->num_states, cnt, slots, sst);
         if (rc != MPCCBF_OK) return rc;
         const uint32_t T = grid_table_size(b->num_states);
         int rd = 0;
         if (gstep < 0) {
             HIP_TRY(hipMemsetAsync(cnt[0], 0, (size_t)T * 4, stream));
-            HIP_TRY(launch_grid_insert(b->states, b->num_states, 0, 0, b->knn_radius, cnt[0], slots[0], stream));
+            HIP_TRY(launch_grid_insert(b->states, b->num_states, 0, 0, b->knn_radius, cnt[0], slots[0], sst[0],
+                                       stream));
         } else {
             rd = gstep % 3;
             a.grid.ins_cnt = cnt[(gstep + 1) % 3];
             a.grid.ins_slots = slots[(gstep + 1) % 3];
+            a.grid.ins_sst = sst[(gstep + 1) % 3];
             a.grid.clr_cnt = cnt[(gstep + 2) % 3];
         }
         a.grid.cnt = cnt[rd];
         a.grid.slots = slots[rd];
+        a.grid.sst = sst[rd];
         a.grid.mask = T - 1;
         a.grid.inv_cell = 1.0 / b->knn_radius;
         a.grid.radius = b->knn_radius;
@@ -184,6 +190,7 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     a.dual_res = b->dual_res;
     a.substeps = b->substeps;
     a.nb_out = b->nb_out;
+    a.kclock = kclock;
     if (b->substeps && !b->traj_t)
         return fail(MPCCBF_ERR_INVALID_ARGUMENT, "substeps (closed-loop records) needs traj_t");
     // fallback launch: agents the main launch defers (the lean launch: QPs that need the PDIP or
@@ -276,43 +283,8 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     d.cbf_h = o.cbf_h;
     d.impc_iter = p->impc_iter;
     std::vector<double> v;
-    pack(v, d.o_Z, o.Z);
-    pack(v, d.o_Xs, o.Xs);
-    pack(v, d.o_Pr, o.Pr);
-    pack(v, d.o_LPr, o.LPr);
-    pack(v, d.o_Qs, o.Qs);
-    pack(v, d.o_Qt, o.Qt);
-    pack(v, d.o_Qr, o.Qr);
-    pack(v, d.o_Ks, o.Ks);
-    pack(v, d.o_Kt, o.Kt);
-    pack(v, d.o_Kr, o.Kr);
-    pack(v, d.o_G, o.G);
-    pack(v, d.o_Gs, o.Gs);
-    pack(v, d.o_lo, o.lo);
-    pack(v, d.o_hi, o.hi);
-    pack(v, d.o_Cs, o.Cs);
-    pack(v, d.o_clo, o.clo);
-    pack(v, d.o_chi, o.chi);
-    pack(v, d.o_UZ, o.UZ);
-    pack(v, d.o_US, o.US);
-    pack(v, d.o_PZ, o.PZ);
-    pack(v, d.o_PS, o.PS);
-    pack(v, d.o_AZ, o.AZ);
-    pack(v, d.o_AS, o.AS);
-    d.P = p->num_pieces;
-    d.slack_mode = p->slack_mode ? 1 : 0;
-    d.slack_cost = p->slack_cost;
-    d.slack_decay = p->slack_decay_rate;
-    pack(v, d.o_EB0, o.EB0);
-    pack(v, d.o_EB1, o.EB1);
-    pack(v, d.o_cum, o.cum);
-    d.eval_step = o.eval_step;
-    {
-        const double tend = o.cum.empty() ? 0.0 : o.cum.back();
-        d.az_at_eval = (!o.cum.empty() && std::min(o.eval_step, tend) == std::min(p->h, tend)) ? 1 : 0;
-    }
-    d.Ts = p->Ts;
-    d.nsub = (int)(p->h / p->Ts);
+    // operator buffer: the operators of the separable kernels first (the "hot" prefix the
+    // one-agent-per-wave kernel stages in LDS, DevOps::hot), then the rest
     // separable layout: box rows regrouped by channel, 16 per channel (lanes of a group)
     d.sep = 0;
     d.o_Gsep = 0;
@@ -358,6 +330,44 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
             d.sep_rows_per_dim = rpd;
         }
     }
+    pack(v, d.o_Z, o.Z);
+    pack(v, d.o_Xs, o.Xs);
+    pack(v, d.o_Pr, o.Pr);
+    pack(v, d.o_Qs, o.Qs);
+    pack(v, d.o_Qt, o.Qt);
+    pack(v, d.o_Qr, o.Qr);
+    pack(v, d.o_Ks, o.Ks);
+    pack(v, d.o_Kt, o.Kt);
+    pack(v, d.o_Kr, o.Kr);
+    pack(v, d.o_Cs, o.Cs);
+    pack(v, d.o_clo, o.clo);
+    pack(v, d.o_chi, o.chi);
+    pack(v, d.o_UZ, o.UZ);
+    pack(v, d.o_US, o.US);
+    pack(v, d.o_PZ, o.PZ);
+    pack(v, d.o_PS, o.PS);
+    pack(v, d.o_AZ, o.AZ);
+    pack(v, d.o_AS, o.AS);
+    d.P = p->num_pieces;
+    d.slack_mode = p->slack_mode ? 1 : 0;
+    d.slack_cost = p->slack_cost;
+    d.slack_decay = p->slack_decay_rate;
+    pack(v, d.o_EB0, o.EB0);
+    pack(v, d.o_EB1, o.EB1);
+    pack(v, d.o_cum, o.cum);
+    d.hot = (int32_t)v.size();
+    pack(v, d.o_LPr, o.LPr);
+    pack(v, d.o_G, o.G);
+    pack(v, d.o_Gs, o.Gs);
+    pack(v, d.o_lo, o.lo);
+    pack(v, d.o_hi, o.hi);
+    d.eval_step = o.eval_step;
+    {
+        const double tend = o.cum.empty() ? 0.0 : o.cum.back();
+        d.az_at_eval = (!o.cum.empty() && std::min(o.eval_step, tend) == std::min(p->h, tend)) ? 1 : 0;
+    }
+    d.Ts = p->Ts;
+    d.nsub = (int)(p->h / p->Ts);
     // FoV controller: Voronoi operators, dense 16-wide box rows, P / LP padded to 16 x 16
     d.cbf_mode = p->cbf_mode;
     d.C = p->num_control_points;
@@ -698,6 +708,8 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(hipSetDevice(c->device));
     const bool timing = r->step_ms || r->solve_ms;
+    if (r->kernel_clock && r->num_steps > 0)  // (the start is kept complemented: zero for both)
+        HIP_TRY(hipMemsetAsync(r->kernel_clock, 0, 2 * sizeof(uint64_t) * (size_t)r->num_steps, stream));
     const int need = 3 * std::max(r->num_steps, r->reserve_steps) + 1;
     while ((int)c->events.size() < need) {
         hipEvent_t e;
@@ -713,15 +725,16 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
     // (each IMPC launch zeroes the table two steps ahead, see impc_enqueue)
     const bool gtab = b->nb_row_ptr == nullptr && count > 0 && r->num_steps > 0;
     uint32_t *gcnt[3] = {}, *gslots[3] = {};
+    double* gsst[3] = {};
     if (gtab) {
         if (b->knn_k < 1 || !(b->knn_radius > 0))
             return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
-        const int rc = grid_tables(c, ns, gcnt, gslots);
+        const int rc = grid_tables(c, ns, gcnt, gslots, gsst);
         if (rc != MPCCBF_OK) return rc;
         const size_t cb = (size_t)grid_table_size(ns) * 4;
         HIP_TRY(hipMemsetAsync(gcnt[0], 0, cb, stream));
         HIP_TRY(hipMemsetAsync(gcnt[1], 0, cb, stream));
-        HIP_TRY(launch_grid_insert(b->states, ns, 0, 0, b->knn_radius, gcnt[0], gslots[0], stream));
+        HIP_TRY(launch_grid_insert(b->states, ns, 0, 0, b->knn_radius, gcnt[0], gslots[0], gsst[0], stream));
     }
     for (int s = 0; s < r->num_steps; s++) {
         double* cur = tables[s & 1];
@@ -741,7 +754,8 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
         }
         const bool tk = r->solve_ms && (r->solve_stride <= 1 || s % r->solve_stride == 0);
         const int rc = impc_enqueue(c, &sb, stream, tk ? ev[3 * s + 1] : nullptr, tk ? ev[3 * s + 2] : nullptr,
-                                    gtab ? s : -1);
+                                    gtab ? s : -1,
+                                    r->kernel_clock ? (unsigned long long*)r->kernel_clock + 2 * (size_t)s : nullptr);
         if (rc != MPCCBF_OK) return rc;
         if (r->comm && r->comm->nranks > 1 && r->comm->local) {
             // in-process group: every rank's block of this step copied into this rank's table
@@ -765,7 +779,7 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
         // of the next step
         if (gtab && count < ns)
             HIP_TRY(launch_grid_insert(nxt, ns, first, first + count, b->knn_radius, gcnt[(s + 1) % 3],
-                                       gslots[(s + 1) % 3], stream));
+                                       gslots[(s + 1) % 3], gsst[(s + 1) % 3], stream));
         if (r->step_ms || (timing && s == r->num_steps - 1)) HIP_TRY(hipEventRecord(ev[3 * s + 3], stream));
     }
     guard.g = nullptr;  // every barrier of the call passed: the peers no longer wait on this rank

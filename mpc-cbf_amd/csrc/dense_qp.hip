@@ -750,10 +750,12 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     for (size_t b = 0; b < big.size() && e == hipSuccess; b++) {
         const ReducedQP& r = hred[b];
         int st_b = RS_SOLVE;
-        if (r.status == MPCCBF_INFEASIBLE) st_b = MPCCBF_INFEASIBLE;
+        // the device kernel's order (dense_reduce_kernel): inconsistent equalities, then capacity,
+        // then a violated constant row
+        if (r.eq_infeasible) st_b = MPCCBF_INFEASIBLE;
         else if (r.nz > DENSE_NZ) st_b = RS_CAP_NZ;
         else if (r.m > DENSE_ROWS) st_b = RS_CAP_ROWS;
-        else if (r.status >= 0) st_b = r.status;  // (nz = 0: x = xp)
+        else if (r.status >= 0) st_b = r.status;  // (a violated constant row; nz = 0: x = xp)
         std::vector<double>& blk = hblk[b];
         blk.assign((size_t)DQ_HDR + (size_t)std::min(r.m, DENSE_ROWS) * DQ_ROW, 0.0);
         double pmax = 0.0;

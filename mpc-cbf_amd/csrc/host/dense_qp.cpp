@@ -80,7 +80,7 @@ ReducedQP reduce_dense_qp(const mpccbf_dense_qp& qp) {
     for (int k = 0; k < E.r; k++) {
         double v = 0.0;
         for (int j = 0; j < n; j++) v += E(k, j) * r.xp[j];
-        if (std::fabs(v - eq_rhs[k]) > kFeasTol) r.status = MPCCBF_INFEASIBLE;
+        if (std::fabs(v - eq_rhs[k]) > kFeasTol) r.status = MPCCBF_INFEASIBLE, r.eq_infeasible = true;
     }
 
     // ---- reduced objective: x^T Hs x with x = xp + Z y  ->  1/2 y^T (2 Z^T Hs Z) y + ...

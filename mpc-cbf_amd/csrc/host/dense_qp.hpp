@@ -21,6 +21,8 @@ namespace mpccbf {
 struct ReducedQP {
     int n = 0, nz = 0, m = 0;
     int status = -1;            // >= 0: decided on the host (no device solve needed)
+    bool eq_infeasible = false; // inconsistent equalities (INFEASIBLE whatever the sizes; a violated
+                                // constant row is INFEASIBLE only within the device capacity)
     bool pd = false;            // P positive definite (Cholesky start available)
     Mat Z;                      // n x nz
     std::vector<double> xp;     // n

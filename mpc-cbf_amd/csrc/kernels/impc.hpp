@@ -64,6 +64,9 @@ struct DevOps {
     // a fresh curve's evaluation time min(eval_step, T_end), so the next state of an agent with a new
     // curve is one operator product (no piece lookup and Bernstein evaluation on the device)
     int32_t az_at_eval;
+    // the operator buffer's prefix [0, hot) holds every operator of the separable collision kernels
+    // (staged in LDS by impc_wide_kernel)
+    int32_t hot;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;
@@ -79,12 +82,17 @@ constexpr int SEP_NZD_HOST = 2;  // reduced variables per channel the separable 
 // scan: mpccbf_run_steps rotates three tables (read this step | filled with this step's next
 // states by the IMPC kernel itself | zeroed by the IMPC kernel for the step after next).
 constexpr int GRID_CAP = 64;
+// The first GRID_SST slots of every bucket also carry their row's planar state (px, py, vx, vy):
+// a query reads the 3 x 3 cells' counts, entries and states in one round trip (impc_wide.hpp)
+constexpr int GRID_SST = 7;
 
 struct GridArgs {
     const uint32_t* cnt;   // T bucket counts of the table read this step
     const uint32_t* slots; // GRID_CAP x T state rows (slot-major)
+    const double* sst;     // GRID_SST x T x 4: slot j < GRID_SST's (px, py, vx, vy) (slot-major)
     uint32_t* ins_cnt;     // table of the next step (NULL: none): next_states rows are inserted
     uint32_t* ins_slots;
+    double* ins_sst;
     uint32_t* clr_cnt;     // bucket counts zeroed by this launch (NULL: none)
     uint32_t mask;
     double inv_cell;
@@ -102,11 +110,17 @@ __host__ __device__ inline uint32_t cell_hash(long long cx, long long cy, uint32
     return (uint32_t)(h ^ (h >> 29)) & mask;
 }
 
-// insert state row `row` at planar position (x, y) into the table (ins_cnt, ins_slots)
-__device__ inline void grid_insert(const GridArgs& g, double x, double y, uint32_t row) {
+// insert state row `row` at planar position (x, y), velocity (vx, vy) into the table (ins_cnt,
+// ins_slots, ins_sst)
+__device__ inline void grid_insert(const GridArgs& g, double x, double y, double vx, double vy, uint32_t row) {
     const uint32_t h = cell_hash((long long)floor(x * g.inv_cell), (long long)floor(y * g.inv_cell), g.mask);
     const uint32_t j = atomicAdd(&g.ins_cnt[h], 1u);
-    if (j < (uint32_t)GRID_CAP) g.ins_slots[(size_t)j * (g.mask + 1u) + h] = row;
+    const size_t e = (size_t)j * (g.mask + 1u) + h;
+    if (j < (uint32_t)GRID_CAP) g.ins_slots[e] = row;
+    if (j < (uint32_t)GRID_SST) {
+        double4* d = reinterpret_cast<double4*>(g.ins_sst) + e;
+        *d = make_double4(x, y, vx, vy);
+    }
 }
 
 // hash table size for n agents: power of two >= n (>= 1024)
@@ -158,6 +172,9 @@ struct ImpcArgs {
     double* substeps;
     // diagnostics: num_agents x 16 neighbour ids as the kernel uses them (-1 padded), or nullptr
     int32_t* nb_out;
+    // launch clock (mpccbf_run::kernel_clock): [0] = ~(min over waves of the start), [1] = max of
+    // the end (s_memrealtime, 100 MHz), or nullptr
+    unsigned long long* kclock;
 };
 
 constexpr int NSTAMP = 8;

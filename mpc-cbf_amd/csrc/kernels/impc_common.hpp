@@ -834,7 +834,7 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
         if (have_curve || t_prev >= 0.0) {
             t_new = fmin(t_prev + op.eval_step, tmax);  // example :190-193
             const double* xr = have_curve ? nullptr : args.x + (size_t)ai * op.n;
-            if (AZE && have_curve && op.az_at_eval && !args.substeps) {
+            if (AZE && have_curve && op.az_at_eval) {
                 // a fresh curve at min(eval_step, T_end) = min(h, T_end): the AZ / AS rows
                 const double* AZ = opp(buf, op.o_AZ);
                 const double* AS = opp(buf, op.o_AS);
@@ -886,10 +886,10 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
     }
     if (args.substeps) args.substeps[((size_t)ai * op.nsub + op.nsub - 1) * 6 + gl] = v;
     if (args.next_states) args.next_states[(size_t)ai * 6 + gl] = v;
-    if (args.grid.ins_cnt) {  // the next step's neighbour table gets this row (lane 0: x, lane 1: y)
+    if (args.grid.ins_cnt) {  // the next step's neighbour table gets this row (lanes 0, 1, 3, 4)
         const int base = (int)(threadIdx.x & 63u) & ~(G - 1);
-        const double y = __shfl(v, base + 1, 64);
-        if (gl == 0) grid_insert(args.grid, v, y, (uint32_t)(args.agent_first + ai));
+        const double y = __shfl(v, base + 1, 64), vx = __shfl(v, base + 3, 64), vy = __shfl(v, base + 4, 64);
+        if (gl == 0) grid_insert(args.grid, v, y, vx, vy, (uint32_t)(args.agent_first + ai));
     }
 }
 
@@ -913,6 +913,18 @@ __device__ __forceinline__ void grid_clear(const ImpcArgs& args) {
     const uint32_t T = args.grid.mask + 1u;
     const uint32_t nthr = gridDim.x * blockDim.x;
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < T; e += nthr) args.grid.clr_cnt[e] = 0u;
+}
+
+// launch clock (ImpcArgs::kclock): the earliest wave start and the latest wave end of the launch
+// (s_memrealtime, 100 MHz, chip-wide), one non-returning atomic per wave each; the start is kept
+// complemented (max of ~t = ~min t) so one zero fill initialises both
+__device__ __forceinline__ void kclock_start(const ImpcArgs& args) {
+    if (args.kclock && (threadIdx.x & 63u) == 0)
+        atomicMax(&args.kclock[0], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void kclock_end(const ImpcArgs& args) {
+    if (args.kclock && (threadIdx.x & 63u) == 0)
+        atomicMax(&args.kclock[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // diagnostics: wall-clock stamp (s_memrealtime, 100 MHz, chip-wide) of phase `k` of agent ai —

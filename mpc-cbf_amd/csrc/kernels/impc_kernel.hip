@@ -98,6 +98,7 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
     }
     const bool nb_overflow = nnb < 0;
     if (nb_overflow) nnb = 0;
+    write_nb_out(args, ai, gl, grid_mode, nb_scratch[gib], nb0, nnb);
     stamp(args, ai, gl, 2);
 
     double y[NZ], ykeep[NZ];
@@ -865,11 +866,13 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     const int gib = threadIdx.x / 16;
     lds_poison();
     if constexpr (!QUEUE) {
+        kclock_start(args);
         grid_clear(args);
         const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * GPB + gib;
         if (ai >= args.num_agents) return;
         impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
                                                    nb_scratch[gib], keep_all[gib]);
+        kclock_end(args);
     } else {
         // one queue entry per group (no grid-stride loop: carried across iterations the agent's
         // state spills, 0 -> 352 B/lane); groups beyond the queue's length leave at once. The
@@ -904,9 +907,11 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
     const bool grid_mode = args.nb_row_ptr == nullptr;
     WideQuery gq;
     WideCells gc;
-    if (grid_mode) wn_begin(args, s0[0], s0[1], gl, gq);
+    if (grid_mode) wn_issue(args, s0[0], s0[1], gl, gq);
+    // linear term: lane i < 6 forms q_i, the constant's terms summed over the first 16-lane row
+    // (agent_linear_term_lanes; lanes >= 9 contribute 0, so the row total is the whole sum)
     double kconst;
-    const double qlane = agent_linear_term_lanes<NZ, 64>(op, buf, args, ai, s0, gl, kconst);
+    const double qlane = agent_linear_term_lanes<NZ, 16>(op, buf, args, ai, s0, gl, kconst);
     // this lane's box row: channel d = gl / 16, slot gl % 16 (host layout [channel][16][SEP_ROW])
     WRow rw;
     {
@@ -933,12 +938,11 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
         rw.hi = gl < W_BOX ? rv[9] - sh : 1.0;
         const double* pd = opp(buf, op.o_Pinv) + 3 * (d < SEP_D ? d : 0);
         rw.w = wide_weight(wide_n2(pd[0], pd[1], pd[2], rv[0], rv[1]));
+        rw.sl = rcp(1.0 + fabs(rw.lo));
+        rw.su = rcp(1.0 + fabs(rw.hi));
     }
-    if (grid_mode) {
-        wn_cells(args, gq, gc);
-        wn_slots(args, gc, gl, gq);
-    }
-    if (grid_mode) wn_states(args, gc, gl, gq);
+    wide_sample_us(op, buf, s0, L, gl);
+    if (grid_mode) wn_cells(args, gq, gc);
     const bool infeasible = constant_rows_infeasible<64>(op, buf, s0, gl);
     stamp(args, ai, gl, 1);
 
@@ -956,26 +960,55 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
     if (nb_overflow) nnb = 0;
     stamp(args, ai, gl, 2);
 
-    double q[NZ];
+    double q[NZ], yu[NZ];
 #pragma unroll
     for (int j = 0; j < NZ; j++) q[j] = lane_of(qlane, j);
     kconst = uni(kconst);
+    const double* Pinv = opp(buf, op.o_Pinv);
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++) {  // the unconstrained minimiser -P^-1 q (both IMPC iterations)
+        const int o = 2 * d;
+        yu[o] = -fma(Pinv[3 * d], q[o], Pinv[3 * d + 1] * q[o + 1]);
+        yu[o + 1] = -fma(Pinv[3 * d + 1], q[o], Pinv[3 * d + 2] * q[o + 1]);
+    }
+    // non-finite data (a NaN / Inf state, target or neighbour state): such a model is not solved
+    // (CPLEX rejects non-finite coefficients), ERROR; the linear term and the box rows are checked
+    // here, the CBF rows per iteration
+    bool nfin_fixed;
+    {
+        bool nf = gl < W_BOX && (!isfinite(rw.lo) || !isfinite(rw.hi));
+#pragma unroll
+        for (int j = 0; j < NZ; j++) nf = nf || !isfinite(q[j]);
+        nfin_fixed = __ballot(nf) != 0ull;
+    }
+#ifdef MPCCBF_PDIP_STAMPS
+    long long* wdbg = args.stamps ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 16 : nullptr;
+#else
+    long long* wdbg = nullptr;
+#endif
     double y[NZ], yk[NZ];
 #pragma unroll
     for (int j = 0; j < NZ; j++) y[j] = yk[j] = 0.0;
     bool have_curve = false, success = true;
     if (gl == 0) L.act[POL_K] = 0.0;
     int steps0 = 0;
-    const double* Pinv = opp(buf, op.o_Pinv);
+    // per-iteration results, written together after the loop (impc_iter <= 2 here; more iterations
+    // are written as they finish)
+    int st_w0 = ST_UNKNOWN, st_w1 = ST_UNKNOWN, nit_w0 = 0, nit_w1 = 0;
+    double obj_w0 = __builtin_nan(""), obj_w1 = __builtin_nan(""), prs_w0 = obj_w0, prs_w1 = obj_w0,
+           drs_w0 = obj_w0, drs_w1 = obj_w0;
+    const bool want_rp = args.primal_res != nullptr;
 
     for (int it = 0; it < op.impc_iter; it++) {
         const size_t oi = (size_t)ai * op.impc_iter + it;
         if (!success) {  // the reference breaks out of the IMPC loop (:208-211)
-            write_iteration(args, oi, gl, ST_UNKNOWN, __builtin_nan(""), 0);
+            if (it >= 2) write_iteration(args, oi, gl, ST_UNKNOWN, __builtin_nan(""), 0);
             continue;
         }
         bool row_infeasible = false;
-        const int count = uni_i(wide_cbf_rows(op, buf, args, it, s0, y, grid_mode, L, nb0, nnb, gl, row_infeasible));
+        long long* wd = it == 0 ? wdbg : nullptr;
+        const int count = uni_i(wide_cbf_rows(op, buf, args, it, s0, y, grid_mode, L, nb0, nnb, gl, row_infeasible, wd));
+        bool nfin = false;
         if (gl >= W_BOX) {  // this iteration's CBF rows into the CBF lanes (unused: inert 0 <= 1)
             const int c = gl - W_BOX;
             const bool on = c < count;
@@ -983,9 +1016,16 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
 #pragma unroll
             for (int j = 0; j < 4; j++) rw.g[j] = on ? src[j] : 0.0;
             rw.hi = on ? src[4] : 1.0;
-            const double* Pi = opp(buf, op.o_Pinv);
-            rw.w = wide_weight(wide_n2(Pi[0], Pi[1], Pi[2], rw.g[0], rw.g[1]) +
-                               wide_n2(Pi[3], Pi[4], Pi[5], rw.g[2], rw.g[3]));
+            rw.w = wide_weight(wide_n2(Pinv[0], Pinv[1], Pinv[2], rw.g[0], rw.g[1]) +
+                               wide_n2(Pinv[3], Pinv[4], Pinv[5], rw.g[2], rw.g[3]));
+            rw.su = rcp(1.0 + fabs(rw.hi));
+            nfin = !isfinite(rw.hi) || !isfinite(rw.g[0]) || !isfinite(rw.g[1]) || !isfinite(rw.g[2]) ||
+                   !isfinite(rw.g[3]);
+        }
+        {
+            long long* wdbg = wd;
+            (void)wdbg;
+            WST(4);
         }
         if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
         if (count > W_CBF) {  // beyond the 16 CBF lanes: the fallback launch (8 slots per lane)
@@ -994,11 +1034,7 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
                 return;
             }
         }
-        bool nfin = false;
-#pragma unroll
-        for (int j = 0; j < NZ; j++) nfin = nfin || !isfinite(q[j]) || !isfinite(rw.g[j]);
-        nfin = nfin || !isfinite(rw.hi) || (gl < W_BOX && !isfinite(rw.lo));
-        const bool nonfinite = __ballot(nfin) != 0ull;
+        const bool nonfinite = nfin_fixed || __ballot(nfin) != 0ull;
         int st, nit = 0;
         double prs = __builtin_nan(""), drs = __builtin_nan("");
         if (count > W_CBF || nb_overflow || nonfinite) {
@@ -1006,13 +1042,6 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
         } else if (infeasible || row_infeasible) {
             st = ST_INFEASIBLE;
         } else {
-            double yu[NZ];
-#pragma unroll
-            for (int d = 0; d < SEP_D; d++) {
-                const int o = 2 * d;
-                yu[o] = -fma(Pinv[3 * d], q[o], Pinv[3 * d + 1] * q[o + 1]);
-                yu[o + 1] = -fma(Pinv[3 * d + 1], q[o], Pinv[3 * d + 2] * q[o + 1]);
-            }
             int k0 = 0;
             if (it > 0 && op.das_warm > 0 && steps0 >= op.das_warm) {
                 wave_lds_sync();
@@ -1020,9 +1049,10 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
             }
             double tl = 0.0;
             const int r = wide_dual_as(rw, opp(buf, op.o_Pr), Pinv, q, yu, op.tol, op.dual_as, L.pol, y, prs, drs,
-                                       nit, tl, k0, L.act, it == 0 ? L.act : nullptr);
+                                       nit, tl, k0, L.act, it == 0 ? L.act : nullptr, want_rp, wd);
             if (r > 0) {
                 st = ST_OPTIMAL;
+                if (!want_rp) prs = __builtin_nan("");
             } else if (r < 0 && tl > 10.0 * op.feas_tol) {
                 st = ST_INFEASIBLE;
                 prs = tl;
@@ -1037,33 +1067,75 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
         }
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {
-            objv = reduced_objective<NZ>(op, buf, q, y, kconst);
+            // 1/2 y^T P y + q^T y + k (reduced_objective) on the first 16-lane row: lane i < 6 row i
+            const double* Pr = opp(buf, op.o_Pr) + (size_t)(gl < NZ ? gl : 0) * NZ;
+            double pr[NZ], pyi = 0.0, yi = y[0], qi = q[0];
+#pragma unroll
+            for (int j = 0; j < NZ; j++) pr[j] = Pr[j];
+#pragma unroll
+            for (int j = 1; j < NZ; j++) {
+                yi = gl == j ? y[j] : yi;
+                qi = gl == j ? q[j] : qi;
+            }
+#pragma unroll
+            for (int j = 0; j < NZ; j++) pyi = fma(pr[j], y[j], pyi);
+            objv = grp_sum<16>(gl < NZ ? yi * (0.5 * pyi + qi) : (gl == NZ ? kconst : 0.0));
 #pragma unroll
             for (int i = 0; i < NZ; i++) yk[i] = y[i];
             have_curve = true;
         } else {
             success = false;
         }
-        write_iteration(args, oi, gl, st, objv, nit, prs, drs);
+        {
+            long long* wdbg = wd;
+            (void)wdbg;
+            WST(12);
+        }
+        if (it == 0) {
+            st_w0 = st, nit_w0 = nit, obj_w0 = objv, prs_w0 = prs, drs_w0 = drs;
+        } else if (it == 1) {
+            st_w1 = st, nit_w1 = nit, obj_w1 = objv, prs_w1 = prs, drs_w1 = drs;
+        } else {
+            write_iteration(args, oi, gl, st, objv, nit, prs, drs);
+        }
         if (it == 0) steps0 = nit;
         if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
     }
+    write_iteration(args, (size_t)ai * op.impc_iter, gl, st_w0, obj_w0, nit_w0, prs_w0, drs_w0);
+    if (op.impc_iter > 1) write_iteration(args, (size_t)ai * op.impc_iter + 1, gl, st_w1, obj_w1, nit_w1, prs_w1, drs_w1);
     write_agent_outputs<NZ, 64>(op, buf, args, ai, gl, s0, yk, have_curve);
     stamp(args, ai, gl, 7);
-    return;
 }
 
+// The operators (the buffer's hot prefix, DevOps::hot doubles) are staged into LDS once per block,
+// while the agents' state loads are in flight: every operator read of the agent chain is then an
+// LDS read (~100 cycles) instead of a scalar / vector memory round trip (~1,000 cycles under load).
 template <int BS>
 __global__ void __launch_bounds__(BS) impc_wide_kernel(const DevOps op, const double* __restrict__ buf,
                                                         const ImpcArgs args) {
     constexpr int WPB = BS / 64;
+    constexpr int PER = WIDE_OPS / BS;
     __shared__ WideLds lds_all[WPB];
+    __shared__ double ops[WIDE_OPS];
     lds_poison();
+    kclock_start(args);
+    {
+        double v[PER];
+#pragma unroll
+        for (int r = 0; r < PER; r++) {
+            const int i = r * BS + (int)threadIdx.x;
+            v[r] = i < op.hot ? buf[i] : 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < PER; r++) ops[r * BS + threadIdx.x] = v[r];
+    }
     grid_clear(args);
+    __syncthreads();
     const int wv = uni_i((int)(threadIdx.x >> 6));
     const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * WPB + wv;
     if (ai >= args.num_agents) return;
-    impc_wide_agent(op, buf, args, ai, lds_all[wv]);
+    impc_wide_agent(op, ops, args, ai, lds_all[wv]);
+    kclock_end(args);
 }
 
 }  // namespace dev
@@ -1092,7 +1164,7 @@ static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const I
 // variables) with the dual active set on; CBF samples <= MAX_CBF_H.
 static bool impc_wide_ok(const DevOps& op) {
     return op.cbf_mode == 0 && !op.slack_mode && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 &&
-           op.dual_as > 0 && op.cbf_h <= MAX_CBF_H;
+           op.dual_as > 0 && op.cbf_h <= MAX_CBF_H && op.hot > 0 && op.hot <= dev::WIDE_OPS;
 }
 
 // Agents per launch up to which the default layout is the wide kernel: one wave per agent at one

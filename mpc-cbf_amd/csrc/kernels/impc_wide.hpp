@@ -45,6 +45,8 @@ constexpr int W_ROW = 5;    // staged CBF row: 4 coefficients (x0, x1, y0, y1) +
 // active sides the wide solver holds (the 16-lane pipeline's POL_K = 6: a QP that needs more is
 // deferred to it; k <= 2 at steady state)
 constexpr int WK = 4;
+// operator doubles the wide kernel stages in LDS (DevOps::hot must fit: ~1,700 at K = 15)
+constexpr int WIDE_OPS = 2048;
 
 // ---- wave-uniform helpers -------------------------------------------------------------------
 __device__ __forceinline__ double uni(double v) {  // lane 0's value, as a scalar (uniform) operand
@@ -59,6 +61,22 @@ __device__ __forceinline__ double lane_of(double v, int l) {  // lane l's value 
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+// profiling build (make prof): shader-clock stamps of iteration 0's sub-phases, 16 per agent after
+// the phase stamps (tools/wide_stamps.py): WST(k) writes stamp k of this agent (lane 0)
+#ifdef MPCCBF_PDIP_STAMPS
+#define WST(k)                                                                                         \
+    do {                                                                                               \
+        if (wdbg) {                                                                                    \
+            const long long t_ = (long long)__builtin_amdgcn_s_memtime();                              \
+            if ((threadIdx.x & 63u) == 0) wdbg[k] = t_;                                                \
+        }                                                                                              \
+    } while (0)
+#else
+#define WST(k) \
+    do {       \
+    } while (0)
+#endif
+
 template <int N>
 __device__ __forceinline__ void uni_arr(double (&a)[N]) {
 #pragma unroll
@@ -104,11 +122,45 @@ __device__ __forceinline__ void wave_max2(double& a, double& b) {
     b = fmax(b0, b1);
 }
 
+// 64-lane max of a 32-bit unsigned key (every lane ends with it): DPP row stages folded into
+// v_max_u32, then the permlane16 / permlane32 swaps across the 16-lane rows. The candidate rule's
+// normalised violations are non-negative and reduced as float bit patterns (a violated side has a
+// positive score; the key is 0 when no side is violated), a third of the instructions of the f64
+// max (no NaN canonicalisation, one register instead of two).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, dpp_u32<DPP_XOR1>(v));
+    v = max(v, dpp_u32<DPP_XOR2>(v));
+    v = max(v, dpp_u32<DPP_HALF_MIRROR>(v));
+    v = max(v, dpp_u32<DPP_MIRROR>(v));
+    {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = max(r[0], r[1]);
+    }
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = max(r[0], r[1]);
+    }
+    return v;
+}
+__device__ __forceinline__ double wave_max_f64(double a) {
+    a = grp_max<16>(a);
+    double a0, a1;
+    row_pair<false>(a, a0, a1);
+    a = fmax(a0, a1);
+    row_pair<true>(a, a0, a1);
+    return fmax(a0, a1);
+}
+
 // ---- this lane's row -----------------------------------------------------------------------
 struct WRow {
     double g[SEP_NZ];  // coefficients on y (box: the channel's pair, CBF: x and y pairs)
     double lo, hi;     // CBF lanes: lo = -1e300 (no lower side)
     double w;          // candidate weight 1 / sqrt(g P^-1 g), float-rounded (the 16-lane wrow)
+    double sl, su;     // violation scales 1 / (1 + |lo|), 1 / (1 + |hi|)
 };
 
 // the candidate weight of a row with coefficients (g0, g1) on one channel whose P^-1 block is
@@ -150,7 +202,9 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
                             const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
                             double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
                             int& steps, double& tlow, int k0, const double* __restrict__ warm_ids,
-                            double* __restrict__ save) {
+                            double* __restrict__ save, bool want_rp, long long* wdbg = nullptr) {
+    (void)wdbg;
+    WST(5);
     const int gl = lane_bits_opaque<63>();
     double pi[SEP_D][3];
     sep_pinv(Pinv, pi);
@@ -160,9 +214,9 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
         pb[o][0] = P[o * 6 + 2 * (o / 2)];
         pb[o][1] = P[o * 6 + 2 * (o / 2) + 1];
     }
-    // violation scales 1 / (1 + |bound|); the candidate weight 1 / sqrt(g P^-1 g) is the row's
-    // (WRow::w, formed where the row is)
-    const double sl = rcp(1.0 + fabs(rw.lo)), su = rcp(1.0 + fabs(rw.hi));
+    // violation scales 1 / (1 + |bound|) and the candidate weight 1 / sqrt(g P^-1 g): the row's
+    // (formed where the row is)
+    const double sl = rw.sl, su = rw.su;
     const double w = rw.w;
     double y[SEP_NZ], u[WK];
 #pragma unroll
@@ -214,10 +268,6 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
                 for (int j = 0; j < SEP_NZ; j++) y[j] = fma(i < k0 ? -lam[i] : 0.0, wi[j], y[j]);
             }
             k = k0;
-            uni_arr(y);
-            uni_arr(u);
-            uni_arr(L);
-            uni_arr(dl);
         } else {
 #pragma unroll
             for (int i = 0; i < WK; i++) {
@@ -229,6 +279,7 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
         }
     }
     double m = 0.0;
+    WST(6);
     for (int outer = 0;; outer++) {
         // this lane's sides: scaled violation (convergence) and normalised violation (candidate)
         double vb, eb;
@@ -247,15 +298,20 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
             nanv = vl != vl || vu != vu;
             vb = fmax(-1.0, fmax(vl, vu));
         }
+        if (outer == 0) WST(7);
         if (outer == 0 && __ballot(nanv) != 0ull) return 0;
-        m = vb;
-        double em = eb;
-        wave_max2(m, em);
-        m = uni(m);
-        if (!(m > add_tol)) break;
+        // the candidate: the largest normalised violation (as a float bit pattern; 0: none), its
+        // lowest lane on ties. Converged when no side is violated beyond add_tol (every score 0)
+        const unsigned key = eb > 0.0 ? __float_as_uint((float)eb) : 0u;
+        const unsigned kmax = (unsigned)uni_i((int)wave_max_u32(key));
+        if (outer == 0) WST(8);
+        if (kmax == 0u) {
+            if (want_rp) m = uni(wave_max_f64(vb));  // the scaled primal residual of the returned point
+            break;
+        }
         if (steps >= maxstep) return 0;
-        const int owner = __ffsll((long long)__ballot(eb == em)) - 1;
-        if (owner < 0) return 0;  // (a NaN score)
+        const int owner = __ffsll((long long)__ballot(key == kmax)) - 1;
+        if (owner < 0) return 0;
         if (gl == owner) wide_stage(rw, pi, sb, gl, cand);
         wave_lds_sync();
         if (k == 0) {
@@ -275,10 +331,9 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
             wave_lds_sync();
             if (gl < 16) pol[gl] = cand[gl];
             const double rz = rsqrt(nw);
-            L[S6::idx(0, 0)] = uni(nw * rz);
-            dl[0] = uni(rz);
-            u[0] = uni(t);
-            uni_arr(y);
+            L[S6::idx(0, 0)] = nw * rz;
+            dl[0] = rz;
+            u[0] = t;
             k = 1;
             wave_lds_sync();
             continue;
@@ -376,9 +431,7 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
             }
 #pragma unroll
             for (int i = 0; i < WK; i++) u[i] = i < k ? fma(-t, sgn[i] * rho[i], u[i]) : u[i];
-            uni_arr(y);
-            uni_arr(u);
-            up = uni(up + t);
+            up += t;
             wave_lds_sync();
             if (uni_b(t2 <= t1)) {  // the candidate joins
                 if (k == WK) return 0;
@@ -393,9 +446,6 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
                         if (j == k) L[S6::idx(i, j)] = i < k ? sp * v[i] : (i == k ? zn * rz : L[S6::idx(i, j)]);
                 }
                 k++;
-                uni_arr(u);
-                uni_arr(dl);
-                uni_arr(L);
                 wave_lds_sync();
                 break;
             }
@@ -409,13 +459,11 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
             wave_lds_sync();
             sep_gram<WK>(pol, k, L);
             if (!uni_b(chol_packed<WK>(L, dl))) return 0;
-            uni_arr(u);
-            uni_arr(L);
-            uni_arr(dl);
         }
     }
     // converged: the iterate's dual residual P y + q + G_A^T lam must meet the tolerance (else the
     // 16-lane pipeline re-solves the active set's equality QP: deferred)
+    WST(9);
     {
         bool nf = false;
 #pragma unroll
@@ -454,6 +502,7 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
     }
     rd *= rcp(1.0 + qn);
     if (!uni_b(rd <= tol)) return 0;
+    WST(10);
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) yo[j] = y[j];
     rp_out = fmax(m, 0.0);
@@ -463,6 +512,7 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
         if (gl == 0) save[POL_K] = (double)k;
     }
     wave_lds_sync();
+    WST(11);
     return 1;
 }
 
@@ -479,28 +529,38 @@ struct WideLds {
 };
 
 // ---- neighbour query on the wave (grid mode) -------------------------------------------------
-// The spatial hash of impc.hpp (GridArgs), queried in three dependent round trips that the caller
-// stages between the setup's loads: wn_begin (lanes 0..8: the 3 x 3 cells' bucket counts),
-// wn_slots (candidate t = lane: its slot entry), wn_states (its state); wn_finish keeps the k
-// nearest (planar distance, ties by agent index: the 16-lane query's order) and leaves them in
-// L.nbx / L.nbi sorted by agent index. More than 64 candidates: further chunks of 64 merged into
-// the running set. A bucket past its capacity: the whole state table is scanned (same result).
+// The spatial hash of impc.hpp (GridArgs) in ONE dependent round trip after the agent's state:
+// lane t < 63 takes slot t % 7 of cell t / 7 of the 3 x 3 cells around the agent and loads, at
+// addresses that depend on the position alone, the cell's bucket count, the slot's row and the
+// row's (px, py, vx, vy) from the table's slot-state plane (GridArgs::sst, GRID_SST = 7 slots) —
+// wn_issue, staged by the caller between the setup's loads; wn_finish keeps the k nearest (planar
+// distance, ties by agent index: the 16-lane query's order) and leaves them in L.nbx / L.nbi sorted
+// by agent index. A bucket with more than 7 rows: its further slots (row, then state) in chunks of
+// 64 merged into the running set; a bucket past its capacity: the whole state table (same result).
 struct WideQuery {
-    uint32_t h, n;   // lane c < 9: cell c's bucket and count
-    int j;           // this lane's first-chunk candidate (raw slot entry, then the agent; -1: none)
+    uint32_t h, n;   // this lane's cell's bucket and count
+    int j;           // this lane's slot row
     double st[4];    // its (px, py, vx, vy)
 };
 
-__device__ __forceinline__ void wn_begin(const ImpcArgs& args, double px, double py, int gl, WideQuery& q) {
+__device__ __forceinline__ void wn_issue(const ImpcArgs& args, double px, double py, int gl, WideQuery& q) {
     const GridArgs& gr = args.grid;
     const long long cx = (long long)floor(px * gr.inv_cell), cy = (long long)floor(py * gr.inv_cell);
-    const int c = gl < 9 ? gl : 0;
+    const int t = gl < 9 * GRID_SST ? gl : 0;
+    const int c = t / GRID_SST, js = t - c * GRID_SST;
     q.h = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
+    const size_t e = (size_t)js * (gr.mask + 1u) + q.h;
     q.n = gr.cnt[q.h];
+    q.j = (int)gr.slots[e];
+    const double4 v = reinterpret_cast<const double4*>(gr.sst)[e];
+    q.st[0] = v.x;
+    q.st[1] = v.y;
+    q.st[2] = v.z;
+    q.st[3] = v.w;
 }
 
-// uniform cell table from the lanes' counts: per cell its bucket, count (0 for a repeated bucket)
-// and first candidate index; total candidates; full = some bucket overflowed
+// the cells as uniform values: bucket, count (0 for a repeated bucket) and first index among the
+// rows past the 7 inline slots; total such rows; full = some bucket past its capacity
 struct WideCells {
     uint32_t hs[9], nc[9], off[9], total;
     bool full;
@@ -511,8 +571,8 @@ __device__ __forceinline__ void wn_cells(const ImpcArgs& args, const WideQuery& 
     bool full = false;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
-        c.hs[k] = (uint32_t)__builtin_amdgcn_readlane((int)q.h, k);
-        uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)q.n, k);
+        c.hs[k] = (uint32_t)__builtin_amdgcn_readlane((int)q.h, k * GRID_SST);
+        uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)q.n, k * GRID_SST);
         full = full || n > (uint32_t)GRID_CAP;
         bool dup = false;
 #pragma unroll
@@ -520,38 +580,24 @@ __device__ __forceinline__ void wn_cells(const ImpcArgs& args, const WideQuery& 
         n = dup ? 0u : n;
         c.nc[k] = n;
         c.off[k] = tot;
-        tot += n;
+        tot += n > (uint32_t)GRID_SST ? n - GRID_SST : 0u;
     }
     c.full = full;
     c.total = full ? (uint32_t)args.num_states : tot;
 }
 
-// candidate t's slot-table entry (0 when none: the loads stay unconditional)
-__device__ __forceinline__ uint32_t wn_entry(const GridArgs& gr, const WideCells& c, uint32_t t) {
+// row index of candidate t among the rows past the inline slots (-1: none)
+__device__ __forceinline__ int wn_more(const GridArgs& gr, const WideCells& c, uint32_t t) {
+    if (t >= c.total) return -1;
+    if (c.full) return (int)t;
     uint32_t e = 0;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
         const uint32_t u = t - c.off[k];
-        e = ((c.off[k] <= t) & (u < c.nc[k])) ? u * (gr.mask + 1u) + c.hs[k] : e;
+        const uint32_t extra = c.nc[k] > (uint32_t)GRID_SST ? c.nc[k] - GRID_SST : 0u;
+        e = ((c.off[k] <= t) & (u < extra)) ? (u + GRID_SST) * (gr.mask + 1u) + c.hs[k] : e;
     }
-    return (t < c.total && !c.full) ? e : 0u;
-}
-
-__device__ __forceinline__ int wn_agent(const WideCells& c, uint32_t t, int raw) {
-    return t >= c.total ? -1 : (c.full ? (int)t : raw);
-}
-
-__device__ __forceinline__ void wn_slots(const ImpcArgs& args, const WideCells& c, int gl, WideQuery& q) {
-    q.j = (int)args.grid.slots[wn_entry(args.grid, c, (uint32_t)gl)];
-}
-
-__device__ __forceinline__ void wn_states(const ImpcArgs& args, const WideCells& c, int gl, WideQuery& q) {
-    q.j = wn_agent(c, (uint32_t)gl, q.j);
-    const size_t r = (size_t)(q.j >= 0 ? q.j : 0) * 6;
-    q.st[0] = args.states[r];
-    q.st[1] = args.states[r + 1];
-    q.st[2] = args.states[r + 3];
-    q.st[3] = args.states[r + 4];
+    return (int)gr.slots[e];
 }
 
 __device__ __forceinline__ bool wn_before(double da, int ja, double db, int jb) {
@@ -559,23 +605,32 @@ __device__ __forceinline__ bool wn_before(double da, int ja, double db, int jb) 
 }
 
 __device__ __forceinline__ int wn_finish(const ImpcArgs& args, int self, double px, double py, const WideCells& c,
-                                      WideQuery& q, WideLds& L, int gl) {
+                                         const WideQuery& q, WideLds& L, int gl) {
     const GridArgs& gr = args.grid;
     const double r2 = gr.radius * gr.radius;
     const int kk = gr.k < NB_MAX ? gr.k : NB_MAX;
     // the running set: lane l < nk holds the l-th nearest so far
     double kd = 1e300, kx0 = 0.0, kx1 = 0.0, kx2 = 0.0, kx3 = 0.0;
     int kj = 0x7fffffff, nk = 0;
-    for (uint32_t t0 = 0; t0 < c.total; t0 += 64) {
-        const uint32_t t = t0 + (uint32_t)gl;
+    // chunk 0: the inline slots (lane t: slot t % 7 of cell t / 7); then the rows past them
+    for (int ch = 0;; ch++) {
+        const uint32_t t0 = ch == 0 ? 0u : (uint32_t)(ch - 1) * 64u;
+        if (ch > 0 && t0 >= c.total) break;
         int j;
         double st[4];
-        if (t0 == 0) {
+        bool valid;
+        if (ch == 0) {
+            const int cc = gl / GRID_SST, js = gl - cc * GRID_SST;
+            uint32_t ncell = 0;
+#pragma unroll
+            for (int k = 0; k < 9; k++) ncell = cc == k ? c.nc[k] : ncell;
+            valid = !c.full && gl < 9 * GRID_SST && (uint32_t)js < ncell;
             j = q.j;
 #pragma unroll
             for (int i = 0; i < 4; i++) st[i] = q.st[i];
         } else {
-            j = wn_agent(c, t, (int)gr.slots[wn_entry(gr, c, t)]);
+            j = wn_more(gr, c, t0 + (uint32_t)gl);
+            valid = j >= 0;
             const size_t r = (size_t)(j >= 0 ? j : 0) * 6;
             st[0] = args.states[r];
             st[1] = args.states[r + 1];
@@ -584,8 +639,8 @@ __device__ __forceinline__ int wn_finish(const ImpcArgs& args, int self, double 
         }
         const double ex = st[0] - px, ey = st[1] - py;
         const double d2 = ex * ex + ey * ey;
-        const bool keep = j >= 0 && j != self && d2 <= r2;
-        unsigned long long msk = __ballot(keep);
+        const bool keep = valid && j != self && d2 <= r2;
+        const unsigned long long msk = __ballot(keep);
         if (msk == 0ull) continue;
         const double dn = keep ? d2 : 1e300;
         const int jn = keep ? j : 0x7fffffff;
@@ -647,52 +702,54 @@ __device__ __forceinline__ int wn_finish(const ImpcArgs& args, int self, double 
     return nk;
 }
 
+// U_k s0 (the state's part of the acceleration at CBF sample k; stage_cbf_rows' us), one component
+// per lane into the per-sample table: the same for both IMPC iterations, formed once at setup
+__device__ __forceinline__ void wide_sample_us(const DevOps& op, const double* __restrict__ buf, const double (&s0)[6],
+                                               WideLds& L, int gl) {
+    for (int t = gl; t < 3 * op.cbf_h; t += 64) {
+        const int k = t / 3, d = t - 3 * k;
+        const double* USk = opp(buf, op.o_US) + (size_t)k * 18 + d * 6;
+        double us[6], v = 0.0;
+#pragma unroll
+        for (int s = 0; s < 6; s++) us[s] = USk[s];
+#pragma unroll
+        for (int s = 0; s < 6; s++) v = fma(us[s], s0[s], v);
+        L.smp[k * 9 + 6 + d] = v;
+    }
+}
+
 // The CBF rows of IMPC iteration `it` (stage_cbf_rows on the wave: one (sample, neighbour) row per
 // lane, filtered and compacted into L.stage in (sample, neighbour) order). Returns the row count
 // (wave-uniform); row_infeasible: a row no acceleration in the box satisfies.
 __device__ int wide_cbf_rows(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args, int it,
                              const double (&s0)[6], const double (&y)[SEP_NZ], bool grid_mode, WideLds& L,
-                             int nb0, int nnb, int gl, bool& row_infeasible) {
+                             int nb0, int nnb, int gl, bool& row_infeasible, long long* wdbg = nullptr) {
+    (void)wdbg;
     constexpr int NZ = SEP_NZ;
+    WST(0);
     const int nk = (it == 0) ? 1 : op.cbf_h;
-    // per-sample table, one entry per lane: the ego state at sample k (iteration 1: the previous
-    // curve at h_samples(k), :161-168; cbf_ego_state) and U_k s0 (stage_cbf_rows' us)
-    for (int t = gl; t < 9 * nk; t += 64) {
-        double v = 0.0;
-        if (t < 6 * nk) {
+    // iteration 1: the ego state at sample k (the previous curve at h_samples(k), :161-168;
+    // cbf_ego_state), one component per lane into the per-sample table (U_k s0 is there since the
+    // setup, wide_sample_us); iteration 0: the state itself, from registers
+    if (it > 0) {
+        for (int t = gl; t < 6 * nk; t += 64) {
             const int k = t / 6, s = t - 6 * k;
-            if (it == 0) {
-                continue;  // (the state itself: written below by lane 0, static indices)
-            } else {
-                const double* PZ = opp(buf, op.o_PZ) + (size_t)k * 6 * NZ + s * NZ;
-                const double* PS = opp(buf, op.o_PS) + (size_t)k * 36 + s * 6;
-                double ps[6], pz[NZ];
+            const double* PZ = opp(buf, op.o_PZ) + (size_t)k * 6 * NZ + s * NZ;
+            const double* PS = opp(buf, op.o_PS) + (size_t)k * 36 + s * 6;
+            double ps[6], pz[NZ], v = 0.0;
 #pragma unroll
-                for (int u = 0; u < 6; u++) ps[u] = PS[u];
+            for (int u = 0; u < 6; u++) ps[u] = PS[u];
 #pragma unroll
-                for (int j = 0; j < NZ; j++) pz[j] = PZ[j];
+            for (int j = 0; j < NZ; j++) pz[j] = PZ[j];
 #pragma unroll
-                for (int u = 0; u < 6; u++) v = fma(ps[u], s0[u], v);
+            for (int u = 0; u < 6; u++) v = fma(ps[u], s0[u], v);
 #pragma unroll
-                for (int j = 0; j < NZ; j++) v = fma(pz[j], y[j], v);
-            }
+            for (int j = 0; j < NZ; j++) v = fma(pz[j], y[j], v);
             L.smp[k * 9 + s] = v;
-        } else {
-            const int u2 = t - 6 * nk, k = u2 / 3, d = u2 - 3 * k;
-            const double* USk = opp(buf, op.o_US) + (size_t)k * 18 + d * 6;
-            double us[6];
-#pragma unroll
-            for (int s = 0; s < 6; s++) us[s] = USk[s];
-#pragma unroll
-            for (int s = 0; s < 6; s++) v = fma(us[s], s0[s], v);
-            L.smp[k * 9 + 6 + d] = v;
         }
     }
-    if (it == 0 && gl == 0) {
-#pragma unroll
-        for (int i = 0; i < 6; i++) L.smp[i] = s0[i];
-    }
     wave_lds_sync();
+    WST(1);
     const double* UZ = opp(buf, op.o_UZ);
     const int ntot = nnb * nk;
     int count = 0;
@@ -721,10 +778,12 @@ __device__ int wide_cbf_rows(const DevOps& op, const double* __restrict__ buf, c
                 npy = ns[1];
                 nvx = ns[3];
                 nvy = ns[4];
+                // (keeps the two reads apart: merged after the branch they became one flat load)
+                asm volatile("" : "+v"(npx), "+v"(npy), "+v"(nvx), "+v"(nvy));
             }
             double e[6];
 #pragma unroll
-            for (int s = 0; s < 6; s++) e[s] = L.smp[k * 9 + s];
+            for (int s = 0; s < 6; s++) e[s] = it == 0 ? s0[s] : L.smp[k * 9 + s];
             double a[3], b;
             safety_cbf(e, npx, npy, nvx, nvy, op.d_min, a, b);
             double bmax = 0.0, bmin = 0.0;
@@ -740,6 +799,7 @@ __device__ int wide_cbf_rows(const DevOps& op, const double* __restrict__ buf, c
             for (int jz = 0; jz < 4; jz++) cg[jz] = -(a[0] * uz[jz] + a[1] * uz[4 + jz] + a[2] * uz[8 + jz]);
             chi = b + (a[0] * L.smp[k * 9 + 6] + a[1] * L.smp[k * 9 + 7] + a[2] * L.smp[k * 9 + 8]);
         }
+        if (base == 0) WST(2);
         const unsigned long long msk = __ballot(keep);
         const int slot = count + __popcll(msk & ((1ull << gl) - 1ull));
         if (keep && slot < W_CBF) {
@@ -752,6 +812,7 @@ __device__ int wide_cbf_rows(const DevOps& op, const double* __restrict__ buf, c
     }
     row_infeasible = __ballot(rinf) != 0ull;
     wave_lds_sync();
+    WST(3);
     return count;
 }
 

@@ -255,33 +255,36 @@ __global__ void __launch_bounds__(256) grid_insert_kernel(const double* __restri
     const int gap = skip1 - skip0;
     if (i >= n - gap) return;
     const int r = i < skip0 ? i : i + gap;
-    grid_insert(g, st[(size_t)r * 6], st[(size_t)r * 6 + 1], (uint32_t)r);
+    const double* s = st + (size_t)r * 6;
+    grid_insert(g, s[0], s[1], s[3], s[4], (uint32_t)r);
 }
 
 }  // namespace dev
 
 static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
-// one table: bucket counts (T) | slots (GRID_CAP x T, slot-major)
+// one table: bucket counts (T) | slots (GRID_CAP x T, slot-major) | slot states (GRID_SST x T x 4)
 size_t grid_table_bytes(int num_states) {
     const uint32_t T = grid_table_size(num_states);
-    return al256((size_t)T * 4) + (size_t)T * GRID_CAP * 4;
+    return al256((size_t)T * 4) + al256((size_t)T * GRID_CAP * 4) + (size_t)T * GRID_SST * 32;
 }
 
-void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots) {
+void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots, double** sst) {
     const uint32_t T = grid_table_size(num_states);
     *cnt = (uint32_t*)base;
     *slots = (uint32_t*)((char*)base + al256((size_t)T * 4));
+    *sst = (double*)((char*)base + al256((size_t)T * 4) + al256((size_t)T * GRID_CAP * 4));
 }
 
 hipError_t launch_grid_insert(const double* states, int n, int skip0, int skip1, double radius,
-                              uint32_t* cnt, uint32_t* slots, hipStream_t s) {
+                              uint32_t* cnt, uint32_t* slots, double* sst, hipStream_t s) {
     const int m = n - (skip1 - skip0);
     if (m <= 0) return hipSuccess;
     GridArgs g;
     memset(&g, 0, sizeof(g));
     g.ins_cnt = cnt;
     g.ins_slots = slots;
+    g.ins_sst = sst;
     g.mask = grid_table_size(n) - 1u;
     g.inv_cell = 1.0 / radius;
     hipLaunchKernelGGL(dev::grid_insert_kernel, dim3((m + 255) / 256), dim3(256), 0, s, states, n, skip0, skip1, g);

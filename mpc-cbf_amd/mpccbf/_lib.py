@@ -88,7 +88,7 @@ class Run(C.Structure):
     _fields_ = [("num_steps", C.c_int32), ("states_alt", C.c_void_p), ("status_log", C.c_void_p),
                 ("iters_log", C.c_void_p), ("step_ms", C.c_void_p), ("solve_ms", C.c_void_p),
                 ("comm", C.c_void_p), ("reserve_steps", C.c_int32), ("solve_stride", C.c_int32),
-                ("final_table", C.c_int32)]
+                ("final_table", C.c_int32), ("kernel_clock", C.c_void_p)]
 
 
 class DenseQP(C.Structure):
@@ -253,10 +253,12 @@ class Context:
                   status=None, obj=None, iters=None, status_log=None, iters_log=None,
                   timing=False, comm=None, reserve_steps=0, solve_stride=1, step_timing=True,
                   stream=None, traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0,
-                  cov=None):
+                  cov=None, kernel_clock=None):
         """Closed-loop control steps on the device (mpccbf_run_steps). Returns a dict with the
         table holding the final states ('final', a tensor) and, with timing=True, per-step
-        device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms)."""
+        device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms). kernel_clock: a
+        (num_steps, 2) uint64-sized device tensor (torch.int64) for every IMPC launch's first-wave
+        start / last-wave end (s_memrealtime, 100 MHz ticks)."""
         if num_agents is None:
             num_agents = states.shape[0] - agent_first
         b = Batch(num_states=states.shape[0], states=_ptr(states), agent_first=agent_first,
@@ -273,7 +275,7 @@ class Context:
                 step_ms=None if step_ms is None else step_ms.ctypes.data,
                 solve_ms=None if solve_ms is None else solve_ms.ctypes.data,
                 comm=None if comm is None else comm.handle, reserve_steps=reserve_steps,
-                solve_stride=solve_stride)
+                solve_stride=solve_stride, kernel_clock=_ptr(kernel_clock))
         _check(load().mpccbf_run_steps(self._h, C.byref(b), C.byref(r), _stream(stream)))
         out = {"final": states if r.final_table == 0 else states_alt}
         if timing:

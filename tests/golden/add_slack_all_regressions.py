@@ -36,5 +36,5 @@ for s, ag in ((100, 87), (143, 52)):
                 "robot (255 slack variables, weights 1000 * 0.9^rank down to ~2e-9). Round 3: GPU "
                 "[OPTIMAL, UNKNOWN], oracle [UNKNOWN, UNKNOWN].",
         "states": st[order].tolist(), "target": targets[ag].tolist()})
-json.dump(js, open(path, "w"))
+json.dump(js, open(path, "w"), indent=1)
 print(len(js["cases"]), "cases")

@@ -53,3 +53,12 @@ def test_rank_share_and_uneven(bench):
         bench.workload_sizes(bench.parse(["--agents-total", "8192", "--rank-share", "8"]), 2, 0)
     with pytest.raises(AssertionError):
         bench.workload_sizes(bench.parse(["--agents-total", "1000"]), 3, 0)
+
+
+@pytest.mark.parametrize("world", [3, 5, 6, 7])
+def test_default_uneven_world_falls_back_to_weak(bench, world):
+    a = bench.parse([])
+    total, per, first = bench.workload_sizes(a, world, 1)
+    assert (total, per, first) == (4096 * world, 4096, 4096) and a.agents_total <= 0
+    a = bench.parse(["--workload", "fov"])
+    assert bench.workload_sizes(a, world, 0)[:2] == (512 * world, 512)

@@ -203,3 +203,15 @@ def test_dense_beyond_device_elimination_capacity(mpclib, oracle):
         q["hi"] = np.concatenate([q["hi"], np.full(extra, rhs)])
         st, xs, _ = mpclib.dense_qp_solve_batch([q])
         assert st[0] == mpclib.INFEASIBLE and xs[0] is None, (n, st[0])
+    # a violated constant row (an inequality along an equality row, its bounds excluding the
+    # equality's value) with a reduced dimension above 8: decided only within capacity, so a
+    # capacity error on both paths (the device reduction's order), not INFEASIBLE on one of them
+    for n in (30, 90):
+        q = _random_qp(rng, n, 10, 5, 0, 0)
+        eqm = q["lo"] == q["hi"]
+        row, rhs = q["A"][eqm][0], q["lo"][eqm][0]
+        q["A"] = np.vstack([q["A"], row[None, :]])
+        q["lo"] = np.concatenate([q["lo"], [rhs + 1.0]])
+        q["hi"] = np.concatenate([q["hi"], [rhs + 2.0]])
+        with pytest.raises(mpclib.MpccbfError, match="capacity|exceeds"):
+            mpclib.dense_qp_solve_batch([q])

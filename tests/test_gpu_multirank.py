@@ -26,7 +26,7 @@ def _torch():
     return torch
 
 
-def _run(mpclib, torch, cfg, states, targets, steps, nranks, cov=None):
+def _run(mpclib, torch, cfg, states, targets, steps, nranks, cov=None, variant=None, names=None):
     dev = torch.device("cuda", 0)
     n = len(states)
     per = n // nranks
@@ -40,6 +40,8 @@ def _run(mpclib, torch, cfg, states, targets, steps, nranks, cov=None):
             stream = torch.cuda.Stream(device=dev)
             with torch.cuda.stream(stream):
                 ctx = mpclib.Context(cfg)
+                if variant is not None:
+                    ctx.set_variant(variant)
                 out = ctx.alloc_outputs(per)
                 a = torch.tensor(states, device=dev)
                 b = torch.empty_like(a)
@@ -53,6 +55,8 @@ def _run(mpclib, torch, cfg, states, targets, steps, nranks, cov=None):
                                     traj_t=traj_t, pos_std=0.001, vel_std=0.01, noise_seed=7,
                                     status_log=slog, iters_log=ilog, comm=comms[r], stream=stream, cov=cv)
                 stream.synchronize()
+                if names is not None:
+                    names.append(ctx.kernel_name)
                 results[r] = (res["final"].cpu().numpy(), slog.cpu().numpy(), out["x"].cpu().numpy(),
                               ilog.cpu().numpy())
         except Exception as e:  # surfaced in the main thread
@@ -70,16 +74,22 @@ def _run(mpclib, torch, cfg, states, targets, steps, nranks, cov=None):
     return results
 
 
-@pytest.mark.parametrize("nranks,n_agents", [(2, 1024), (4, 1024), (8, 8192)])
-def test_local_group_matches_single_rank(mpclib, nranks, n_agents):
-    """(8, 8192) is BASELINE config 4's shape: 8 ranks x 1024 agents of an 8192-agent table."""
+@pytest.mark.parametrize("nranks,n_agents,variant", [(2, 1024, 4), (4, 1024, 0), (8, 8192, 0), (8, 8192, 4)])
+def test_local_group_matches_single_rank(mpclib, nranks, n_agents, variant):
+    """(8, 8192) is BASELINE config 4's shape: 8 ranks x 1024 agents of an 8192-agent table.
+    variant 0 (share-adaptive): every rank's 1024 agents take the one-agent-per-wave kernel, so
+    the single-rank loop is run with that kernel forced (variant 5) and the two must agree bit for
+    bit; variant 4: the 16-lane kernel on both sides."""
     torch = _torch()
     cfg = swarm.config(15)
     states, targets = swarm.lattice_swarm(n_agents, seed=13)
     states[:, :2] *= 0.6  # crowded: CBF rows, infeasible QPs, fallback trajectories
     steps = 12
-    single = _run(mpclib, torch, cfg, states, targets, steps, 1)[0]
-    multi = _run(mpclib, torch, cfg, states, targets, steps, nranks)
+    names = []
+    single = _run(mpclib, torch, cfg, states, targets, steps, 1, variant=5 if variant == 0 else variant)[0]
+    multi = _run(mpclib, torch, cfg, states, targets, steps, nranks, variant=variant, names=names)
+    assert all(nm == ("impc_wide_kernel<256>" if variant == 0 else "impc_sep_kernel<1,1,false,256>")
+               for nm in names), names
     per = n_agents // nranks
     for r, (final, slog, x, _) in enumerate(multi):
         # every rank ends with the whole gathered table, equal to the single-rank loop

@@ -200,6 +200,33 @@ def test_separable_and_dense_layouts_agree(mpclib):
     assert np.nanmax(np.abs(res[0]["x"] - res[3]["x"])) <= 1e-6
 
 
+def test_nb_out_written_by_every_collision_kernel(mpclib):
+    """mpccbf_batch.nb_out (the neighbour list each agent's QPs were built from) from the generic
+    dense-layout kernel (variant 3) equals the separable kernels' (variants 4 and 5) on the same
+    grid query: every entry written (no sentinel left), same sets."""
+    torch = _torch()
+    dev = torch.device("cuda", 0)
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(512, seed=5)
+    states[:, :2] *= 0.6
+    st = torch.tensor(states, device=dev)
+    tg = torch.tensor(targets, device=dev)
+    res = {}
+    for variant in (3, 4, 5):
+        ctx = mpclib.Context(cfg)
+        ctx.set_variant(variant)
+        out = ctx.alloc_outputs(len(states))
+        nbo = torch.full((len(states), 16), -5, dtype=torch.int32, device=dev)
+        ctx.impc_solve(st, targets=tg, knn_k=8, knn_radius=6.0, nb_out=nbo, **out)
+        torch.cuda.synchronize()
+        res[variant] = nbo.cpu().numpy()
+        assert not np.any(res[variant] == -5), variant
+    ref = [sorted(v for v in row if v >= 0) for row in res[4]]
+    assert sum(len(r) for r in ref) > 3 * len(states)
+    for variant in (3, 5):
+        assert [sorted(v for v in row if v >= 0) for row in res[variant]] == ref, variant
+
+
 def _manual_loop(ctx, st0, tg, steps, first, count, torch):
     a = st0.clone()
     b = st0.clone()

@@ -153,3 +153,41 @@ def test_gauss_seidel_trace_matches_oracle(mpclib, neighbours):
     sj = sim.Simulator(cfg, states, targets, neighbours=neighbours, knn_k=8, knn_radius=6.0, record=False, **kw)
     sj.run(steps * cfg["h"])
     assert np.max(np.abs(sj.states.cpu().numpy() - gpu[-1])) > 1e-6
+
+
+def test_next_state_same_with_and_without_substeps(mpclib):
+    """A fresh curve's next state is the AZ / AS product (the curve at min(h, T_end)) whether or not
+    the sub-step records are requested, so one closed loop is bit-reproducible across output
+    options; the last sub-step record is that next state, and without noise it is the kept curve at
+    h (oracle Bernstein evaluation of the device's control points) within 1e-9."""
+    torch = _torch()
+    dev = torch.device("cuda", 0)
+    cfg = swarm.config(15)
+    n = 256
+    states, targets = swarm.lattice_swarm(n, seed=6)
+    ctx = mpclib.Context(cfg)
+    st = torch.tensor(states, device=dev)
+    tg = torch.tensor(targets, device=dev)
+    nsub = int(round(cfg["h"] / cfg["Ts"]))
+    res = {}
+    for noise in (0.0, 1.0):
+        for with_sub in (False, True):
+            out = ctx.alloc_outputs(n)
+            traj_t = torch.full((n,), -1.0, dtype=torch.float64, device=dev)
+            sub = torch.zeros((n, nsub, 6), dtype=torch.float64, device=dev) if with_sub else None
+            ctx.impc_solve(st, targets=tg, knn_k=8, knn_radius=6.0, traj_t=traj_t, substeps=sub,
+                           pos_std=1e-3 * noise, vel_std=1e-2 * noise, noise_seed=9, **out)
+            torch.cuda.synchronize()
+            res[(noise, with_sub)] = (out["next_states"].cpu().numpy(), out["x"].cpu().numpy(),
+                                      out["status"].cpu().numpy(), None if sub is None else sub.cpu().numpy())
+        a, b = res[(noise, False)], res[(noise, True)]
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(b[3][:, -1, :], b[0])
+    nxt, x, status, _ = res[(0.0, False)]
+    p = O.make_params(cfg)
+    fresh = np.any(status == O.OPTIMAL, axis=1)
+    assert fresh.sum() > n // 2
+    t = min(cfg["h"], cfg["num_pieces"] * cfg["piece_max_parameter"])
+    for i in np.nonzero(fresh)[0]:
+        exp = np.concatenate([O.eval_curve(p, x[i], t, 0), O.eval_curve(p, x[i], t, 1)])
+        assert np.max(np.abs(nxt[i] - exp)) < 1e-9, (i, nxt[i] - exp)

@@ -127,6 +127,16 @@ for v in VARIANTS:
     print(f"   solve0 per Newton iteration: mean {per.mean():.2f} p50 {np.median(per):.2f} us "
           f"(iters mean {its[ok0, 0].mean():.1f})")
     crit = int(np.argmax(end))
+    if os.environ.get("CP_JSON"):  # bench.py's roofline.critical_path reads these entries
+        import json
+        path = os.environ["CP_JSON"]
+        d = json.load(open(path)) if os.path.exists(path) else {"entries": []}
+        d["entries"].append({"kernel": ctx.kernel_name, "workload": "fov" if FOV else "collision", "agents": N,
+                             "variant": v, "span_us": float(end.max()), "agent_wall_max_us": float(np.max(end - start)),
+                             "agent_wall_mean_us": float(np.mean(end - start)),
+                             "phases_mean_us": {nm: float(np.mean(s[:, k + 1] - s[:, k])) for k, nm in enumerate(PH)},
+                             "critical_agent_phases_us": [float(x) for x in np.diff(s[crit])]})
+        json.dump(d, open(path, "w"), indent=1)
     print(f"   critical agent {crit}: status {status[crit]}, start {start[crit]:.1f}, "
           f"phases {np.round(np.diff(s[crit]), 2)}")
     print(f"   critical agent iters {its[crit]}")

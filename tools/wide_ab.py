@@ -21,15 +21,19 @@ def main():
     ap.add_argument("--crowded", action="store_true")
     ap.add_argument("--time", action="store_true")
     ap.add_argument("--knn", type=int, default=8)
+    ap.add_argument("--scale", type=float, default=0.0, help="lattice spacing scale (default 1, --crowded 0.6)")
+    ap.add_argument("--variants", default="5,4", help="A,B: the variant under test and the reference")
     args = ap.parse_args()
     import torch
     from mpccbf import swarm, Context
 
     dev = torch.device("cuda", 0)
     cfg = swarm.config(15)
-    states_h, targets_h = swarm.lattice_swarm(args.agents, spacing_scale=0.6 if args.crowded else 1.0)
+    scale = args.scale if args.scale > 0 else (0.6 if args.crowded else 1.0)
+    states_h, targets_h = swarm.lattice_swarm(args.agents, spacing_scale=scale)
     targets = torch.tensor(targets_h, device=dev)
-    ctx = {v: Context(cfg) for v in (0, 4)}
+    va, vb = (int(v) for v in args.variants.split(","))
+    ctx = {va: Context(cfg), vb: Context(cfg)}
     for v, c in ctx.items():
         c.set_variant(v)
     print("kernels:", {v: c.kernel_name for v, c in ctx.items()}, flush=True)
@@ -37,13 +41,13 @@ def main():
     # evolve the swarm with variant 4, keeping some tables
     tables = []
     st = torch.tensor(states_h, device=dev)
-    out = ctx[4].alloc_outputs(args.agents)
+    out = ctx[vb].alloc_outputs(args.agents)
     keep_at = set([0, 1, 2, 3, 5, 8, 12, 20, 30, 45] + list(range(60, args.steps + 1, 30)))
     for s in range(args.steps + 1):
         if s in keep_at:
             tables.append((s, st.clone()))
         nxt = torch.empty_like(st)
-        ctx[4].impc_solve(st, targets=targets, knn_k=args.knn, knn_radius=radius, next_states=nxt,
+        ctx[vb].impc_solve(st, targets=targets, knn_k=args.knn, knn_radius=radius, next_states=nxt,
                           x=out["x"], status=out["status"], obj=out["obj"], iters=out["iters"], step_index=s,
                           pos_std=0.001, vel_std=0.01, noise_seed=20251015)
         st = nxt
@@ -59,7 +63,7 @@ def main():
             torch.cuda.synchronize()
             res[v] = {k: t.cpu().numpy() for k, t in o.items()}
             res[v]["nb"] = nbo.cpu().numpy()
-        a, b = res[0], res[4]
+        a, b = res[va], res[vb]
         mism = int(np.sum(a["status"] != b["status"]))
         tot_mismatch += mism
         nbm = int(np.sum(np.any(a["nb"] != b["nb"], axis=1)))
