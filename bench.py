@@ -309,7 +309,8 @@ def main():
             dist.broadcast(uid, 0)
             comm = Comm(bytes(uid.cpu().tolist()), world, rank, local)
 
-        kclock = torch.zeros((nsteps, 2), dtype=torch.int64, device=dev)
+        kc_waves = ctx.launch_waves(per)
+        kclock = torch.zeros((nsteps, max(kc_waves, 1), 2), dtype=torch.int64, device=dev) if kc_waves else None
 
         def closed_loop(log, timing):
             """warm-up + nsteps control steps from the initial swarm; returns (seconds, run dict).
@@ -344,8 +345,12 @@ def main():
         region_ms = e0.elapsed_time(e1)
         # each IMPC launch's own duration in the timed pass: the kernel's first-wave start to its
         # last-wave end on the device clock (s_memrealtime, 100 MHz; mpccbf_run::kernel_clock)
-        kc = kclock.cpu().numpy().view(np.uint64)
-        launch_us = ((kc[:, 1] - ~kc[:, 0]).astype(np.float64)) * 1e-2
+        # (collision kernels only: the FoV kernels carry no clock, their kernel time is the events')
+        launch_us = None
+        if kclock is not None:
+            from mpccbf._lib import kernel_clock_us
+            launch_us = kernel_clock_us(kclock.cpu().numpy())
+            launch_us = launch_us if np.all(np.isfinite(launch_us)) else None
         # replay of the identical steps (same initial swarm, counter-based noise keyed by the step
         # index) with HIP events on the launch stream: per-step device time (p99) and the IMPC
         # kernel's duration on every step (roofline), without perturbing the throughput pass

@@ -260,12 +260,15 @@ typedef struct mpccbf_run {
     int32_t solve_stride;   /* time the IMPC kernel on every solve_stride-th step only (<= 1: all);
                                solve_ms of untimed steps is set to -1 */
     int32_t final_table;    /* out: 0 = batch->states holds the final states, 1 = states_alt */
-    /* ABI 11: device clock of every step's IMPC launch, or NULL: 2 x num_steps uint64 (device,
-     * zero-filled by the call): per step the bitwise complement of the s_memrealtime counter
-     * (100 MHz) when the launch's first wave started, and the counter when its last wave finished
-     * — the kernel's own duration (end - ~start), without the dispatch gaps that events around it
-     * include */
+    /* ABI 11: device clock of every step's IMPC launch, or NULL: num_steps x kernel_clock_waves x 2
+     * uint64 (device, zero-filled by the call). Wave w of step s's launch writes the pair [s][w] =
+     * (the s_memrealtime counter, 100 MHz, when the wave started, when it finished) with plain
+     * stores; waves without an agent write nothing. The launch's own duration is the largest end
+     * minus the smallest start over the nonzero pairs, without the dispatch gaps that events around
+     * it include. kernel_clock_waves >= mpccbf_impc_launch_waves(ctx, num_agents); the collision
+     * kernels only (the FoV kernels write nothing). */
     uint64_t* kernel_clock;
+    int32_t kernel_clock_waves;
 } mpccbf_run;
 
 int mpccbf_run_steps(mpccbf_ctx* ctx, const mpccbf_batch* batch, mpccbf_run* run, void* hip_stream);
@@ -278,6 +281,11 @@ int mpccbf_run_steps(mpccbf_ctx* ctx, const mpccbf_batch* batch, mpccbf_run* run
 int mpccbf_set_variant(mpccbf_ctx* ctx, int variant);
 /* Name of the IMPC kernel instantiation the current variant launches (diagnostics). */
 const char* mpccbf_kernel_name(const mpccbf_ctx* ctx);
+
+/* ABI 11: waves of the IMPC launch mpccbf_impc_solve / mpccbf_run_steps makes for num_agents
+ * agents with the context's variant that write mpccbf_run::kernel_clock (0: that kernel has no
+ * clock). */
+int32_t mpccbf_impc_launch_waves(const mpccbf_ctx* ctx, int32_t num_agents);
 
 /* Neighbour lists on the device: for each agent of [agent_first, agent_first+num_agents) the
  * (at most) k nearest other agents of `states` (planar distance) within `radius`, sorted by

@@ -26,6 +26,7 @@ namespace mpccbf {
 hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, int variant,
                        hipStream_t s);
 const char* impc_kernel_name(const DevOps& op, int variant, int n);
+int impc_clock_waves(const DevOps& op, int variant, int n);
 void impc_set_device_simds(int simds);
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
 hipError_t launch_fov_rows_eval(int count, const double* ego, const double* nb, double fov, double Ds, double Rs,
@@ -221,6 +222,7 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
         ImpcArgs f = a;
         f.defer = nullptr;
         f.defer_clear = nullptr;
+        f.kclock = nullptr;  // (the clock is the main launch's)
         f.queue = q_this;
         e = launch_impc_fallback(c->dev, c->dbuf, f, impc_rows_may_exceed(c->dev, !grid, b->knn_k), stream);
         // (a queue the fallback never read is zeroed by the main launch after next)
@@ -515,6 +517,10 @@ int mpccbf_impc_solve(mpccbf_ctx* c, const mpccbf_batch* b, void* stream) {
     return impc_enqueue(c, b, (hipStream_t)stream, nullptr, nullptr);
 }
 
+int32_t mpccbf_impc_launch_waves(const mpccbf_ctx* c, int32_t num_agents) {
+    return c ? impc_clock_waves(c->dev, c->variant, num_agents) : 0;
+}
+
 const char* mpccbf_kernel_name(const mpccbf_ctx* c) {
     if (!c) return "";
     if (c->dev.cbf_mode == 1) return c->dev.slack_mode ? "impc_fov_kernel<true>" : "impc_fov_kernel<false>";
@@ -708,8 +714,13 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
     hipStream_t stream = (hipStream_t)stream_;
     HIP_TRY(hipSetDevice(c->device));
     const bool timing = r->step_ms || r->solve_ms;
-    if (r->kernel_clock && r->num_steps > 0)  // (the start is kept complemented: zero for both)
-        HIP_TRY(hipMemsetAsync(r->kernel_clock, 0, 2 * sizeof(uint64_t) * (size_t)r->num_steps, stream));
+    const int kcw = impc_clock_waves(c->dev, c->variant, count);  // (pairs per step)
+    if (r->kernel_clock && r->kernel_clock_waves < kcw)
+        return fail(MPCCBF_ERR_INVALID_ARGUMENT, "run: kernel_clock_waves < mpccbf_impc_launch_waves (" +
+                                                     std::to_string(kcw) + ")");
+    if (r->kernel_clock && r->num_steps > 0)
+        HIP_TRY(hipMemsetAsync(r->kernel_clock, 0,
+                               2 * sizeof(uint64_t) * (size_t)r->kernel_clock_waves * (size_t)r->num_steps, stream));
     const int need = 3 * std::max(r->num_steps, r->reserve_steps) + 1;
     while ((int)c->events.size() < need) {
         hipEvent_t e;
@@ -755,7 +766,9 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
         const bool tk = r->solve_ms && (r->solve_stride <= 1 || s % r->solve_stride == 0);
         const int rc = impc_enqueue(c, &sb, stream, tk ? ev[3 * s + 1] : nullptr, tk ? ev[3 * s + 2] : nullptr,
                                     gtab ? s : -1,
-                                    r->kernel_clock ? (unsigned long long*)r->kernel_clock + 2 * (size_t)s : nullptr);
+                                    r->kernel_clock ? (unsigned long long*)r->kernel_clock +
+                                                          2 * (size_t)r->kernel_clock_waves * s
+                                                    : nullptr);
         if (rc != MPCCBF_OK) return rc;
         if (r->comm && r->comm->nranks > 1 && r->comm->local) {
             // in-process group: every rank's block of this step copied into this rank's table

@@ -21,9 +21,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -71,15 +75,20 @@ struct DenseBatch {
     double feas_tol;
     // count flags: 1 = reduced on the host (beyond the device elimination's 64 variables / 64
     // equalities; host/dense_qp.cpp), its reduced QP, status, m and pd uploaded, x expanded on the host
-    const int32_t* hostred;
+    const int32_t* hostred;  // (NULL: none)
+    int32_t lds_rows, lds_stride;  // the reduce kernel's E^T image (reduce_stride)
 };
 
 namespace dev {
 
-constexpr int LDS_S = DENSE_EMAX + 1;  // row stride of the E^T image (odd: spread banks)
+// E^T / H image in dynamic LDS, sized per batch: rows = the batch's largest n, row stride S = the
+// larger of its largest n and equality count, made odd (spread banks); at most 64 x 65 doubles
+__host__ __device__ inline int reduce_stride(int nmax, int emax) {
+    const int s = nmax > emax ? nmax : emax;
+    return s | 1;
+}
 
 struct ReduceLds {
-    double et[DENSE_NMAX * LDS_S];   // E^T: row i = variable, column c = equality (lane c)
     double z[DENSE_NMAX * DENSE_NZ]; // Z row-major
     double xp[DENSE_NMAX];
     double hz[DENSE_NMAX * DENSE_NZ];
@@ -95,8 +104,10 @@ __device__ __forceinline__ bool fin_bound(double v) { return isfinite(v) && fabs
 __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int l = threadIdx.x;
-    if (qi >= a.count || a.hostred[qi]) return;  // (reduced on the host)
+    if (qi >= a.count || (a.hostred && a.hostred[qi])) return;  // (reduced on the host)
     __shared__ ReduceLds s;
+    extern __shared__ double et[];  // E^T: row i = variable, column c = equality (lane c)
+    const int LDS_S = a.lds_stride, NROWS = a.lds_rows;
     const int32_t* ib = a.ints + a.off_i[qi];
     const double* db = a.dbl + a.off_d[qi];
     const int n = ib[0], me = ib[1], mi = ib[2], nh = ib[3];
@@ -118,10 +129,10 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     bool infeasible = false, eq_infeasible = false;
 
     // ---- E^T into LDS (lane c: equality c's row as column c), zero elsewhere
-    for (int e = l; e < DENSE_NMAX * LDS_S; e += 64) s.et[e] = 0.0;
+    for (int e = l; e < NROWS * LDS_S; e += 64) et[e] = 0.0;
     __syncthreads();
     if (l < me) {
-        for (int k = eptr[l]; k < eptr[l + 1]; k++) s.et[ecol[k] * LDS_S + l] = eval[k];
+        for (int k = eptr[l]; k < eptr[l + 1]; k++) et[ecol[k] * LDS_S + l] = eval[k];
         s.perm[l] = l;
     }
     __syncthreads();
@@ -134,7 +145,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         double nrm = -1.0;
         if (l >= t && l < me) {
             nrm = 0.0;
-            for (int i = t; i < n; i++) nrm = fma(s.et[i * LDS_S + l], s.et[i * LDS_S + l], nrm);
+            for (int i = t; i < n; i++) nrm = fma(et[i * LDS_S + l], et[i * LDS_S + l], nrm);
         }
         const double best = grp_max<64>(nrm);
         const int p = __ffsll((long long)__ballot(nrm == best && l >= t && l < me)) - 1;
@@ -143,9 +154,9 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         if (!(sig > 1e-12 * r00) || p < 0) break;  // the remaining columns are dependent
         // swap columns t and p (lane i: row i)
         if (p != t && l < n) {
-            const double v = s.et[l * LDS_S + t];
-            s.et[l * LDS_S + t] = s.et[l * LDS_S + p];
-            s.et[l * LDS_S + p] = v;
+            const double v = et[l * LDS_S + t];
+            et[l * LDS_S + t] = et[l * LDS_S + p];
+            et[l * LDS_S + p] = v;
         }
         if (p != t && l == 0) {
             const int q = s.perm[t];
@@ -153,14 +164,14 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
             s.perm[p] = q;
         }
         __syncthreads();
-        const double xt = s.et[t * LDS_S + t];
+        const double xt = et[t * LDS_S + t];
         const double alpha = xt >= 0.0 ? -sig : sig;
         const double vt = xt - alpha;
         const double vn2 = best - xt * xt + vt * vt;  // |v|^2
         const double bt = vn2 > 0.0 ? 2.0 / vn2 : 0.0;
         __syncthreads();
         if (l == 0) {
-            s.et[t * LDS_S + t] = vt;  // v = (vt, x_{t+1}, ...)
+            et[t * LDS_S + t] = vt;  // v = (vt, x_{t+1}, ...)
             s.rdiag[t] = alpha;
             s.beta[t] = bt;
         }
@@ -168,9 +179,9 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         // apply to columns t+1 .. me-1 (lane c)
         if (l > t && l < me) {
             double w = 0.0;
-            for (int i = t; i < n; i++) w = fma(s.et[i * LDS_S + t], s.et[i * LDS_S + l], w);
+            for (int i = t; i < n; i++) w = fma(et[i * LDS_S + t], et[i * LDS_S + l], w);
             w *= bt;
-            for (int i = t; i < n; i++) s.et[i * LDS_S + l] = fma(-w, s.et[i * LDS_S + t], s.et[i * LDS_S + l]);
+            for (int i = t; i < n; i++) et[i * LDS_S + l] = fma(-w, et[i * LDS_S + t], et[i * LDS_S + l]);
         }
         __syncthreads();
         rank = t + 1;
@@ -180,7 +191,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     if (l < me) s.bp[l] = erhs[s.perm[l]];
     __syncthreads();
     for (int t = 0; t < rank; t++) {
-        const double part = (l < t) ? s.et[l * LDS_S + t] * s.u[l] : 0.0;  // R[l][t] u_l, l < t
+        const double part = (l < t) ? et[l * LDS_S + t] * s.u[l] : 0.0;  // R[l][t] u_l, l < t
         const double sum = grp_sum<64>(part);
         if (l == 0) s.u[t] = (s.bp[t] - sum) / s.rdiag[t];
         __syncthreads();
@@ -191,7 +202,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
 #pragma unroll
     for (int j = 0; j < DENSE_NZ; j++) zc[j] = (l == rank + j && j < nz) ? 1.0 : 0.0;
     for (int t = rank - 1; t >= 0; t--) {
-        const double vi = (l >= t && l < n) ? s.et[l * LDS_S + t] : 0.0;
+        const double vi = (l >= t && l < n) ? et[l * LDS_S + t] : 0.0;
         const double bt = s.beta[t];
         double d = grp_sum<64>(vi * w);
         w = fma(-bt * d, vi, w);
@@ -221,12 +232,12 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     // row l over j = 0 .. n-1 — a fixed summation order (no dependence on how the hardware orders
     // LDS atomics), and no lane walks the whole nonzero list (that serial scan of global loads and
     // divisions cost ~1.7 ms per 4096-QP call)
-    for (int e = l; e < n * LDS_S; e += 64) s.et[e] = 0.0;
+    for (int e = l; e < n * LDS_S; e += 64) et[e] = 0.0;
     __syncthreads();
     for (int e = l; e < nh; e += 64) {
         const int k = hidx[e];
         const int i = k / n, j = k - i * n;
-        s.et[i * LDS_S + j] = hval[e];
+        et[i * LDS_S + j] = hval[e];
     }
     __syncthreads();
     if (l < n) {
@@ -234,7 +245,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
 #pragma unroll
         for (int b = 0; b < DENSE_NZ; b++) hzl[b] = 0.0;
         for (int j = 0; j < n; j++) {
-            const double hv = 0.5 * (s.et[l * LDS_S + j] + s.et[j * LDS_S + l]);
+            const double hv = 0.5 * (et[l * LDS_S + j] + et[j * LDS_S + l]);
             hxl = fma(hv, s.xp[j], hxl);
 #pragma unroll
             for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[j * DENSE_NZ + b], hzl[b]);
@@ -415,7 +426,7 @@ __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
 __global__ void __launch_bounds__(64) dense_expand_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int l = threadIdx.x;
-    if (qi >= a.count || a.status[qi] != ST_OPTIMAL || a.hostred[qi]) return;  // (host-reduced: host expands)
+    if (qi >= a.count || a.status[qi] != ST_OPTIMAL || (a.hostred && a.hostred[qi])) return;  // (host-reduced: host expands)
     __shared__ double xs[DENSE_NMAX];
     const int32_t* ib = a.ints + a.off_i[qi];
     const double* db = a.dbl + a.off_d[qi];
@@ -472,6 +483,7 @@ struct HostBuf {  // pinned staging of the packed QPs
 };
 thread_local DevBuf g_dense_buf;
 thread_local HostBuf g_dense_host;
+thread_local HostBuf g_dense_out;  // pinned x | obj | status of the last call
 
 size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
 
@@ -498,23 +510,30 @@ PackPlan plan_qp(const mpccbf_dense_qp& qp) {
     if (qp.m > 0 && !(qp.A && qp.lo && qp.hi)) return fail("dense QP: A, lo, hi are required when m > 0");
     const int n = qp.n, m = qp.m;
     pl.n = n;
+    // branch-free scans (vectorised): a flag for a non-finite entry, the nonzero counts
+    bool nonfin = false;
+    int nh = 0;
     for (size_t k = 0; k < (size_t)n * n; k++) {
         const double v = qp.H[k];
-        if (!std::isfinite(v)) return fail("dense QP: H has a non-finite entry");
-        pl.nh += v != 0.0;
+        nh += v != 0.0;
+        nonfin |= !(std::fabs(v) <= DBL_MAX);
     }
-    for (int i = 0; i < n; i++)
-        if (!std::isfinite(qp.c[i])) return fail("dense QP: c has a non-finite entry");
+    if (nonfin) return fail("dense QP: H has a non-finite entry");
+    pl.nh = nh;
+    for (int i = 0; i < n; i++) nonfin |= !(std::fabs(qp.c[i]) <= DBL_MAX);
+    if (nonfin) return fail("dense QP: c has a non-finite entry");
     for (int k = 0; k < m; k++) {
         const double lo = qp.lo[k], hi = qp.hi[k];
         if (std::isnan(lo) || std::isnan(hi)) return fail("dense QP: NaN row bound");
+        const bool eq = finite_bound(lo) && lo == hi, in = !eq && (finite_bound(lo) || finite_bound(hi));
+        if (!eq && !in) continue;  // a free row: not read
         const double* a = qp.A + (size_t)k * n;
         int nnz = 0;
         for (int j = 0; j < n; j++) nnz += a[j] != 0.0;
-        if (finite_bound(lo) && lo == hi) {
+        if (eq) {
             pl.me++;
             pl.enz += nnz;
-        } else if (finite_bound(lo) || finite_bound(hi)) {
+        } else {
             pl.mi++;
             pl.inz += nnz;
         }
@@ -536,12 +555,12 @@ PackPlan plan_qp(const mpccbf_dense_qp& qp) {
     return pl;
 }
 
+// Writes one QP's packed form. Branch-free compaction (each entry written, the cursor advanced by
+// its nonzero flag): a section's cursor may write one entry past its end, so the equality rows are
+// packed before the first inequality entry and each section's leading words after the section
+// before it, and the caller leaves one spare double and int after the QP.
 void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, int32_t* ib) {
     const int n = qp.n;
-    ib[0] = n;
-    ib[1] = pl.me;
-    ib[2] = pl.mi;
-    ib[3] = pl.nh;
     int32_t* hidx = ib + 4;
     int32_t* eptr = hidx + pl.nh;
     int32_t* ecol = eptr + pl.me + 1;
@@ -554,73 +573,142 @@ void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, int32_t*
     double* ilo = evalv + pl.enz;
     double* ihi = ilo + pl.mi;
     double* ivalv = ihi + pl.mi;
+    int h = 0;
+    for (int k = 0; k < n * n; k++) {
+        const double v = qp.H[k];
+        hidx[h] = k;
+        hval[h] = v;
+        h += v != 0.0;
+    }
+    ib[0] = n;
+    ib[1] = pl.me;
+    ib[2] = pl.mi;
+    ib[3] = pl.nh;
     std::memcpy(c, qp.c, (size_t)n * sizeof(double));
     db[n] = qp.c0;
-    int h = 0;
-    for (int k = 0; k < n * n; k++)
-        if (qp.H[k] != 0.0) {
-            hidx[h] = k;
-            hval[h++] = qp.H[k];
+    auto row = [&](const double* a, int32_t* col, double* val, int z) {
+        for (int j = 0; j < n; j++) {
+            const double v = a[j];
+            col[z] = j;
+            val[z] = v;
+            z += v != 0.0;
         }
-    int e = 0, ez = 0, r = 0, rz = 0;
-    eptr[0] = iptr[0] = 0;
-    auto add = [&](bool eq, const double* a, int unit, double lo, double hi) {
-        int32_t* col = eq ? ecol : icol;
-        double* val = eq ? evalv : ivalv;
-        int& z = eq ? ez : rz;
-        if (a) {
-            for (int j = 0; j < n; j++)
-                if (a[j] != 0.0) {
-                    col[z] = j;
-                    val[z++] = a[j];
-                }
-        } else {
-            col[z] = unit;
-            val[z++] = 1.0;
-        }
-        if (eq) {
-            erhs[e] = lo;
-            eptr[++e] = ez;
-        } else {
-            ilo[r] = lo;
-            ihi[r] = hi;
-            iptr[++r] = rz;
-        }
+        return z;
     };
+    // equality rows (rows with lo == hi, then fixed variables)
+    eptr[0] = 0;
+    int e = 0, ez = 0;
     for (int k = 0; k < qp.m; k++) {
         const double lo = qp.lo[k], hi = qp.hi[k];
-        const double* a = qp.A + (size_t)k * n;
-        if (finite_bound(lo) && lo == hi) add(true, a, 0, lo, hi);
-        else if (finite_bound(lo) || finite_bound(hi)) add(false, a, 0, lo, hi);
+        if (!(finite_bound(lo) && lo == hi)) continue;
+        ez = row(qp.A + (size_t)k * n, ecol, evalv, ez);
+        erhs[e] = lo;
+        eptr[++e] = ez;
     }
     for (int i = 0; i < n; i++) {
         const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
-        if (finite_bound(lo) && lo == hi) add(true, nullptr, i, lo, hi);
-        else if (finite_bound(lo) || finite_bound(hi)) add(false, nullptr, i, lo, hi);
+        if (!(finite_bound(lo) && lo == hi)) continue;
+        ecol[ez] = i;
+        evalv[ez++] = 1.0;
+        erhs[e] = lo;
+        eptr[++e] = ez;
+    }
+    // inequality rows (a finite side, then variable bounds as unit rows)
+    iptr[0] = 0;
+    int r = 0, rz = 0;
+    for (int k = 0; k < qp.m; k++) {
+        const double lo = qp.lo[k], hi = qp.hi[k];
+        if ((finite_bound(lo) && lo == hi) || !(finite_bound(lo) || finite_bound(hi))) continue;
+        rz = row(qp.A + (size_t)k * n, icol, ivalv, rz);
+        ilo[r] = lo;
+        ihi[r] = hi;
+        iptr[++r] = rz;
+    }
+    for (int i = 0; i < n; i++) {
+        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
+        if ((finite_bound(lo) && lo == hi) || !(finite_bound(lo) || finite_bound(hi))) continue;
+        icol[rz] = i;
+        ivalv[rz++] = 1.0;
+        ilo[r] = lo;
+        ihi[r] = hi;
+        iptr[++r] = rz;
     }
 }
 
-// reduced row count of host-reduced QP k (its index in `big`)
-int hred_rows(const std::vector<ReducedQP>& hred, const std::vector<int>& big, int k) {
-    for (size_t b = 0; b < big.size(); b++)
-        if (big[b] == k) return hred[b].m;
-    return 0;
-}
+// Host worker pool for the per-QP validation and packing: created on first use (up to 15 workers
+// beside the calling thread), kept for the process (a thread spawn per call cost more than the
+// packing of a small batch). One batch at a time uses it (a second concurrent caller packs on its
+// own thread).
+class PackPool {
+  public:
+    static PackPool& get() {
+        static PackPool* p = new PackPool();  // never destroyed: workers block on the condition at exit
+        return *p;
+    }
+    int width() const { return (int)workers_.size() + 1; }
+    // f(k0, k1) over [0, count) in width() chunks; the caller runs chunk 0
+    void run(int count, const std::function<void(int, int)>& f) {
+        std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
+        const int w = width();
+        if (!busy.owns_lock() || w == 1 || count < 64) {
+            f(0, count);
+            return;
+        }
+        const int chunk = (count + w - 1) / w;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &f;
+            count_ = count;
+            chunk_ = chunk;
+            pending_ = (int)workers_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        f(0, std::min(count, chunk));
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    PackPool() {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const int nw = (int)std::min(15u, hw - 1);
+        for (int t = 0; t < nw; t++) {
+            workers_.emplace_back([this, t] { loop(t + 1); });
+            workers_.back().detach();
+        }
+    }
+    void loop(int idx) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int, int)>* f;
+            int k0, k1;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                f = job_;
+                k0 = std::min(count_, idx * chunk_);
+                k1 = std::min(count_, k0 + chunk_);
+            }
+            if (k0 < k1) (*f)(k0, k1);
+            std::lock_guard<std::mutex> lk(m_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex busy_, m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int, int)>* job_ = nullptr;
+    int count_ = 0, chunk_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+};
 
 template <typename F>
 void parallel_for(int count, F f) {
-    const int nthr = count >= 64 ? (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1;
-    if (nthr <= 1) {
-        f(0, count);
-        return;
-    }
-    std::vector<std::thread> pool;
-    const int chunk = (count + nthr - 1) / nthr;
-    for (int t = 0; t < nthr; t++) {
-        const int k0 = t * chunk, k1 = std::min(count, k0 + chunk);
-        if (k0 < k1) pool.emplace_back(f, k0, k1);
-    }
-    for (auto& th : pool) th.join();
+    const std::function<void(int, int)> fn(f);
+    PackPool::get().run(count, fn);
 }
 
 }  // namespace
@@ -635,23 +723,48 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     if (count < 0 || (count > 0 && (!qps || !status_out)))
         return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "dense QP batch: null argument");
     if (count == 0) return MPCCBF_OK;
-    // ---- host: validate, plan, pack (QPs split over up to 16 threads)
+    // ---- host: validate and pack every QP in one pass over the caller's arrays (the pack re-reads
+    // a QP right after its validation, from cache), into per-chunk buffers of the worker pool; the
+    // chunks are then copied into the pinned staging behind each other
+    struct Chunk {
+        int k0 = 0, k1 = 0;
+        std::vector<double> d;
+        std::vector<int32_t> i;
+    };
+    static thread_local std::vector<Chunk> chunks_tl;  // (the caller's: reused across its calls)
+    std::vector<Chunk>& chunks = chunks_tl;            // (captured by reference for the workers)
+    const int w = PackPool::get().width();
+    const int csz = (count + w - 1) / w;
+    if ((int)chunks.size() < w) chunks.resize(w);
+    for (Chunk& ch : chunks) ch.k0 = ch.k1 = 0;
     std::vector<PackPlan> plan(count);
+    std::vector<int64_t> off_d(count), off_i(count);  // chunk-local first, then global
     parallel_for(count, [&](int k0, int k1) {
-        for (int k = k0; k < k1; k++) plan[k] = plan_qp(qps[k]);
+        Chunk& ch = chunks[k0 / csz];  // (one call for the whole batch: chunk 0)
+        ch.k0 = k0;
+        ch.k1 = k1;
+        ch.d.clear();
+        ch.i.clear();
+        for (int k = k0; k < k1; k++) {
+            plan[k] = plan_qp(qps[k]);
+            if (!plan[k].err.empty()) continue;
+            off_d[k] = (int64_t)ch.d.size();
+            off_i[k] = (int64_t)ch.i.size();
+            ch.d.resize(ch.d.size() + plan[k].nd + 1);  // (+1: the compaction's spare entry)
+            ch.i.resize(ch.i.size() + plan[k].ni + 1);
+            pack_qp(qps[k], plan[k], ch.d.data() + off_d[k], ch.i.data() + off_i[k]);
+            ch.d.pop_back();
+            ch.i.pop_back();
+        }
     });
     for (int k = 0; k < count; k++)  // the first bad QP's error, as a serial pass would report
         if (!plan[k].err.empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + plan[k].err);
     // QPs beyond the device elimination (more than 64 variables or 64 equality rows): the equality
     // elimination on the host (host/dense_qp.cpp), the reduced QP solved on the device like the rest
-    std::vector<int32_t> hostred(count, 0);
     std::vector<int> big;
     std::vector<ReducedQP> hred;
     for (int k = 0; k < count; k++)
-        if (plan[k].cap) {
-            hostred[k] = 1;
-            big.push_back(k);
-        }
+        if (plan[k].cap) big.push_back(k);
     hred.resize(big.size());
     for (size_t b = 0; b < big.size(); b++) {
         try {
@@ -660,68 +773,99 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
             return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(big[b]) + ": " + ex.what());
         }
     }
-    std::vector<int64_t> off_d(count), off_i(count);
+    std::vector<size_t> cb_d(w), cb_i(w);
     size_t nd = 0, ni = 0;
-    for (int k = 0; k < count; k++) {
-        off_d[k] = (int64_t)nd;
-        off_i[k] = (int64_t)ni;
-        nd += plan[k].nd;
-        ni += plan[k].ni;
+    for (int c = 0; c < w; c++) {
+        cb_d[c] = nd;
+        cb_i[c] = ni;
+        nd += chunks[c].d.size();
+        ni += chunks[c].i.size();
+        for (int k = chunks[c].k0; k < chunks[c].k1; k++) {
+            off_d[k] += (int64_t)cb_d[c];
+            off_i[k] += (int64_t)cb_i[c];
+        }
+    }
+    // reduced QPs sized by their inequality rows (the reduced rows are a subset of them; a QP with
+    // more than DENSE_ROWS is a capacity error before its rows are read): header + rows each. The
+    // interior-point kernel's row slots (64 per lane slot) and the reduction's LDS image are sized
+    // by the batch's largest QP
+    std::vector<int64_t> red_off(count);
+    size_t nred = 0;
+    int rows_max = 1, nmax = 1, emax = 1;
+    for (int k = 0, b = 0; k < count; k++) {
+        red_off[k] = (int64_t)nred;
+        int rows_k;
+        if (plan[k].cap) {
+            rows_k = std::min(hred[b++].m, DENSE_ROWS);
+        } else {
+            rows_k = std::min(plan[k].mi, DENSE_ROWS);
+            nmax = std::max(nmax, plan[k].n);
+            emax = std::max(emax, plan[k].me);
+        }
+        rows_max = std::max(rows_max, rows_k);
+        nred += (size_t)DQ_HDR + (size_t)std::max(rows_k, 1) * DQ_ROW;  // (>= 1 row: the kernel reads row 0)
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_error(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
     int device = 0;
     hipError_t e = hipGetDevice(&device);
+    // ---- pinned staging (one host-to-device copy): packed doubles | packed ints | off_d | off_i |
+    // red_off | host-reduced flags (only when there are host-reduced QPs)
     const size_t b_d = align16(nd * sizeof(double)), b_i = align16(ni * sizeof(int32_t));
     const size_t b_off = align16((size_t)count * sizeof(int64_t));
-    if (e == hipSuccess) e = g_dense_host.reserve(b_d + b_i + 2 * b_off);
+    const size_t b_int = align16((size_t)count * sizeof(int32_t));
+    const size_t b_hr = big.empty() ? 0 : b_int;
+    const size_t in_bytes = b_d + b_i + 3 * b_off + b_hr;
+    if (e == hipSuccess) e = g_dense_host.reserve(in_bytes);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP staging: ") + hipGetErrorString(e));
     char* hb = (char*)g_dense_host.p;
     double* h_d = (double*)hb;
     int32_t* h_i = (int32_t*)(hb + b_d);
+    parallel_for(count, [&](int k0, int k1) {
+        for (int c = 0; c < w; c++) {
+            const Chunk& ch = chunks[c];
+            if (ch.k0 < k0 || ch.k0 >= k1 || ch.k1 <= ch.k0) continue;
+            if (!ch.d.empty()) std::memcpy(h_d + cb_d[c], ch.d.data(), ch.d.size() * sizeof(double));
+            if (!ch.i.empty()) std::memcpy(h_i + cb_i[c], ch.i.data(), ch.i.size() * sizeof(int32_t));
+        }
+    });
     std::memcpy(hb + b_d + b_i, off_d.data(), count * sizeof(int64_t));
     std::memcpy(hb + b_d + b_i + b_off, off_i.data(), count * sizeof(int64_t));
-    parallel_for(count, [&](int k0, int k1) {
-        for (int k = k0; k < k1; k++) pack_qp(qps[k], plan[k], h_d + off_d[k], h_i + off_i[k]);
-    });
-    // ---- device buffers: packed input | reduced QPs | Z, xp | y | x | obj | int outputs
-    // reduced QPs sized by their inequality rows (the reduced rows are a subset of them; a QP with
-    // more than DENSE_ROWS is a capacity error before its rows are read): header + rows each
-    std::vector<int64_t> red_off(count);
-    size_t nred = 0;
-    for (int k = 0; k < count; k++) {
-        red_off[k] = (int64_t)nred;
-        const int rows_k = hostred[k] ? std::min(hred_rows(hred, big, k), DENSE_ROWS) : std::min(plan[k].mi, DENSE_ROWS);
-        nred += (size_t)DQ_HDR + (size_t)std::max(rows_k, 1) * DQ_ROW;  // (>= 1 row: the kernel reads row 0)
+    std::memcpy(hb + b_d + b_i + 2 * b_off, red_off.data(), count * sizeof(int64_t));
+    if (b_hr) {
+        int32_t* hr = (int32_t*)(hb + b_d + b_i + 3 * b_off);
+        for (int k = 0; k < count; k++) hr[k] = plan[k].cap ? 1 : 0;
     }
+    // ---- device buffers: staged input | reduced QPs | Z, xp | y | x | obj | status | m | pd | iters
+    // (x, obj and status contiguous: one device-to-host copy)
     const size_t b_red = align16(nred * sizeof(double));
-    const size_t b_redoff = align16((size_t)count * sizeof(int64_t));
     const size_t b_zx = align16((size_t)count * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX) * sizeof(double));
     const size_t b_y = align16((size_t)count * DENSE_NZ * sizeof(double));
     const size_t b_x = align16((size_t)count * DENSE_NMAX * sizeof(double));
     const size_t b_obj = align16((size_t)count * sizeof(double));
-    const size_t b_int = align16((size_t)count * sizeof(int32_t));
-    const size_t in_bytes = b_d + b_i + 2 * b_off;
-    const size_t need = in_bytes + b_red + b_redoff + b_zx + b_y + b_x + b_obj + 5 * b_int;
+    const size_t need = in_bytes + b_red + b_zx + b_y + b_x + b_obj + 4 * b_int;
     e = g_dense_buf.reserve(need, device);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP buffers: ") + hipGetErrorString(e));
+    const size_t out_bytes = b_x + b_obj + b_int;
+    e = g_dense_out.reserve(out_bytes);
+    if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP staging: ") + hipGetErrorString(e));
     char* base = (char*)g_dense_buf.p;
     DenseBatch a;
     a.dbl = (const double*)base;
     a.ints = (const int32_t*)(base + b_d);
     a.off_d = (const int64_t*)(base + b_d + b_i);
     a.off_i = (const int64_t*)(base + b_d + b_i + b_off);
+    a.red_off = (const int64_t*)(base + b_d + b_i + 2 * b_off);
+    a.hostred = b_hr ? (const int32_t*)(base + b_d + b_i + 3 * b_off) : nullptr;
     a.count = count;
     char* p = base + in_bytes;
     a.red = (double*)p;
     p += b_red;
-    int64_t* d_redoff = (int64_t*)p;
-    a.red_off = d_redoff;
-    p += b_redoff;
     a.zx = (double*)p;
     p += b_zx;
     a.y = (double*)p;
     p += b_y;
+    char* out_dev = p;
     a.x = (double*)p;
     p += b_x;
     a.obj = (double*)p;
@@ -730,17 +874,16 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     a.m = (int32_t*)(p + b_int);
     a.pd = (int32_t*)(p + 2 * b_int);
     a.iters = (int32_t*)(p + 3 * b_int);
-    int32_t* d_hostred = (int32_t*)(p + 4 * b_int);
-    a.hostred = d_hostred;
     a.maxit = 100;
     a.tol = 1e-9;
     a.feas_tol = 1e-6;
+    a.lds_rows = nmax;
+    a.lds_stride = dev::reduce_stride(nmax, emax);
     hipStream_t s = nullptr;
     e = hipMemcpyAsync(base, hb, in_bytes, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_hostred, hostred.data(), count * sizeof(int32_t), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_redoff, red_off.data(), count * sizeof(int64_t), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(count), dim3(64), 0, s, a);
+        const size_t lds = (size_t)a.lds_rows * a.lds_stride * sizeof(double);
+        hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(count), dim3(64), lds, s, a);
         e = hipGetLastError();
     }
     // host-reduced QPs: their reduced form in the device layout (P, LP padded with the identity, q,
@@ -787,24 +930,26 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         if (e == hipSuccess) e = hipMemcpyAsync(a.pd + k, &hpd[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
     }
     if (e == hipSuccess) {
-        hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, DQ_R>), dim3(count), dim3(64), 0, s, a);
+        if (rows_max <= 64) hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, 1>), dim3(count), dim3(64), 0, s, a);
+        else if (rows_max <= 128) hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, 2>), dim3(count), dim3(64), 0, s, a);
+        else hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, DQ_R>), dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
     }
     if (e == hipSuccess) {
         hipLaunchKernelGGL(dev::dense_expand_kernel, dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
     }
-    std::vector<int32_t> st(count);
-    std::vector<double> obj(count), x((size_t)count * DENSE_NMAX);
-    if (e == hipSuccess) e = hipMemcpyAsync(st.data(), a.status, count * sizeof(int32_t), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(obj.data(), a.obj, count * sizeof(double), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(x.data(), a.x, x.size() * sizeof(double), hipMemcpyDeviceToHost, s);
+    char* ho = (char*)g_dense_out.p;
+    if (e == hipSuccess) e = hipMemcpyAsync(ho, out_dev, out_bytes, hipMemcpyDeviceToHost, s);
     std::vector<double> yb(big.size() * DENSE_NZ);
     for (size_t b = 0; b < big.size() && e == hipSuccess; b++)
         e = hipMemcpyAsync(&yb[b * DENSE_NZ], a.y + (size_t)big[b] * DENSE_NZ, DENSE_NZ * sizeof(double),
                            hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP solve: ") + hipGetErrorString(e));
+    const double* x = (const double*)ho;
+    double* obj = (double*)(ho + b_x);
+    const int32_t* st = (const int32_t*)(ho + b_x + b_obj);
     // host-reduced QPs: x = xp + Z y and the full-space objective
     std::vector<std::vector<double>> xbig(big.size());
     for (size_t b = 0; b < big.size(); b++) {
@@ -824,7 +969,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         status_out[k] = st[k];
         if (obj_out) obj_out[k] = st[k] == MPCCBF_OPTIMAL ? obj[k] : __builtin_nan("");
         const double* xs = &x[(size_t)k * DENSE_NMAX];
-        if (hostred[k]) xs = xbig[bi++].data();
+        if (plan[k].cap) xs = xbig[bi++].data();
         if (st[k] == MPCCBF_OPTIMAL && x_out && x_out[k]) std::memcpy(x_out[k], xs, (size_t)qps[k].n * sizeof(double));
     }
     return MPCCBF_OK;

@@ -172,8 +172,8 @@ struct ImpcArgs {
     double* substeps;
     // diagnostics: num_agents x 16 neighbour ids as the kernel uses them (-1 padded), or nullptr
     int32_t* nb_out;
-    // launch clock (mpccbf_run::kernel_clock): [0] = ~(min over waves of the start), [1] = max of
-    // the end (s_memrealtime, 100 MHz), or nullptr
+    // launch clock (mpccbf_run::kernel_clock): per wave of the launch its (start, end)
+    // s_memrealtime pair (100 MHz; impc_common.hpp kclock_*), or nullptr
     unsigned long long* kclock;
 };
 

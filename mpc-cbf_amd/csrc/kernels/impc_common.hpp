@@ -915,16 +915,31 @@ __device__ __forceinline__ void grid_clear(const ImpcArgs& args) {
     for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < T; e += nthr) args.grid.clr_cnt[e] = 0u;
 }
 
-// launch clock (ImpcArgs::kclock): the earliest wave start and the latest wave end of the launch
-// (s_memrealtime, 100 MHz, chip-wide), one non-returning atomic per wave each; the start is kept
-// complemented (max of ~t = ~min t) so one zero fill initialises both
+// launch clock (ImpcArgs::kclock): every wave of the launch writes its start and end time
+// (s_memrealtime, 100 MHz, chip-wide) into its own pair kclock[2 w, 2 w + 1] (w = the hardware
+// block x waves per block + the wave in the block) with one 16-byte store at its end; the start
+// waits in an LDS word (one per wave of the block). Plain stores to distinct words: one atomic per
+// wave on a shared counter serialised ~2,000 atomics and delayed the waves' first loads. Collision
+// kernels only: in the FoV kernels any clock code at the start moved the register allocation into
+// 36-108 B/lane of scratch
+__device__ __forceinline__ volatile unsigned long long* kclock_lds() {
+    __shared__ unsigned long long t0[16];  // one per wave of a block (<= 1024 threads)
+    return t0;
+}
 __device__ __forceinline__ void kclock_start(const ImpcArgs& args) {
-    if (args.kclock && (threadIdx.x & 63u) == 0)
-        atomicMax(&args.kclock[0], ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
+    (void)args;
+    if ((threadIdx.x & 63u) == 0) kclock_lds()[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
 }
 __device__ __forceinline__ void kclock_end(const ImpcArgs& args) {
-    if (args.kclock && (threadIdx.x & 63u) == 0)
-        atomicMax(&args.kclock[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (!args.kclock || (threadIdx.x & 63u) != 0) return;
+    const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    ulonglong2 v;
+    v.x = kclock_lds()[threadIdx.x >> 6];
+    // the end once the wave's own stores (outputs, table inserts) are acknowledged: the launch is
+    // not over before they are
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    v.y = __builtin_amdgcn_s_memrealtime();
+    reinterpret_cast<ulonglong2*>(args.kclock)[w] = v;
 }
 
 // diagnostics: wall-clock stamp (s_memrealtime, 100 MHz, chip-wide) of phase `k` of agent ai —

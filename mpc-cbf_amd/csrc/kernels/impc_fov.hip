@@ -57,7 +57,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     const int lane = threadIdx.x;
     const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x);
     lds_poison();
-    kclock_start(args);
     grid_clear(args);
     if (ai >= args.num_agents) return;
     stamp(args, ai, lane, 0);
@@ -720,7 +719,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     // (diagnostics; here, not after the query: there it pushed the kernel into scratch)
     write_nb_out(args, ai, lane, grid_mode, nb_scratch, nb0, nnb);
     stamp(args, ai, lane, 7);
-    kclock_end(args);
 }
 
 // The FoV controller's per-neighbour rows for `count` (ego, neighbour) pairs, evaluated by the same

@@ -1227,6 +1227,17 @@ bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k, int n) {
     return impc_rows_may_exceed(op, csr, knn_k);
 }
 
+// Waves of the main IMPC launch for n agents that write the launch clock (ImpcArgs::kclock: the
+// separable and wide collision kernels; 0 for the others)
+int impc_clock_waves(const DevOps& op, int variant, int n) {
+    if (n <= 0 || op.cbf_mode != 0) return 0;
+    if (use_wide(op, variant, n)) return ((n + 3) / 4) * 4;  // 256-thread blocks, one agent per wave
+    const bool sep = op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16;
+    if (op.slack_mode ? (sep && op.cbf_h <= 2) : (sep && sep_variant(variant)))
+        return ((n + 15) / 16) * 4;  // 256-thread blocks of 16 groups
+    return 0;
+}
+
 // Instantiation launch_impc picks for (operators, variant, agents per launch); nullptr if none fits.
 const char* impc_kernel_name(const DevOps& op, int variant, int n) {
     if (op.slack_mode)  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2

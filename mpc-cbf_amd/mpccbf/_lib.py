@@ -22,12 +22,24 @@ EXPORTED = [
     "mpccbf_status_string", "mpccbf_abi_version", "mpccbf_run_steps", "mpccbf_comm_unique_id",
     "mpccbf_comm_create", "mpccbf_comm_destroy", "mpccbf_kernel_name", "mpccbf_fov_control_solve",
     "mpccbf_connectivity_control_solve", "mpccbf_host_operators", "mpccbf_host_last_error",
-    "mpccbf_comm_create_local", "mpccbf_fov_rows_eval",
+    "mpccbf_comm_create_local", "mpccbf_fov_rows_eval", "mpccbf_impc_launch_waves",
 ]
 
 
 class MpccbfError(RuntimeError):
     pass
+
+
+def kernel_clock_us(clock) -> np.ndarray:
+    """Per-launch durations in microseconds from a (num_steps, W, 2) kernel_clock array (numpy
+    int64 / uint64): the largest wave end minus the smallest wave start over the written pairs;
+    NaN for a step with no pair."""
+    c = np.asarray(clock).view(np.uint64).astype(np.float64)
+    t0, t1 = c[..., 0], c[..., 1]
+    on = t1 > 0
+    start = np.where(on, t0, np.inf).min(axis=1)
+    end = np.where(on, t1, -np.inf).max(axis=1)
+    return np.where(np.isfinite(start), (end - start) * 1e-2, np.nan)
 
 
 def status_name(s: int) -> str:
@@ -88,7 +100,8 @@ class Run(C.Structure):
     _fields_ = [("num_steps", C.c_int32), ("states_alt", C.c_void_p), ("status_log", C.c_void_p),
                 ("iters_log", C.c_void_p), ("step_ms", C.c_void_p), ("solve_ms", C.c_void_p),
                 ("comm", C.c_void_p), ("reserve_steps", C.c_int32), ("solve_stride", C.c_int32),
-                ("final_table", C.c_int32), ("kernel_clock", C.c_void_p)]
+                ("final_table", C.c_int32), ("kernel_clock", C.c_void_p),
+                ("kernel_clock_waves", C.c_int32)]
 
 
 class DenseQP(C.Structure):
@@ -143,6 +156,8 @@ def load():
     L.mpccbf_comm_destroy.restype = None
     L.mpccbf_kernel_name.argtypes = [vp]
     L.mpccbf_kernel_name.restype = C.c_char_p
+    L.mpccbf_impc_launch_waves.argtypes = [vp, C.c_int32]
+    L.mpccbf_impc_launch_waves.restype = C.c_int32
     L.mpccbf_last_error.restype = C.c_char_p
     L.mpccbf_fov_rows_eval.argtypes = [C.c_int32, vp, vp, C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]
     L.mpccbf_status_string.restype = C.c_char_p
@@ -257,8 +272,9 @@ class Context:
         """Closed-loop control steps on the device (mpccbf_run_steps). Returns a dict with the
         table holding the final states ('final', a tensor) and, with timing=True, per-step
         device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms). kernel_clock: a
-        (num_steps, 2) uint64-sized device tensor (torch.int64) for every IMPC launch's first-wave
-        start / last-wave end (s_memrealtime, 100 MHz ticks)."""
+        (num_steps, W, 2) device tensor (torch.int64, W >= launch_waves(num_agents)) for every
+        wave's start / end of every IMPC launch (s_memrealtime, 100 MHz ticks; zero: no wave);
+        kernel_clock_us() turns it into per-launch durations."""
         if num_agents is None:
             num_agents = states.shape[0] - agent_first
         b = Batch(num_states=states.shape[0], states=_ptr(states), agent_first=agent_first,
@@ -275,7 +291,8 @@ class Context:
                 step_ms=None if step_ms is None else step_ms.ctypes.data,
                 solve_ms=None if solve_ms is None else solve_ms.ctypes.data,
                 comm=None if comm is None else comm.handle, reserve_steps=reserve_steps,
-                solve_stride=solve_stride, kernel_clock=_ptr(kernel_clock))
+                solve_stride=solve_stride, kernel_clock=_ptr(kernel_clock),
+                kernel_clock_waves=0 if kernel_clock is None else int(kernel_clock.shape[1]))
         _check(load().mpccbf_run_steps(self._h, C.byref(b), C.byref(r), _stream(stream)))
         out = {"final": states if r.final_table == 0 else states_alt}
         if timing:
@@ -283,6 +300,10 @@ class Context:
             sm = solve_ms[:num_steps]
             out["solve_ms"] = sm[sm >= 0]
         return out
+
+    def launch_waves(self, num_agents: int) -> int:
+        """Waves of the IMPC launch for num_agents that write the launch clock (0: no clock)."""
+        return int(load().mpccbf_impc_launch_waves(self._h, int(num_agents)))
 
     def alloc_outputs(self, num_agents: int, device=None):
         import torch

@@ -133,3 +133,43 @@ def test_state_noise_statistics_and_determinism(mpclib):
         z = (a[:, cols] - clean[:, cols]).reshape(-1) / sd
         assert abs(z.mean()) < 4.0 / np.sqrt(z.size)
         assert 0.9 < z.std() < 1.1
+
+
+@pytest.mark.parametrize("n,variant", [(1024, 0), (4096, 0)])
+def test_launch_clock_per_wave(mpclib, n, variant):
+    """mpccbf_run::kernel_clock: every wave of every step's IMPC launch writes its (start, end) pair;
+    the launch durations (largest end - smallest start) are positive, below the HIP-event time of
+    the same steps' kernels, and the clocked run gives the same closed loop as an unclocked one (the
+    clock changes no result). A buffer with fewer pairs per step than the launch's waves is refused."""
+    torch = _torch()
+    from mpccbf._lib import kernel_clock_us
+    dev = torch.device("cuda", 0)
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(n, seed=4)
+    ctx = mpclib.Context(cfg)
+    ctx.set_variant(variant)
+    waves = ctx.launch_waves(n)
+    assert waves == (n if n <= 1024 else n // 4)  # one agent per wave / four per wave
+    tg = torch.tensor(targets, device=dev)
+    steps = 20
+    finals = []
+    for clocked in (True, False):
+        a = torch.tensor(states, device=dev)
+        b = torch.empty_like(a)
+        kc = torch.zeros((steps, waves, 2), dtype=torch.int64, device=dev) if clocked else None
+        r = ctx.run_steps(a, b, steps, targets=tg, knn_k=8, knn_radius=6.0, kernel_clock=kc, timing=not clocked)
+        torch.cuda.synchronize()
+        finals.append(r["final"].cpu().numpy())
+        if clocked:
+            us = kernel_clock_us(kc.cpu().numpy())
+            assert np.all(np.isfinite(us)) and np.all(us > 1.0), us
+            written = (kc.cpu().numpy()[..., 1] != 0).sum(axis=1)
+            assert np.all(written == waves), written  # (every wave holds an agent at these sizes)
+        else:
+            ev_us = r["solve_ms"] * 1e3
+    assert np.median(us) <= np.median(ev_us) * 1.05, (np.median(us), np.median(ev_us))
+    np.testing.assert_array_equal(finals[0], finals[1])
+    with pytest.raises(mpclib.MpccbfError, match="kernel_clock_waves"):
+        a = torch.tensor(states, device=dev)
+        ctx.run_steps(a, torch.empty_like(a), 2, targets=tg, knn_k=8, knn_radius=6.0,
+                      kernel_clock=torch.zeros((2, waves - 1, 2), dtype=torch.int64, device=dev))
