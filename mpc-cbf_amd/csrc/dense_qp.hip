@@ -6,7 +6,9 @@
 //
 // Host: validation (the reference's invalid_argument cases) and a streaming sparse pack of each
 // QP — nonzeros of H, c, c0, and the rows classified as equalities (lo == hi, fixed variables)
-// or inequalities (a finite side; variable bounds as unit rows) in CSR — one host-to-device copy.
+// or inequalities (a finite side; variable bounds as unit rows) in CSR — into pinned host memory
+// that the kernels read over the bus (no copy), in slices: the device reduces one slice while the
+// host packs the next.
 // Device, one 64-lane wavefront per QP, three launches:
 //   dense_reduce_kernel  exact equality elimination: Householder QR with column pivoting of E^T
 //                        (lane = equality row; rank by |R_tt| <= 1e-12 |R_00|), x = xp + Z y with
@@ -17,7 +19,8 @@
 //                        decided here), compacted;
 //   dense_qp_kernel      the Mehrotra PDIP + phase-1 certificate of the structured kernel
 //                        (kernels/pdip.hpp), reduced dimension padded to 8;
-//   dense_expand_kernel  x = xp + Z y and the full-space objective x^T H x + c^T x + c0.
+//   dense_expand_kernel  x = xp + Z y and the objective k0 + q^T y + 1/2 y^T P y (= the full-space
+//                        x^T Hs x + c^T x + c0 at that x), written to pinned host memory.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,6 +35,7 @@
 #include <vector>
 
 #include "../../include/mpccbf.h"
+#include "host/dense_pack.hpp"
 #include "host/dense_qp.hpp"
 #include "host/errors.hpp"
 #include "kernels/group.hpp"
@@ -57,7 +61,7 @@ constexpr int RS_SOLVE = -1, RS_CAP_NZ = -2, RS_CAP_ROWS = -3;
 struct DenseBatch {
     const double* dbl;
     const int32_t* ints;
-    const int64_t* off_d;  // per QP
+    const int64_t* off_d;  // per QP, + the total at [count]
     const int64_t* off_i;
     int32_t count;
     double* red;      // reduced QPs (the PDIP's input), QP k at red + red_off[k]: header + its rows
@@ -68,8 +72,9 @@ struct DenseBatch {
     int32_t* pd;      // count: 1 if P is positive definite (LP its factor)
     double* y;        // count x DENSE_NZ
     int32_t* iters;
-    double* x;        // count x DENSE_NMAX
-    double* obj;      // count
+    double* x;        // count x DENSE_NMAX (host, pinned: written by dense_expand_kernel)
+    double* obj;      // count (host, pinned)
+    int32_t* status_out;  // count (host, pinned): the final statuses
     int32_t maxit;
     double tol;
     double feas_tol;
@@ -77,6 +82,11 @@ struct DenseBatch {
     // equalities; host/dense_qp.cpp), its reduced QP, status, m and pd uploaded, x expanded on the host
     const int32_t* hostred;  // (NULL: none)
     int32_t lds_rows, lds_stride;  // the reduce kernel's E^T image (reduce_stride)
+    // the packed input (dbl, ints, off_*, red_off, hostred) lives in pinned host memory and is read
+    // by the kernels over the bus (no copy); the reduce kernel first stages its QP's packed words
+    // into LDS with one batch of loads: stage_d / stage_i words (the batch's largest QP; 0: direct)
+    int32_t stage_d, stage_i;
+    int32_t first;  // dense_reduce_kernel: the slice's first QP (block b reduces QP first + b)
 };
 
 namespace dev {
@@ -102,7 +112,7 @@ struct ReduceLds {
 __device__ __forceinline__ bool fin_bound(double v) { return isfinite(v) && fabs(v) < kInf; }
 
 __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
-    const int qi = blockIdx.x;
+    const int qi = a.first + (int)blockIdx.x;
     const int l = threadIdx.x;
     if (qi >= a.count || (a.hostred && a.hostred[qi])) return;  // (reduced on the host)
     __shared__ ReduceLds s;
@@ -110,6 +120,38 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     const int LDS_S = a.lds_stride, NROWS = a.lds_rows;
     const int32_t* ib = a.ints + a.off_i[qi];
     const double* db = a.dbl + a.off_d[qi];
+    if (a.stage_d > 0) {
+        // the QP's packed words into LDS (after the E^T image): every load issued before any store,
+        // 8 per lane in flight, so the bus latency is paid a few times instead of once per read
+        double* sd = et + (size_t)NROWS * LDS_S;
+        int32_t* si = (int32_t*)(sd + a.stage_d);
+        const int nd = (int)(a.off_d[qi + 1] - a.off_d[qi]), ni = (int)(a.off_i[qi + 1] - a.off_i[qi]);
+        for (int e0 = 0; e0 < nd; e0 += 8 * 64) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int e = e0 + u * 64 + l;
+                v[u] = db[e < nd ? e : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (e0 + u * 64 + l < nd) sd[e0 + u * 64 + l] = v[u];
+        }
+        for (int e0 = 0; e0 < ni; e0 += 8 * 64) {
+            int32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int e = e0 + u * 64 + l;
+                v[u] = ib[e < ni ? e : 0];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (e0 + u * 64 + l < ni) si[e0 + u * 64 + l] = v[u];
+        }
+        __syncthreads();
+        db = sd;
+        ib = si;
+    }
     const int n = ib[0], me = ib[1], mi = ib[2], nh = ib[3];
     const int32_t* hidx = ib + 4;
     const int32_t* eptr = hidx + nh;
@@ -280,6 +322,9 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
             for (int i = 0; i < n; i++) v = fma(s.z[i * DENSE_NZ + l], 2.0 * s.hx[i] + c[i], v);
         red[2 * DENSE_NZ * DENSE_NZ + l] = v;  // q
     }
+    // the objective's constant at y = 0: c0 + xp^T (Hs xp + c) (the expansion evaluates
+    // k0 + q^T y + 1/2 y^T P y: the full-space objective at x = xp + Z y)
+    const double k0 = db[n] + grp_sum<64>(l < n ? s.xp[l] * (s.hx[l] + c[l]) : 0.0);
     // Cholesky of P (lane 0, in LDS; nz <= 8): the PDIP's start factor when P is positive definite
     int pd = 0;
     if (l == 0 && nz <= DENSE_NZ) {
@@ -306,7 +351,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
             red[DENSE_NZ * DENSE_NZ + j] = (ok && r < nz) ? L[j] : (r == cc ? 1.0 : 0.0);  // padding: identity
         }
         red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ] = ok ? 0.0 : 1e-10 * fmax(1.0, pmax);  // Newton ridge if PSD
-        red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 1] = 0.0;
+        red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 1] = k0;
         pd = ok ? 1 : 0;
     }
     // ---- inequality rows in y: g = Z^T a, bounds shifted by a^T xp; constant rows decided here
@@ -422,29 +467,29 @@ __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
     }
 }
 
-// x = xp + Z y (y = 0 when the equalities decided x) and x^T H x + c^T x + c0 for OPTIMAL QPs.
+// x = xp + Z y (y = 0 when the equalities decided x) and the objective for OPTIMAL QPs; every
+// QP's final status into the pinned output.
 __global__ void __launch_bounds__(64) dense_expand_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int l = threadIdx.x;
-    if (qi >= a.count || a.status[qi] != ST_OPTIMAL || (a.hostred && a.hostred[qi])) return;  // (host-reduced: host expands)
-    __shared__ double xs[DENSE_NMAX];
-    const int32_t* ib = a.ints + a.off_i[qi];
-    const double* db = a.dbl + a.off_d[qi];
-    const int n = ib[0], nh = ib[3];
-    const int32_t* hidx = ib + 4;
-    const double* c = db;
-    const double* hval = db + n + 1;
+    if (qi >= a.count) return;
+    const int st = a.status[qi];
+    if (l == 0) a.status_out[qi] = st;
+    if (st != ST_OPTIMAL || (a.hostred && a.hostred[qi])) return;  // (host-reduced: host expands)
+    // x = xp + Z y; the objective from the reduced QP, k0 + q^T y + 1/2 y^T P y (P, q, k0 in the
+    // device block the reduction wrote: nothing read from the host input)
     const double* zx = a.zx + (size_t)qi * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX);
+    const double* red = a.red + a.red_off[qi];
+    const double* yq = a.y + (size_t)qi * DENSE_NZ;
     double xv = zx[DENSE_NMAX * DENSE_NZ + l];
 #pragma unroll
-    for (int b = 0; b < DENSE_NZ; b++) xv = fma(zx[l * DENSE_NZ + b], a.y[(size_t)qi * DENSE_NZ + b], xv);
-    xs[l] = l < n ? xv : 0.0;
-    __syncthreads();
-    double f = l < n ? c[l] * xv : 0.0;
-    for (int e = l; e < nh; e += 64) f = fma(hval[e] * xs[hidx[e] / n], xs[hidx[e] % n], f);
+    for (int b = 0; b < DENSE_NZ; b++) xv = fma(zx[l * DENSE_NZ + b], yq[b], xv);
+    const int pa = l >> 3, pb = l & 7;  // lane (a, b): 1/2 P_ab y_a y_b; lanes 0..7 also q_l y_l
+    double f = 0.5 * red[l] * yq[pa] * yq[pb];
+    if (l < DENSE_NZ) f = fma(red[2 * DENSE_NZ * DENSE_NZ + l], yq[l], f);
     f = grp_sum<64>(f);
-    if (l < n) a.x[(size_t)qi * DENSE_NMAX + l] = xv;
-    if (l == 0) a.obj[qi] = f + db[n];
+    a.x[(size_t)qi * DENSE_NMAX + l] = xv;  // (beyond n: 0; the host copies n)
+    if (l == 0) a.obj[qi] = f + red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 1];
 }
 
 }  // namespace dev
@@ -468,18 +513,24 @@ struct DevBuf {
         return e;
     }
 };
-struct HostBuf {  // pinned staging of the packed QPs
+struct HostBuf {  // pinned (page-locked, device-mapped) host memory the kernels read / write
     void* p = nullptr;
+    void* dp = nullptr;  // the device's pointer to it
     size_t bytes = 0;
     hipError_t reserve(size_t need) {
         if (p && bytes >= need) return hipSuccess;
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = dp = nullptr;
         bytes = 0;
-        hipError_t e = hipHostMalloc(&p, need);
+        need += need / 4;  // (headroom: a slightly larger batch does not pin again)
+        hipError_t e = hipHostMalloc(&p, need, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(&dp, p, 0);
         if (e == hipSuccess) bytes = need;
         return e;
     }
+    // device address of a host address inside the buffer
+    template <typename T>
+    T* dev(const void* h) const { return (T*)((char*)dp + ((const char*)h - (const char*)p)); }
 };
 thread_local DevBuf g_dense_buf;
 thread_local HostBuf g_dense_host;
@@ -487,153 +538,12 @@ thread_local HostBuf g_dense_out;  // pinned x | obj | status of the last call
 
 size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
 
-bool finite_bound(double v) { return std::isfinite(v) && std::fabs(v) < kInf; }
-
-// Host half: validation (the reference's invalid_argument cases: NULL pointers, n < 1, m < 0,
-// non-finite H / c, NaN bounds) and the row classification; sizes of the packed form.
-struct PackPlan {
-    int n = 0, me = 0, mi = 0, nh = 0, enz = 0, inz = 0;
-    size_t nd = 0, ni = 0;  // doubles / ints of the packed QP
-    std::string err;
-    bool cap = false;
-};
-
-PackPlan plan_qp(const mpccbf_dense_qp& qp) {
-    PackPlan pl;
-    auto fail = [&](const char* m) {
-        pl.err = m;
-        return pl;
-    };
-    if (qp.n < 1) return fail("dense QP: n must be >= 1");
-    if (qp.m < 0) return fail("dense QP: m must be >= 0");
-    if (!qp.H || !qp.c) return fail("dense QP: H and c are required");
-    if (qp.m > 0 && !(qp.A && qp.lo && qp.hi)) return fail("dense QP: A, lo, hi are required when m > 0");
-    const int n = qp.n, m = qp.m;
-    pl.n = n;
-    // branch-free scans (vectorised): a flag for a non-finite entry, the nonzero counts
-    bool nonfin = false;
-    int nh = 0;
-    for (size_t k = 0; k < (size_t)n * n; k++) {
-        const double v = qp.H[k];
-        nh += v != 0.0;
-        nonfin |= !(std::fabs(v) <= DBL_MAX);
-    }
-    if (nonfin) return fail("dense QP: H has a non-finite entry");
-    pl.nh = nh;
-    for (int i = 0; i < n; i++) nonfin |= !(std::fabs(qp.c[i]) <= DBL_MAX);
-    if (nonfin) return fail("dense QP: c has a non-finite entry");
-    for (int k = 0; k < m; k++) {
-        const double lo = qp.lo[k], hi = qp.hi[k];
-        if (std::isnan(lo) || std::isnan(hi)) return fail("dense QP: NaN row bound");
-        const bool eq = finite_bound(lo) && lo == hi, in = !eq && (finite_bound(lo) || finite_bound(hi));
-        if (!eq && !in) continue;  // a free row: not read
-        const double* a = qp.A + (size_t)k * n;
-        int nnz = 0;
-        for (int j = 0; j < n; j++) nnz += a[j] != 0.0;
-        if (eq) {
-            pl.me++;
-            pl.enz += nnz;
-        } else {
-            pl.mi++;
-            pl.inz += nnz;
-        }
-    }
-    for (int i = 0; i < n; i++) {
-        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
-        if (std::isnan(lo) || std::isnan(hi)) return fail("dense QP: NaN variable bound");
-        if (finite_bound(lo) && lo == hi) {
-            pl.me++;
-            pl.enz++;
-        } else if (finite_bound(lo) || finite_bound(hi)) {
-            pl.mi++;
-            pl.inz++;
-        }
-    }
-    pl.cap = n > DENSE_NMAX || pl.me > DENSE_EMAX;
-    pl.ni = 4 + (size_t)pl.nh + (pl.me + 1) + pl.enz + (pl.mi + 1) + pl.inz;
-    pl.nd = (size_t)n + 1 + pl.nh + pl.me + pl.enz + 2 * (size_t)pl.mi + pl.inz;
-    return pl;
-}
-
-// Writes one QP's packed form. Branch-free compaction (each entry written, the cursor advanced by
-// its nonzero flag): a section's cursor may write one entry past its end, so the equality rows are
-// packed before the first inequality entry and each section's leading words after the section
-// before it, and the caller leaves one spare double and int after the QP.
-void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, int32_t* ib) {
-    const int n = qp.n;
-    int32_t* hidx = ib + 4;
-    int32_t* eptr = hidx + pl.nh;
-    int32_t* ecol = eptr + pl.me + 1;
-    int32_t* iptr = ecol + pl.enz;
-    int32_t* icol = iptr + pl.mi + 1;
-    double* c = db;
-    double* hval = db + n + 1;
-    double* erhs = hval + pl.nh;
-    double* evalv = erhs + pl.me;
-    double* ilo = evalv + pl.enz;
-    double* ihi = ilo + pl.mi;
-    double* ivalv = ihi + pl.mi;
-    int h = 0;
-    for (int k = 0; k < n * n; k++) {
-        const double v = qp.H[k];
-        hidx[h] = k;
-        hval[h] = v;
-        h += v != 0.0;
-    }
-    ib[0] = n;
-    ib[1] = pl.me;
-    ib[2] = pl.mi;
-    ib[3] = pl.nh;
-    std::memcpy(c, qp.c, (size_t)n * sizeof(double));
-    db[n] = qp.c0;
-    auto row = [&](const double* a, int32_t* col, double* val, int z) {
-        for (int j = 0; j < n; j++) {
-            const double v = a[j];
-            col[z] = j;
-            val[z] = v;
-            z += v != 0.0;
-        }
-        return z;
-    };
-    // equality rows (rows with lo == hi, then fixed variables)
-    eptr[0] = 0;
-    int e = 0, ez = 0;
-    for (int k = 0; k < qp.m; k++) {
-        const double lo = qp.lo[k], hi = qp.hi[k];
-        if (!(finite_bound(lo) && lo == hi)) continue;
-        ez = row(qp.A + (size_t)k * n, ecol, evalv, ez);
-        erhs[e] = lo;
-        eptr[++e] = ez;
-    }
-    for (int i = 0; i < n; i++) {
-        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
-        if (!(finite_bound(lo) && lo == hi)) continue;
-        ecol[ez] = i;
-        evalv[ez++] = 1.0;
-        erhs[e] = lo;
-        eptr[++e] = ez;
-    }
-    // inequality rows (a finite side, then variable bounds as unit rows)
-    iptr[0] = 0;
-    int r = 0, rz = 0;
-    for (int k = 0; k < qp.m; k++) {
-        const double lo = qp.lo[k], hi = qp.hi[k];
-        if ((finite_bound(lo) && lo == hi) || !(finite_bound(lo) || finite_bound(hi))) continue;
-        rz = row(qp.A + (size_t)k * n, icol, ivalv, rz);
-        ilo[r] = lo;
-        ihi[r] = hi;
-        iptr[++r] = rz;
-    }
-    for (int i = 0; i < n; i++) {
-        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
-        if ((finite_bound(lo) && lo == hi) || !(finite_bound(lo) || finite_bound(hi))) continue;
-        icol[rz] = i;
-        ivalv[rz++] = 1.0;
-        ilo[r] = lo;
-        ihi[r] = hi;
-        iptr[++r] = rz;
-    }
-}
+static_assert(dense_pack::DENSE_NMAX == DENSE_NMAX && dense_pack::DENSE_EMAX == DENSE_EMAX &&
+              dense_pack::kInf == kInf, "dense_pack.hpp and dense_qp.hip agree");
+using dense_pack::finite_bound;
+using dense_pack::PackPlan;
+using dense_pack::plan_qp;
+using dense_pack::pack_qp;
 
 // Host worker pool for the per-QP validation and packing: created on first use (up to 15 workers
 // beside the calling thread), kept for the process (a thread spawn per call cost more than the
@@ -723,39 +633,11 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     if (count < 0 || (count > 0 && (!qps || !status_out)))
         return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "dense QP batch: null argument");
     if (count == 0) return MPCCBF_OK;
-    // ---- host: validate and pack every QP in one pass over the caller's arrays (the pack re-reads
-    // a QP right after its validation, from cache), into per-chunk buffers of the worker pool; the
-    // chunks are then copied into the pinned staging behind each other
-    struct Chunk {
-        int k0 = 0, k1 = 0;
-        std::vector<double> d;
-        std::vector<int32_t> i;
-    };
-    static thread_local std::vector<Chunk> chunks_tl;  // (the caller's: reused across its calls)
-    std::vector<Chunk>& chunks = chunks_tl;            // (captured by reference for the workers)
-    const int w = PackPool::get().width();
-    const int csz = (count + w - 1) / w;
-    if ((int)chunks.size() < w) chunks.resize(w);
-    for (Chunk& ch : chunks) ch.k0 = ch.k1 = 0;
+    // ---- host: validate and size every QP (worker pool), then pack each straight into the pinned
+    // input at its offset (worker pool). The kernels read it there over the bus: no copy
     std::vector<PackPlan> plan(count);
-    std::vector<int64_t> off_d(count), off_i(count);  // chunk-local first, then global
     parallel_for(count, [&](int k0, int k1) {
-        Chunk& ch = chunks[k0 / csz];  // (one call for the whole batch: chunk 0)
-        ch.k0 = k0;
-        ch.k1 = k1;
-        ch.d.clear();
-        ch.i.clear();
-        for (int k = k0; k < k1; k++) {
-            plan[k] = plan_qp(qps[k]);
-            if (!plan[k].err.empty()) continue;
-            off_d[k] = (int64_t)ch.d.size();
-            off_i[k] = (int64_t)ch.i.size();
-            ch.d.resize(ch.d.size() + plan[k].nd + 1);  // (+1: the compaction's spare entry)
-            ch.i.resize(ch.i.size() + plan[k].ni + 1);
-            pack_qp(qps[k], plan[k], ch.d.data() + off_d[k], ch.i.data() + off_i[k]);
-            ch.d.pop_back();
-            ch.i.pop_back();
-        }
+        for (int k = k0; k < k1; k++) plan[k] = plan_qp(qps[k]);
     });
     for (int k = 0; k < count; k++)  // the first bad QP's error, as a serial pass would report
         if (!plan[k].err.empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + plan[k].err);
@@ -773,26 +655,17 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
             return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(big[b]) + ": " + ex.what());
         }
     }
-    std::vector<size_t> cb_d(w), cb_i(w);
-    size_t nd = 0, ni = 0;
-    for (int c = 0; c < w; c++) {
-        cb_d[c] = nd;
-        cb_i[c] = ni;
-        nd += chunks[c].d.size();
-        ni += chunks[c].i.size();
-        for (int k = chunks[c].k0; k < chunks[c].k1; k++) {
-            off_d[k] += (int64_t)cb_d[c];
-            off_i[k] += (int64_t)cb_i[c];
-        }
-    }
-    // reduced QPs sized by their inequality rows (the reduced rows are a subset of them; a QP with
-    // more than DENSE_ROWS is a capacity error before its rows are read): header + rows each. The
-    // interior-point kernel's row slots (64 per lane slot) and the reduction's LDS image are sized
-    // by the batch's largest QP
-    std::vector<int64_t> red_off(count);
-    size_t nred = 0;
-    int rows_max = 1, nmax = 1, emax = 1;
+    // offsets (+ totals), reduced-QP blocks sized by their inequality rows (the reduced rows are a
+    // subset of them; a QP with more than DENSE_ROWS is a capacity error before its rows are read),
+    // the batch maxima that size the kernels (PDIP row slots, the reduction's LDS image and staging)
+    std::vector<int64_t> off_d(count + 1), off_i(count + 1), red_off(count);
+    size_t nd = 0, ni = 0, nred = 0;
+    int rows_max = 1, nmax = 1, emax = 1, sd_max = 0, si_max = 0;
     for (int k = 0, b = 0; k < count; k++) {
+        off_d[k] = (int64_t)nd;
+        off_i[k] = (int64_t)ni;
+        nd += plan[k].nd + 1;  // (+1: the spare word pack_qp's compaction may write past the QP)
+        ni += plan[k].ni + 1;
         red_off[k] = (int64_t)nred;
         int rows_k;
         if (plan[k].cap) {
@@ -801,91 +674,98 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
             rows_k = std::min(plan[k].mi, DENSE_ROWS);
             nmax = std::max(nmax, plan[k].n);
             emax = std::max(emax, plan[k].me);
+            sd_max = std::max(sd_max, (int)plan[k].nd + 1);
+            si_max = std::max(si_max, (int)plan[k].ni + 1);
         }
         rows_max = std::max(rows_max, rows_k);
         nred += (size_t)DQ_HDR + (size_t)std::max(rows_k, 1) * DQ_ROW;  // (>= 1 row: the kernel reads row 0)
     }
+    off_d[count] = (int64_t)nd;
+    off_i[count] = (int64_t)ni;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_error(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
     int device = 0;
     hipError_t e = hipGetDevice(&device);
-    // ---- pinned staging (one host-to-device copy): packed doubles | packed ints | off_d | off_i |
-    // red_off | host-reduced flags (only when there are host-reduced QPs)
+    // ---- pinned input: packed doubles | packed ints | off_d | off_i | red_off | host-reduced
+    // flags (only when there are host-reduced QPs); pinned output: x | obj | status
     const size_t b_d = align16(nd * sizeof(double)), b_i = align16(ni * sizeof(int32_t));
-    const size_t b_off = align16((size_t)count * sizeof(int64_t));
+    const size_t b_off = align16((size_t)(count + 1) * sizeof(int64_t));
     const size_t b_int = align16((size_t)count * sizeof(int32_t));
     const size_t b_hr = big.empty() ? 0 : b_int;
     const size_t in_bytes = b_d + b_i + 3 * b_off + b_hr;
+    const size_t b_x = align16((size_t)count * DENSE_NMAX * sizeof(double));
+    const size_t b_obj = align16((size_t)count * sizeof(double));
     if (e == hipSuccess) e = g_dense_host.reserve(in_bytes);
+    if (e == hipSuccess) e = g_dense_out.reserve(b_x + b_obj + b_int);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP staging: ") + hipGetErrorString(e));
     char* hb = (char*)g_dense_host.p;
     double* h_d = (double*)hb;
     int32_t* h_i = (int32_t*)(hb + b_d);
-    parallel_for(count, [&](int k0, int k1) {
-        for (int c = 0; c < w; c++) {
-            const Chunk& ch = chunks[c];
-            if (ch.k0 < k0 || ch.k0 >= k1 || ch.k1 <= ch.k0) continue;
-            if (!ch.d.empty()) std::memcpy(h_d + cb_d[c], ch.d.data(), ch.d.size() * sizeof(double));
-            if (!ch.i.empty()) std::memcpy(h_i + cb_i[c], ch.i.data(), ch.i.size() * sizeof(int32_t));
-        }
-    });
-    std::memcpy(hb + b_d + b_i, off_d.data(), count * sizeof(int64_t));
-    std::memcpy(hb + b_d + b_i + b_off, off_i.data(), count * sizeof(int64_t));
-    std::memcpy(hb + b_d + b_i + 2 * b_off, red_off.data(), count * sizeof(int64_t));
-    if (b_hr) {
-        int32_t* hr = (int32_t*)(hb + b_d + b_i + 3 * b_off);
-        for (int k = 0; k < count; k++) hr[k] = plan[k].cap ? 1 : 0;
-    }
-    // ---- device buffers: staged input | reduced QPs | Z, xp | y | x | obj | status | m | pd | iters
-    // (x, obj and status contiguous: one device-to-host copy)
+    int64_t* h_offd = (int64_t*)(hb + b_d + b_i);
+    int64_t* h_offi = (int64_t*)(hb + b_d + b_i + b_off);
+    int64_t* h_redoff = (int64_t*)(hb + b_d + b_i + 2 * b_off);
+    int32_t* h_hr = (int32_t*)(hb + b_d + b_i + 3 * b_off);
+    std::memcpy(h_offd, off_d.data(), (count + 1) * sizeof(int64_t));
+    std::memcpy(h_offi, off_i.data(), (count + 1) * sizeof(int64_t));
+    std::memcpy(h_redoff, red_off.data(), count * sizeof(int64_t));
+    if (b_hr)
+        for (int k = 0; k < count; k++) h_hr[k] = plan[k].cap ? 1 : 0;
+    // ---- device buffers: reduced QPs | Z, xp | y | status | m | pd | iters
     const size_t b_red = align16(nred * sizeof(double));
     const size_t b_zx = align16((size_t)count * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX) * sizeof(double));
     const size_t b_y = align16((size_t)count * DENSE_NZ * sizeof(double));
-    const size_t b_x = align16((size_t)count * DENSE_NMAX * sizeof(double));
-    const size_t b_obj = align16((size_t)count * sizeof(double));
-    const size_t need = in_bytes + b_red + b_zx + b_y + b_x + b_obj + 4 * b_int;
-    e = g_dense_buf.reserve(need, device);
+    e = g_dense_buf.reserve(b_red + b_zx + b_y + 4 * b_int, device);
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP buffers: ") + hipGetErrorString(e));
-    const size_t out_bytes = b_x + b_obj + b_int;
-    e = g_dense_out.reserve(out_bytes);
-    if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP staging: ") + hipGetErrorString(e));
-    char* base = (char*)g_dense_buf.p;
+    char* p = (char*)g_dense_buf.p;
     DenseBatch a;
-    a.dbl = (const double*)base;
-    a.ints = (const int32_t*)(base + b_d);
-    a.off_d = (const int64_t*)(base + b_d + b_i);
-    a.off_i = (const int64_t*)(base + b_d + b_i + b_off);
-    a.red_off = (const int64_t*)(base + b_d + b_i + 2 * b_off);
-    a.hostred = b_hr ? (const int32_t*)(base + b_d + b_i + 3 * b_off) : nullptr;
+    a.dbl = g_dense_host.dev<const double>(h_d);
+    a.ints = g_dense_host.dev<const int32_t>(h_i);
+    a.off_d = g_dense_host.dev<const int64_t>(h_offd);
+    a.off_i = g_dense_host.dev<const int64_t>(h_offi);
+    a.red_off = g_dense_host.dev<const int64_t>(h_redoff);
+    a.hostred = b_hr ? g_dense_host.dev<const int32_t>(h_hr) : nullptr;
     a.count = count;
-    char* p = base + in_bytes;
     a.red = (double*)p;
     p += b_red;
     a.zx = (double*)p;
     p += b_zx;
     a.y = (double*)p;
     p += b_y;
-    char* out_dev = p;
-    a.x = (double*)p;
-    p += b_x;
-    a.obj = (double*)p;
-    p += b_obj;
     a.status = (int32_t*)p;
     a.m = (int32_t*)(p + b_int);
     a.pd = (int32_t*)(p + 2 * b_int);
     a.iters = (int32_t*)(p + 3 * b_int);
+    char* ho = (char*)g_dense_out.p;
+    a.x = g_dense_out.dev<double>(ho);
+    a.obj = g_dense_out.dev<double>(ho + b_x);
+    a.status_out = g_dense_out.dev<int32_t>(ho + b_x + b_obj);
     a.maxit = 100;
     a.tol = 1e-9;
     a.feas_tol = 1e-6;
     a.lds_rows = nmax;
     a.lds_stride = dev::reduce_stride(nmax, emax);
+    size_t lds = (size_t)a.lds_rows * a.lds_stride * sizeof(double);
+    const size_t stage = (size_t)sd_max * sizeof(double) + (size_t)si_max * sizeof(int32_t);
+    a.stage_d = a.stage_i = 0;
+    if (lds + stage <= 48 * 1024) {  // (beyond: the kernel reads its QP over the bus where it uses it)
+        a.stage_d = sd_max;
+        a.stage_i = si_max;
+        lds += stage;
+    }
     hipStream_t s = nullptr;
-    e = hipMemcpyAsync(base, hb, in_bytes, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) {
-        const size_t lds = (size_t)a.lds_rows * a.lds_stride * sizeof(double);
-        hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(count), dim3(64), lds, s, a);
+    // pack a slice (worker pool), launch its reduction, pack the next meanwhile
+    const int nslice = count >= 1024 ? 4 : 1;
+    const int slice = (count + nslice - 1) / nslice;
+    for (int q0 = 0; q0 < count && e == hipSuccess; q0 += slice) {
+        const int q1 = std::min(count, q0 + slice);
+        parallel_for(q1 - q0, [&](int k0, int k1) {
+            for (int k = q0 + k0; k < q0 + k1; k++) pack_qp(qps[k], plan[k], h_d + off_d[k], h_i + off_i[k]);
+        });
+        a.first = q0;
+        hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(q1 - q0), dim3(64), lds, s, a);
         e = hipGetLastError();
     }
+    a.first = 0;
     // host-reduced QPs: their reduced form in the device layout (P, LP padded with the identity, q,
     // the Newton ridge when P is only semidefinite, rows [g | lo | hi]) and the decision
     std::vector<std::vector<double>> hblk(big.size());
@@ -939,8 +819,6 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         hipLaunchKernelGGL(dev::dense_expand_kernel, dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
     }
-    char* ho = (char*)g_dense_out.p;
-    if (e == hipSuccess) e = hipMemcpyAsync(ho, out_dev, out_bytes, hipMemcpyDeviceToHost, s);
     std::vector<double> yb(big.size() * DENSE_NZ);
     for (size_t b = 0; b < big.size() && e == hipSuccess; b++)
         e = hipMemcpyAsync(&yb[b * DENSE_NZ], a.y + (size_t)big[b] * DENSE_NZ, DENSE_NZ * sizeof(double),

@@ -1,0 +1,170 @@
+// dense_pack.hpp — host half of the generic dense QP path (dense_qp.hip): validation of one
+// mpccbf_dense_qp (the reference's invalid_argument cases) and its packed form for the device
+// (layout: dense_qp.hip DenseBatch). Header-only so tools/dense_pack_bench.cpp times the same code.
+#pragma once
+
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+
+#include "../../../include/mpccbf.h"
+
+namespace mpccbf {
+namespace dense_pack {
+
+constexpr double kInf = 1e300;  // |bound| >= 1e300 means "absent" (numeric_limits lowest/max)
+constexpr int DENSE_NMAX = 64;  // variables per QP on the device elimination (lane = variable)
+constexpr int DENSE_EMAX = 64;  // equalities per QP on the device elimination
+
+inline bool finite_bound(double v) { return std::isfinite(v) && std::fabs(v) < kInf; }
+
+// Host half: validation (the reference's invalid_argument cases: NULL pointers, n < 1, m < 0,
+// non-finite H / c, NaN bounds) and the row classification; sizes of the packed form.
+struct PackPlan {
+    int n = 0, me = 0, mi = 0, nh = 0, enz = 0, inz = 0;
+    size_t nd = 0, ni = 0;  // doubles / ints of the packed QP
+    std::string err;
+    bool cap = false;
+};
+
+inline PackPlan plan_qp(const mpccbf_dense_qp& qp) {
+    PackPlan pl;
+    auto fail = [&](const char* m) {
+        pl.err = m;
+        return pl;
+    };
+    if (qp.n < 1) return fail("dense QP: n must be >= 1");
+    if (qp.m < 0) return fail("dense QP: m must be >= 0");
+    if (!qp.H || !qp.c) return fail("dense QP: H and c are required");
+    if (qp.m > 0 && !(qp.A && qp.lo && qp.hi)) return fail("dense QP: A, lo, hi are required when m > 0");
+    const int n = qp.n, m = qp.m;
+    pl.n = n;
+    // branch-free scans (vectorised): a flag for a non-finite entry, the nonzero counts
+    bool nonfin = false;
+    int nh = 0;
+    for (size_t k = 0; k < (size_t)n * n; k++) {
+        const double v = qp.H[k];
+        nh += v != 0.0;
+        nonfin |= !(std::fabs(v) <= DBL_MAX);
+    }
+    if (nonfin) return fail("dense QP: H has a non-finite entry");
+    pl.nh = nh;
+    for (int i = 0; i < n; i++) nonfin |= !(std::fabs(qp.c[i]) <= DBL_MAX);
+    if (nonfin) return fail("dense QP: c has a non-finite entry");
+    for (int k = 0; k < m; k++) {
+        const double lo = qp.lo[k], hi = qp.hi[k];
+        if (std::isnan(lo) || std::isnan(hi)) return fail("dense QP: NaN row bound");
+        const bool eq = finite_bound(lo) && lo == hi, in = !eq && (finite_bound(lo) || finite_bound(hi));
+        if (!eq && !in) continue;  // a free row: not read
+        const double* a = qp.A + (size_t)k * n;
+        int nnz = 0;
+        for (int j = 0; j < n; j++) nnz += a[j] != 0.0;
+        if (eq) {
+            pl.me++;
+            pl.enz += nnz;
+        } else {
+            pl.mi++;
+            pl.inz += nnz;
+        }
+    }
+    for (int i = 0; i < n; i++) {
+        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
+        if (std::isnan(lo) || std::isnan(hi)) return fail("dense QP: NaN variable bound");
+        if (finite_bound(lo) && lo == hi) {
+            pl.me++;
+            pl.enz++;
+        } else if (finite_bound(lo) || finite_bound(hi)) {
+            pl.mi++;
+            pl.inz++;
+        }
+    }
+    pl.cap = n > DENSE_NMAX || pl.me > DENSE_EMAX;
+    pl.ni = 4 + (size_t)pl.nh + (pl.me + 1) + pl.enz + (pl.mi + 1) + pl.inz;
+    pl.nd = (size_t)n + 1 + pl.nh + pl.me + pl.enz + 2 * (size_t)pl.mi + pl.inz;
+    return pl;
+}
+
+// Writes one QP's packed form. Branch-free compaction (each entry written, the cursor advanced by
+// its nonzero flag): a section's cursor may write one entry past its end, so the equality rows are
+// packed before the first inequality entry and each section's leading words after the section
+// before it, and the caller leaves one spare double and int after the QP.
+inline void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, int32_t* ib) {
+    const int n = qp.n;
+    int32_t* hidx = ib + 4;
+    int32_t* eptr = hidx + pl.nh;
+    int32_t* ecol = eptr + pl.me + 1;
+    int32_t* iptr = ecol + pl.enz;
+    int32_t* icol = iptr + pl.mi + 1;
+    double* c = db;
+    double* hval = db + n + 1;
+    double* erhs = hval + pl.nh;
+    double* evalv = erhs + pl.me;
+    double* ilo = evalv + pl.enz;
+    double* ihi = ilo + pl.mi;
+    double* ivalv = ihi + pl.mi;
+    int h = 0;
+    for (int k = 0; k < n * n; k++) {
+        const double v = qp.H[k];
+        hidx[h] = k;
+        hval[h] = v;
+        h += v != 0.0;
+    }
+    ib[0] = n;
+    ib[1] = pl.me;
+    ib[2] = pl.mi;
+    ib[3] = pl.nh;
+    std::memcpy(c, qp.c, (size_t)n * sizeof(double));
+    db[n] = qp.c0;
+    auto row = [&](const double* a, int32_t* col, double* val, int z) {
+        for (int j = 0; j < n; j++) {
+            const double v = a[j];
+            col[z] = j;
+            val[z] = v;
+            z += v != 0.0;
+        }
+        return z;
+    };
+    // equality rows (rows with lo == hi, then fixed variables)
+    eptr[0] = 0;
+    int e = 0, ez = 0;
+    for (int k = 0; k < qp.m; k++) {
+        const double lo = qp.lo[k], hi = qp.hi[k];
+        if (!(finite_bound(lo) && lo == hi)) continue;
+        ez = row(qp.A + (size_t)k * n, ecol, evalv, ez);
+        erhs[e] = lo;
+        eptr[++e] = ez;
+    }
+    for (int i = 0; i < n; i++) {
+        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
+        if (!(finite_bound(lo) && lo == hi)) continue;
+        ecol[ez] = i;
+        evalv[ez++] = 1.0;
+        erhs[e] = lo;
+        eptr[++e] = ez;
+    }
+    // inequality rows (a finite side, then variable bounds as unit rows)
+    iptr[0] = 0;
+    int r = 0, rz = 0;
+    for (int k = 0; k < qp.m; k++) {
+        const double lo = qp.lo[k], hi = qp.hi[k];
+        if ((finite_bound(lo) && lo == hi) || !(finite_bound(lo) || finite_bound(hi))) continue;
+        rz = row(qp.A + (size_t)k * n, icol, ivalv, rz);
+        ilo[r] = lo;
+        ihi[r] = hi;
+        iptr[++r] = rz;
+    }
+    for (int i = 0; i < n; i++) {
+        const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
+        if ((finite_bound(lo) && lo == hi) || !(finite_bound(lo) || finite_bound(hi))) continue;
+        icol[rz] = i;
+        ivalv[rz++] = 1.0;
+        ilo[r] = lo;
+        ihi[r] = hi;
+        iptr[++r] = rz;
+    }
+}
+
+}  // namespace dense_pack
+}  // namespace mpccbf
