@@ -41,6 +41,12 @@ pmc fovs_fetch --workload fov --slack -- FETCH_SIZE
 pmc fovs_write --workload fov --slack -- WRITE_SIZE
 pmc fovs_sqa --workload fov --slack -- $SQA
 pmc fovs_mfma --workload fov --slack -- $SQM
+# the 8-rank share (config 4's per-rank launch: the one-agent-per-wave kernel) under the collision
+# table (its kernel has its own name there)
+pmc collision_wfetch --rank-share 8 --agents-total 8192 -- FETCH_SIZE
+pmc collision_wwrite --rank-share 8 --agents-total 8192 -- WRITE_SIZE
+pmc collision_wsqa --rank-share 8 --agents-total 8192 -- $SQA
+pmc collision_wsqb --rank-share 8 --agents-total 8192 -- $SQB
 pmc collision_cache -- SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES
 # the bench lines below read their traffic / VALU figures from this round's summary
 python3 $ROOT/tools/pmc_summary.py $OUT/${TAG}_pmc > $ROOT/profiles/${TAG}_pmc_summary.json
@@ -74,9 +80,12 @@ prof all256 --neighbours all --agents-per-gpu 256 --crowded --steps 200 --warmup
 prof fov --workload fov
 prof fov_slack --workload fov --slack
 prof dense --workload dense --steps 10 --warmup 2
-step pytest; (cd $ROOT && timeout -k 10 400 python3 -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $OUT/${TAG}_pytest_gpu.log 2>&1)
+step pytest; (cd $ROOT && timeout -k 10 600 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/${TAG}_pytest_gpu.log 2>&1) || true
+step reference instances; (cd $ROOT && timeout -k 10 400 python3 -u tools/reference_instances.py --out $OUT/${TAG}_reference_instances.json > $OUT/${TAG}_reference_instances.log 2>&1)
+step critical path; rm -f $OUT/${TAG}_critical_path.json
+(cd $ROOT && CP_JSON=$OUT/${TAG}_critical_path.json MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/stamps/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 1024 60 0 > $OUT/${TAG}_stamps_share.log 2>&1)
 step fovs status; (cd $ROOT && MPCCBF_CHECK_SLACK=1 timeout -k 10 300 python3 $ROOT/tools/fov_status_check.py 1000 $OUT/${TAG}_fovs_status.npz > $OUT/${TAG}_fovs_status.log 2>&1)
-step stamps; (cd $ROOT && MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/stamps/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1)
+step stamps; (cd $ROOT && CP_JSON=$OUT/${TAG}_critical_path.json MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/stamps/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision.log 2>&1)
 step stamps pdip; (cd $ROOT && MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 4096 100 0 > $OUT/${TAG}_stamps_collision_das.log 2>&1)
 step stamps fov; (cd $ROOT && WORKLOAD=fov MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/stamps/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov.log 2>&1)
 step stamps fov das; (cd $ROOT && WORKLOAD=fov MPCCBF_LIB=$ROOT/mpc-cbf_amd/build/prof/libmpccbf.so timeout -k 10 120 python3 tools/stamp_profile.py 512 100 0 > $OUT/${TAG}_stamps_fov_das.log 2>&1)
