@@ -472,14 +472,25 @@ def main():
         kern_avg, p99, kern_max = vals[7], vals[8], vals[9]
         launch_avg, launch_max = vals[11], vals[12]
         flops_rank0 = flops
-    kern_bracket = kern_avg
     nbk = total - 1 if args.neighbours == "all" else args.knn  # neighbours per agent (at most)
-    # the dominant kernel's average duration: the device clock of every IMPC launch of the timed
-    # pass (first-wave start to last-wave end; rocprof's kernel time); the host-loop form has no
-    # such clock and keeps the HIP-event brackets
+    # the dominant kernel's average duration per launch, in this order: the waves' own clock of the
+    # timed pass (collision kernels: first wave start to last wave end); else, when a step is that
+    # one launch (FoV on one GPU: no fallback, no foreign rows), the timed region per step (the
+    # launches back to back); else HIP events around every launch of the replay. The events around
+    # a launch hold its dispatch too (+4-5 us on config 3: kernel_event_bracket_avg_us)
     region_avg = (region_ms / nsteps) if region_ms is not None else None
-    if launch_avg > 0:
+    kern_bracket = kern_avg
+    kern_src = "events"
+    # (every other robot as a neighbour: the main launch defers nearly every agent to the capacity
+    # launch, so the events around both are the step's kernel time)
+    fb_launch = args.neighbours == "all"
+    if launch_avg > 0 and not fb_launch:
         kern_avg, kern_max = launch_avg * 1e-3, launch_max * 1e-3
+        kern_src = "clock"
+    elif region_avg is not None and world == 1 and args.rank_share <= 0 and not fb_launch and \
+            not kname.startswith("impc_wide_kernel"):
+        kern_avg = region_avg
+        kern_src = "region"
 
     if rank == 0:
         solved = hist["OPTIMAL"] + hist["INFEASIBLE"]
@@ -563,17 +574,17 @@ def main():
                 "kernel": kname,
                 "kernel_avg_us": kern_avg * 1e3,
                 "kernel_max_us": kern_max * 1e3,
-                "kernel_timing": ("the device clock of every IMPC launch of the timed pass: first-wave start "
-                                  "to last-wave end (s_memrealtime, mpccbf_run::kernel_clock), the kernel's own "
-                                  "duration as rocprof reports it" if launch_avg > 0 else
-                                  "HIP events around every IMPC launch (host-driven loop)"),
+                "kernel_timing": {
+                    "clock": "the timed pass's waves themselves, first wave start to last wave end (stores "
+                             "drained), s_memrealtime per wave (mpccbf_run::kernel_clock): the launch without "
+                             "its dispatch and end-of-kernel write-back, which rocprof's duration adds (~1.5 us)",
+                    "region": "the timed region per step: one launch per step, back to back",
+                    "events": "HIP events around every IMPC launch (they hold its dispatch too)"}[kern_src],
+                "kernel_event_bracket_avg_us": kern_bracket * 1e3,
                 "step_region_avg_us": None if region_avg is None else region_avg * 1e3,
                 "step_region_timing": "HIP events at the two ends of the timed region divided by the steps "
                                       "(kernel + fallback / insert launches + dispatch gaps)",
-                "kernel_event_bracket_avg_us": kern_bracket * 1e3,
-                "kernel_event_bracket_timing": "HIP events around the IMPC launch(es) of every step of an "
-                                               "identical replay of the timed steps" + (
-                                                   " (statuses bit-identical to the timed pass)" if replay_same else ""),
+                "replay_statuses_identical": bool(replay_same) if replay_same is not None else None,
                 "flops_per_launch": flops_per_launch,
                 "flops_model": "executed solver steps (dual active-set + PDIP Newton) x the FP64 flops "
                                "of an active-set step (bench.py flops_per_qp_sep, a lower bound); QPs "
