@@ -334,7 +334,7 @@ def main():
             e0.record()  # torch's current stream: the one run_steps launches on
             r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=log[0], iters_log=log[1],
                               timing=timing, solve_stride=1, step_index=args.warmup,
-                              kernel_clock=None if timing else kclock, **common)
+                              kernel_clock=kclock if timing else None, **common)
             e1.record()
             barrier_sync()
             return time.perf_counter() - t0, r
@@ -343,18 +343,18 @@ def main():
         elapsed, _ = closed_loop(logs[0], timing=False)
         # device time of the timed region by HIP events at its two ends (no event between launches)
         region_ms = e0.elapsed_time(e1)
-        # each IMPC launch's own duration in the timed pass: the kernel's first-wave start to its
-        # last-wave end on the device clock (s_memrealtime, 100 MHz; mpccbf_run::kernel_clock)
-        # (collision kernels only: the FoV kernels carry no clock, their kernel time is the events')
+        # replay of the identical steps (same initial swarm, counter-based noise keyed by the step
+        # index) with HIP events on the launch stream: per-step device time (p99), the events around
+        # every IMPC launch, and each launch's own duration on the device clock (first-wave start to
+        # last-wave end, s_memrealtime 100 MHz, mpccbf_run::kernel_clock; collision kernels only: the
+        # FoV kernels carry none) — the clock's per-wave stores cost ~0.6 us per launch, so the
+        # throughput pass carries neither
+        _, rr = closed_loop(logs[1], timing=True)
         launch_us = None
         if kclock is not None:
             from mpccbf._lib import kernel_clock_us
             launch_us = kernel_clock_us(kclock.cpu().numpy())
             launch_us = launch_us if np.all(np.isfinite(launch_us)) else None
-        # replay of the identical steps (same initial swarm, counter-based noise keyed by the step
-        # index) with HIP events on the launch stream: per-step device time (p99) and the IMPC
-        # kernel's duration on every step (roofline), without perturbing the throughput pass
-        _, rr = closed_loop(logs[1], timing=True)
         step_ms, kern_ms = rr["step_ms"].astype(np.float64), rr["solve_ms"].astype(np.float64)
         replay_same = bool(torch.equal(logs[0][0], logs[1][0]) and torch.equal(logs[0][1], logs[1][1]))
         if world == 1 and not args.no_trace and args.rank_share <= 0:
@@ -575,9 +575,10 @@ def main():
                 "kernel_avg_us": kern_avg * 1e3,
                 "kernel_max_us": kern_max * 1e3,
                 "kernel_timing": {
-                    "clock": "the timed pass's waves themselves, first wave start to last wave end (stores "
-                             "drained), s_memrealtime per wave (mpccbf_run::kernel_clock): the launch without "
-                             "its dispatch and end-of-kernel write-back, which rocprof's duration adds (~1.5 us)",
+                    "clock": "the waves themselves on every launch of an identical replay of the timed steps, "
+                             "first wave start to last wave end (stores drained), s_memrealtime per wave "
+                             "(mpccbf_run::kernel_clock): the launch without its dispatch and end-of-kernel "
+                             "write-back, which rocprof's duration adds",
                     "region": "the timed region per step: one launch per step, back to back",
                     "events": "HIP events around every IMPC launch (they hold its dispatch too)"}[kern_src],
                 "kernel_event_bracket_avg_us": kern_bracket * 1e3,
