@@ -134,7 +134,8 @@ for v in VARIANTS:
         d["entries"].append({"kernel": ctx.kernel_name, "workload": "fov" if FOV else "collision", "agents": N,
                              "variant": v, "span_us": float(end.max()), "agent_wall_max_us": float(np.max(end - start)),
                              "agent_wall_mean_us": float(np.mean(end - start)),
-                             "phases_mean_us": {nm: float(np.mean(s[:, k + 1] - s[:, k])) for k, nm in enumerate(PH)},
+                             "phases_mean_us": {nm: float(np.mean((s[:, k + 1] - s[:, k])[(s[:, k] > 0) & (s[:, k + 1] > 0)]))
+                                                for k, nm in enumerate(PH)},
                              "critical_agent_phases_us": [float(x) for x in np.diff(s[crit])]})
         json.dump(d, open(path, "w"), indent=1)
     print(f"   critical agent {crit}: status {status[crit]}, start {start[crit]:.1f}, "
