@@ -681,6 +681,110 @@ __device__ int stage_cbf_rows(const DevOps& op, const double* buf, const ImpcArg
     return count;
 }
 
+// The same rows in one pass over the (sample, neighbour) pairs (16-lane groups, the separable
+// kernel): lane p of a pass takes sample k0 + p / nnb and neighbour p % nnb, so iteration 1's two
+// samples fill one pass where stage_cbf_rows makes one per sample with half the lanes idle. The
+// samples' ego states and U_k s0 terms are formed once per group into smp (up to 3 samples at a
+// time: lane 6 k + s the state, lane 18 + 3 k + d the U_k s0 term, 27 doubles) with the same
+// arithmetic as cbf_ego_state, and the pairs go in the same sample-major order: the staged rows
+// are bit-identical to stage_cbf_rows'.
+template <int NZ>
+__device__ int stage_cbf_rows_pairs(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
+                                    const double (&s0)[6], const double (&y)[NZ], bool grid_mode,
+                                    const NbScratch* nbs, int nb0, int nnb, double* stage, int cap, int gl,
+                                    bool* infeasible, double* smp) {
+    constexpr int G = 16, KC = 3;
+    const double* UZ = opp(buf, op.o_UZ);
+    const double* US = opp(buf, op.o_US);
+    const int nk = (it == 0) ? 1 : op.cbf_h;
+    int count = 0;
+    bool row_infeasible = false;
+    for (int k0 = 0; k0 < nk; k0 += KC) {
+        const int kn = nk - k0 < KC ? nk - k0 : KC;
+        wave_lds_sync();  // (the previous chunk's reads of smp are done)
+        for (int t = gl; t < 27; t += G) {
+            const bool st = t < 18;
+            const int kk = st ? t / 6 : (t - 18) / 3;
+            if (kk >= kn) continue;
+            const int k = k0 + kk;
+            double v = 0.0;
+            if (st) {
+                const int sr = t - 6 * kk;
+                if (it == 0) {
+#pragma unroll
+                    for (int u = 0; u < 6; u++) v = u == sr ? s0[u] : v;
+                } else {
+                    const double* PS = opp(buf, op.o_PS) + (size_t)k * 36 + (size_t)sr * 6;
+                    const double* PZ = opp(buf, op.o_PZ) + (size_t)k * 6 * NZ + (size_t)sr * NZ;
+#pragma unroll
+                    for (int u = 0; u < 6; u++) v = fma(PS[u], s0[u], v);
+#pragma unroll
+                    for (int jz = 0; jz < NZ; jz++) v = fma(PZ[jz], y[jz], v);
+                }
+            } else {
+                const int d = t - 18 - 3 * kk;
+                const double* USkd = US + (size_t)k * 18 + (size_t)d * 6;
+#pragma unroll
+                for (int u = 0; u < 6; u++) v = fma(USkd[u], s0[u], v);
+            }
+            smp[t] = v;
+        }
+        wave_lds_sync();
+        const int np = kn * nnb;
+        for (int base = 0; base < np; base += G) {
+            const int p = base + gl;
+            int kk = 0;
+            for (int c = 1; c < KC; c++) kk += p >= c * nnb ? 1 : 0;
+            const int j = p - kk * nnb;
+            bool keep = false;
+            double a[3] = {0.0, 0.0, 0.0}, b = 0.0;
+            if (p < np) {
+                double e[6];
+#pragma unroll
+                for (int sr = 0; sr < 6; sr++) e[sr] = smp[6 * kk + sr];
+                double npx, npy, nvx, nvy;
+                if (grid_mode) {
+                    const int c = nbs->src[j];
+                    npx = nbs->cst[0][c];
+                    npy = nbs->cst[1][c];
+                    nvx = nbs->cst[2][c];
+                    nvy = nbs->cst[3][c];
+                } else {
+                    const double* ns = args.states + (size_t)args.nb_col[nb0 + j] * 6;
+                    npx = ns[0];
+                    npy = ns[1];
+                    nvx = ns[3];
+                    nvy = ns[4];
+                }
+                safety_cbf(e, npx, npy, nvx, nvy, op.d_min, a, b);
+                double bmax = 0.0, bmin = 0.0;
+#pragma unroll
+                for (int d = 0; d < 3; d++) {
+                    const double v1 = -a[d] * op.a_lo[d], v2 = -a[d] * op.a_hi[d];
+                    bmax += fmax(v1, v2);
+                    bmin += fmin(v1, v2);
+                }
+                keep = !(op.cbf_filter && b >= bmax);
+                if (b < bmin - op.feas_tol) row_infeasible = true;
+            }
+            const unsigned long long msk = grp_ballot<G>(keep);
+            const int slot = count + __popcll(msk & ((1ull << gl) - 1ull));
+            if (keep && slot < cap) {
+                double* dst = stage + (size_t)slot * (NZ + 1);
+                const double* UZk = UZ + (size_t)(k0 + kk) * 3 * NZ;  // (this lane's sample)
+#pragma unroll
+                for (int jz = 0; jz < NZ; jz++)
+                    dst[jz] = -(a[0] * UZk[jz] + a[1] * UZk[NZ + jz] + a[2] * UZk[2 * NZ + jz]);
+                dst[NZ] = b + (a[0] * smp[18 + 3 * kk] + a[1] * smp[18 + 3 * kk + 1] + a[2] * smp[18 + 3 * kk + 2]);
+            }
+            count += __popcll(msk);
+        }
+    }
+    *infeasible = grp_ballot<G>(row_infeasible) != 0ull;
+    wave_lds_sync();
+    return count;
+}
+
 // Objective value 1/2 y^T P y + q^T y + k at the solution (x^T H x + c^T x of the full QP).
 template <int NZ>
 __device__ __forceinline__ double reduced_objective(const DevOps& op, const double* buf,

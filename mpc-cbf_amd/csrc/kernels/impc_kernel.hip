@@ -614,8 +614,16 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         } else {
             double sx[6];  // the state again (not kept in registers across the solves)
             load_state_lds(s0k, sx);
-            count = stage_cbf_rows<NZ, G>(op, buf, args, it, sx, y, grid_mode, &nbs,
-                                          nb0, nnb, stage, cap, gl, &row_infeasible);
+            // (the staging area's tail beyond the cap rows holds the samples' terms when it has
+            // room: the dual active set's scratch is larger than 16 rows)
+            constexpr int STG = CB * 16 * (SEP_NZ + 1) > sep_pol_doubles<SB, CB>() ? CB * 16 * (SEP_NZ + 1)
+                                                                                   : sep_pol_doubles<SB, CB>();
+            if (STG - cap * (NZ + 1) >= 27 && it > 0)
+                count = stage_cbf_rows_pairs<NZ>(op, buf, args, it, sx, y, grid_mode, &nbs, nb0, nnb, stage, cap, gl,
+                                                 &row_infeasible, stage + cap * (NZ + 1));
+            else
+                count = stage_cbf_rows<NZ, G>(op, buf, args, it, sx, y, grid_mode, &nbs,
+                                              nb0, nnb, stage, cap, gl, &row_infeasible);
             live = count > 0;
 #pragma unroll
             for (int c = 0; c < CB; c++) {
