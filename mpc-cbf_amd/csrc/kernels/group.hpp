@@ -9,7 +9,8 @@
 //   row_half_mirror      (i <-> 7-i)  row_mirror           (i <-> 15-i)
 // after the two quad stages every lane of a quad holds the quad total, so the mirrors pair each
 // lane with a lane of the other quad / other half-row, which is all an all-reduce needs.
-// Stages across 16-lane rows (G = 32, 64) use ds_swizzle/bpermute via __shfl_xor.
+// Stages across 16-lane rows (G = 32, 64) use v_permlane16_swap / v_permlane32_swap (VALU lane
+// swaps, no LDS round trip; bit-identical to the lane-xor exchange since the combines commute).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -41,6 +42,29 @@ __device__ __forceinline__ double dpp_mov(double v) {
     return __longlong_as_double(__builtin_amdgcn_mov_dpp(b, CTRL, 0xF, 0xF, true));
 }
 
+__device__ __forceinline__ double mk_double(unsigned lo, unsigned hi) {
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// the other 16-lane row's value of v (S32 false: rows 0<->1, 2<->3; true: rows 0,1 <-> 2,3) as
+// the pair {own, partner} in lane-dependent order (the ops applied to it are commutative)
+template <bool S32>
+__device__ __forceinline__ void row_pair(double v, double& a, double& b) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    if constexpr (S32) {
+        const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        a = mk_double(l[0], h[0]);
+        b = mk_double(l[1], h[1]);
+    } else {
+        const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        a = mk_double(l[0], h[0]);
+        b = mk_double(l[1], h[1]);
+    }
+}
+
 enum class Op { Sum, Max, Min };
 
 template <Op OP>
@@ -57,8 +81,15 @@ __device__ __forceinline__ double grp_reduce(double v) {
     v = combine<OP>(v, dpp_mov<DPP_XOR2>(v));
     v = combine<OP>(v, dpp_mov<DPP_HALF_MIRROR>(v));
     v = combine<OP>(v, dpp_mov<DPP_MIRROR>(v));
-    if constexpr (G >= 32) v = combine<OP>(v, __shfl_xor(v, 16, G));
-    if constexpr (G >= 64) v = combine<OP>(v, __shfl_xor(v, 32, G));
+    double a, b;
+    if constexpr (G >= 32) {
+        row_pair<false>(v, a, b);
+        v = combine<OP>(a, b);
+    }
+    if constexpr (G >= 64) {
+        row_pair<true>(v, a, b);
+        v = combine<OP>(a, b);
+    }
     return v;
 }
 
@@ -78,13 +109,20 @@ __device__ __forceinline__ void grp_sum_vec(double (&v)[N]) {
     for (int i = 0; i < N; i++) v[i] += dpp_mov<DPP_HALF_MIRROR>(v[i]);
 #pragma unroll
     for (int i = 0; i < N; i++) v[i] += dpp_mov<DPP_MIRROR>(v[i]);
+    double a, b;
     if constexpr (G >= 32) {
 #pragma unroll
-        for (int i = 0; i < N; i++) v[i] += __shfl_xor(v[i], 16, G);
+        for (int i = 0; i < N; i++) {
+            row_pair<false>(v[i], a, b);
+            v[i] = a + b;
+        }
     }
     if constexpr (G >= 64) {
 #pragma unroll
-        for (int i = 0; i < N; i++) v[i] += __shfl_xor(v[i], 32, G);
+        for (int i = 0; i < N; i++) {
+            row_pair<true>(v[i], a, b);
+            v[i] = a + b;
+        }
     }
 }
 

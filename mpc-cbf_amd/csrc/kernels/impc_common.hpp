@@ -550,7 +550,19 @@ __device__ __forceinline__ double agent_linear_term_lanes(const DevOps& op, cons
     const double* Kr = opp(buf, op.o_Kr);
     const int nr = 3 * op.spd_f;
     const double* rt = args.refs + (size_t)ai * 3 * op.K + 3 * (op.K - op.spd_f);
-    for (int j = 0; j < nr; j++) q = fma(Qr[(size_t)i * nr + j], rt[j], q);
+    // (8 entries' loads at a time, indices clamped: as a plain loop each entry's two loads were
+    // waited for before the next entry's issued)
+    for (int j0 = 0; j0 < nr; j0 += 8) {
+        double qa[8], ra[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int j = j0 + u < nr ? j0 + u : nr - 1;
+            qa[u] = Qr[(size_t)i * nr + j];
+            ra[u] = rt[j];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) q = j0 + u < nr ? fma(qa[u], ra[u], q) : q;
+    }
     for (int j = gl - 6; gl >= 6 && j < nr; j += G - 6) {
         double v = 0.0;
 #pragma unroll
@@ -1010,13 +1022,16 @@ __host__ __device__ __forceinline__ int xcd_block(int b, int nb) {
 }
 
 // the bucket counts of the table two steps ahead are zeroed by the launch's threads, and the other
-// step parity's defer-queue header by block 0 (called by every thread before any early exit)
+// step parity's defer-queue header by block 0 (called by every thread before any early exit).
+// NT: the launch's block size as a constant — blockDim.x is a 16-bit field of the dispatch packet,
+// fetched with a vector load whose wait put one memory round trip at the head of every launch.
+template <int NT>
 __device__ __forceinline__ void grid_clear(const ImpcArgs& args) {
     if (args.defer_clear && blockIdx.x == 0 && threadIdx.x == 0) args.defer_clear[0] = 0;
     if (!args.grid.clr_cnt) return;
     const uint32_t T = args.grid.mask + 1u;
-    const uint32_t nthr = gridDim.x * blockDim.x;
-    for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < T; e += nthr) args.grid.clr_cnt[e] = 0u;
+    const uint32_t nthr = gridDim.x * (uint32_t)NT;
+    for (uint32_t e = blockIdx.x * (uint32_t)NT + threadIdx.x; e < T; e += nthr) args.grid.clr_cnt[e] = 0u;
 }
 
 // launch clock (ImpcArgs::kclock): every wave of the launch writes its start and end time
@@ -1034,9 +1049,10 @@ __device__ __forceinline__ void kclock_start(const ImpcArgs& args) {
     (void)args;
     if ((threadIdx.x & 63u) == 0) kclock_lds()[threadIdx.x >> 6] = __builtin_amdgcn_s_memrealtime();
 }
+template <int NT>  // the block size (as grid_clear)
 __device__ __forceinline__ void kclock_end(const ImpcArgs& args) {
     if (!args.kclock || (threadIdx.x & 63u) != 0) return;
-    const unsigned w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const unsigned w = blockIdx.x * (unsigned)(NT >> 6) + (threadIdx.x >> 6);
     ulonglong2 v;
     v.x = kclock_lds()[threadIdx.x >> 6];
     // the end once the wave's own stores (outputs, table inserts) are acknowledged: the launch is

@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     const int lane = threadIdx.x;
     const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x);
     lds_poison();
-    grid_clear(args);
+    grid_clear<64>(args);
     if (ai >= args.num_agents) return;
     stamp(args, ai, lane, 0);
     const double* zero_row = nullptr;

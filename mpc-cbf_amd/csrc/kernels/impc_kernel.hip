@@ -42,7 +42,7 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
     const int gl = threadIdx.x & (G - 1);
     const int gib = threadIdx.x / G;
     const int ai = blockIdx.x * GPB + gib;  // agent index within the batch
-    grid_clear(args);
+    grid_clear<256>(args);
     if (ai >= args.num_agents) return;      // whole group leaves together
     stamp(args, ai, gl, 0);
 
@@ -875,12 +875,12 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     lds_poison();
     if constexpr (!QUEUE) {
         kclock_start(args);
-        grid_clear(args);
+        grid_clear<BS>(args);
         const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * GPB + gib;
         if (ai >= args.num_agents) return;
         impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
                                                    nb_scratch[gib], keep_all[gib]);
-        kclock_end(args);
+        kclock_end<BS>(args);
     } else {
         // one queue entry per group (no grid-stride loop: carried across iterations the agent's
         // state spills, 0 -> 352 B/lane); groups beyond the queue's length leave at once. The
@@ -1137,13 +1137,13 @@ __global__ void __launch_bounds__(BS) impc_wide_kernel(const DevOps op, const do
 #pragma unroll
         for (int r = 0; r < PER; r++) ops[r * BS + threadIdx.x] = v[r];
     }
-    grid_clear(args);
+    grid_clear<BS>(args);
     __syncthreads();
     const int wv = uni_i((int)(threadIdx.x >> 6));
     const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * WPB + wv;
     if (ai >= args.num_agents) return;
     impc_wide_agent(op, ops, args, ai, lds_all[wv]);
-    kclock_end(args);
+    kclock_end<BS>(args);
 }
 
 }  // namespace dev

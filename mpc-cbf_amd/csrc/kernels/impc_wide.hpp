@@ -85,29 +85,6 @@ __device__ __forceinline__ void uni_arr(double (&a)[N]) {
 __device__ __forceinline__ int uni_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ bool uni_b(bool v) { return __builtin_amdgcn_readfirstlane((int)v) != 0; }
 
-__device__ __forceinline__ double mk_double(unsigned lo, unsigned hi) {
-    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
-// the other 16-lane row's value of v (S32 false: rows 0<->1, 2<->3; true: rows 0,1 <-> 2,3) as
-// the pair {own, partner} in lane-dependent order (the ops applied to it are commutative)
-template <bool S32>
-__device__ __forceinline__ void row_pair(double v, double& a, double& b) {
-    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
-    if constexpr (S32) {
-        const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
-        const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
-        a = mk_double(l[0], h[0]);
-        b = mk_double(l[1], h[1]);
-    } else {
-        const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-        const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-        a = mk_double(l[0], h[0]);
-        b = mk_double(l[1], h[1]);
-    }
-}
-
 // two 64-lane max all-reductions, stage-interleaved (every lane ends with both maxima)
 __device__ __forceinline__ void wave_max2(double& a, double& b) {
     grp_max2<16>(a, b);

@@ -1,6 +1,6 @@
 # dense path: tests, bench, profile (zero-copy pinned input)
 set -o pipefail
-OUT=$GRAFT_REPO_ROOT/gpurun_out/r05k
+OUT=$GRAFT_REPO_ROOT/gpurun_out/${TAGO:-r05k}
 mkdir -p $OUT
 cd $GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m pytest tests/test_dense_qp.py tests/test_qpcpp_adapter.py -m gpu -v --timeout 200 --timeout-method thread > $OUT/pytest_dense.log 2>&1
