@@ -159,6 +159,19 @@ __device__ __forceinline__ void das_load_operators(WaveAS& ws, const double* __r
     wave_lds_sync();
 }
 
+// das_load_operators' stores from operands the caller loaded (P^-1 / P entries lane + 64 k)
+__device__ __forceinline__ void das_store_operators(WaveAS& ws, const double (&pi)[WNZ * WNZ / 64],
+                                                    const double (&pp)[WNZ * WNZ / 64], int lane) {
+#pragma unroll
+    for (int k = 0; k < WNZ * WNZ / 64; k++) {
+        const int e = lane + 64 * k;
+        ws.Pi[(e >> 4) * 17 + (e & 15)] = pi[k];
+        ws.P[(e >> 4) * 17 + (e & 15)] = pp[k];
+        ws.W[e] = 0.0;
+    }
+    wave_lds_sync();
+}
+
 // Returns 1: optimal (sc.y, rp_out, rd_out; the active rows' multipliers in ws.u[0 .. ws.k)); -1: no
 // step reaches the candidate (no feasible point; tlow = the certificate's lower bound on phase
 // 1's t*; cand = the unreachable candidate's image row, the active rows in ws.row[0 .. ws.k) with
@@ -233,40 +246,44 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         }
         wave_lds_sync();
     };
-    for (;;) {
-        // the largest scaled violation of the wave (convergence) and the candidate (lowest lane
-        // on ties): the eligible side with the largest normalised violation (before the weights
-        // exist: the largest scaled one)
-        double vb = -1.0, eb = -1.0;
-        int rb = 0, sdb = 1;
-        double bb = 0.0;
-        bool nf = false;  // a NaN row or iterate fails every comparison: give up instead
-        // the iterate as scalar operands (lane j of the row layout holds y_j): the row scans then
-        // read only their rows from LDS
-        double ys[WNZ];
+    // the candidate weights of this lane's row slots, in registers once they exist
+    float wnr[WR];
 #pragma unroll
-        for (int j = 0; j < WNZ; j++) ys[j] = readlane_d(yi, j);
-        // every slot's row first (24 LDS reads in flight together; slot by slot, each slot's reads
-        // waited for the previous slot's arithmetic)
+    for (int s = 0; s < WR; s++) {
+        const int r = wave_owner_row(lane, s);
+        wnr[s] = have_wn ? ws.wn[r < nrows ? r : 0] : 0.0f;
+    }
+    for (;;) {
+        // every slot's row and the iterate (broadcast reads of sc.y) first: 32 LDS reads in flight
+        // together (slot by slot, each slot's reads waited for the previous slot's arithmetic; the
+        // iterate as 16 scalar operands took 32 readlanes and spilled scalar registers)
         double ts[WR];
         {
-            double rr[WR][WNZ];
+            double rr[WR][WNZ], yv[WNZ];
 #pragma unroll
             for (int s = 0; s < WR; s++)
 #pragma unroll
                 for (int j = 0; j < WNZ; j++) rr[s][j] = rw.g[s][j];
+#pragma unroll
+            for (int j = 0; j < WNZ; j++) yv[j] = sc.y[j];
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int s = 0; s < WR; s++) {
                 double s0 = 0.0, s1 = 0.0;
 #pragma unroll
                 for (int j = 0; j < WNZ; j += 2) {
-                    s0 = fma(rr[s][j], ys[j], s0);
-                    s1 = fma(rr[s][j + 1], ys[j + 1], s1);
+                    s0 = fma(rr[s][j], yv[j], s0);
+                    s1 = fma(rr[s][j + 1], yv[j + 1], s1);
                 }
                 ts[s] = s0 + s1;
             }
         }
+        // this lane's largest scaled violation (convergence) and its candidate: the eligible side
+        // with the largest normalised violation (lowest slot on ties)
+        double vb = -1.0, eb = -1.0;
+        int rb = 0, sdb = 1;
+        double bb = 0.0;
+        bool nf = false;  // a NaN row or iterate fails every comparison: give up instead
 #pragma unroll
         for (int s = 0; s < WR; s++) {
             const double t = ts[s];
@@ -276,28 +293,47 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
             const int r = wave_owner_row(lane, s);
             nf = nf || vl != vl || vu != vu;
             vb = fmax(vb, fmax(vl, vu));
-            const double w = have_wn ? (double)ws.wn[r < nrows ? r : 0] : 0.0;
-            const double el = have_wn ? (vl > add_tol ? al * w : -1.0) : vl;
-            const double eu = have_wn ? (vu > add_tol ? au * w : -1.0) : vu;
-            if (el > eb) eb = el, rb = r, sdb = 0, bb = rw.lo[s];
-            if (eu > eb) eb = eu, rb = r, sdb = 1, bb = rw.hi[s];
+            const double w = (double)wnr[s];
+            const double el = vl > add_tol ? al * w : -1.0;
+            const double eu = vu > add_tol ? au * w : -1.0;
+            const bool tl = el > eb;
+            eb = tl ? el : eb;
+            rb = tl ? r : rb;
+            sdb = tl ? 0 : sdb;
+            bb = tl ? rw.lo[s] : bb;
+            const bool tu = eu > eb;
+            eb = tu ? eu : eb;
+            rb = tu ? r : rb;
+            sdb = tu ? 1 : sdb;
+            bb = tu ? rw.hi[s] : bb;
         }
         if (__ballot(nf) != 0ull) return 0;
-        m = vb;
-        double em = eb;
-        wave_reduce2<Op::Max, Op::Max>(m, em);
         WSTAMP(steps == 0 ? 2 : 8, steps <= 1);
-        if (!(m > add_tol)) break;
+        // converged: no side violated beyond add_tol (m = the scaled primal residual, reduced once)
+        if (__ballot(vb > add_tol) == 0ull) {
+            m = grp_max<64>(vb);
+            break;
+        }
         if (!have_wn) {  // first violation: form the weights and scan again
             row_weights();
             have_wn = true;
+#pragma unroll
+            for (int s = 0; s < WR; s++) {
+                const int r = wave_owner_row(lane, s);
+                wnr[s] = ws.wn[r < nrows ? r : 0];
+            }
             continue;
         }
         if (steps >= maxstep) return 0;
-        const int owner = __ffsll((long long)__ballot(eb == em)) - 1;
-        const int rp = __shfl(rb, owner, 64);
-        const double sp = __shfl(sdb, owner, 64) ? 1.0 : -1.0;
-        const double bp = __shfl(bb, owner, 64);
+        // the candidate: the largest normalised violation as a float bit pattern (a violated side's
+        // is positive: at least 1), its lowest lane on ties
+        const unsigned key = eb > 0.0 ? max(__float_as_uint((float)eb), 1u) : 0u;
+        const unsigned kmax = (unsigned)__builtin_amdgcn_readfirstlane((int)wave_max_u32(key));
+        const int owner = __ffsll((long long)__ballot(key == kmax)) - 1;
+        if (owner < 0) return 0;
+        const int rp = __builtin_amdgcn_readlane(rb, owner);
+        const double sp = __builtin_amdgcn_readlane(sdb, owner) ? 1.0 : -1.0;
+        const double bp = readlane_d(bb, owner);
         const double* gp = Gs + rp * WNZ;
         // the candidate's P^-1 g on the row layout, published
         const double wi = rowdot17(ws.Pi, i, gp);

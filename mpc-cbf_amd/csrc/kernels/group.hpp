@@ -65,6 +65,31 @@ __device__ __forceinline__ void row_pair(double v, double& a, double& b) {
     }
 }
 
+// 64-lane max of a 32-bit unsigned key (every lane ends with it): DPP row stages folded into
+// v_max_u32, then the permlane16 / permlane32 swaps across the 16-lane rows. The candidate rule's
+// normalised violations are non-negative and reduced as float bit patterns (a violated side has a
+// positive score; the key is 0 when no side is violated), a third of the instructions of the f64
+// max (no NaN canonicalisation, one register instead of two).
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_u32(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
+    v = max(v, dpp_u32<DPP_XOR1>(v));
+    v = max(v, dpp_u32<DPP_XOR2>(v));
+    v = max(v, dpp_u32<DPP_HALF_MIRROR>(v));
+    v = max(v, dpp_u32<DPP_MIRROR>(v));
+    {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = max(r[0], r[1]);
+    }
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        v = max(r[0], r[1]);
+    }
+    return v;
+}
+
 enum class Op { Sum, Max, Min };
 
 template <Op OP>

@@ -93,6 +93,61 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     // are formed (v * 0 is NaN for a non-finite v): the rows that persist across the IMPC
     // iterations (q, box-row bounds, Voronoi rows) and each iteration's FoV rows
     bool nfin_fixed = false;
+    // The setup's state-independent operator loads — the box rows' shift coefficients, bounds,
+    // weights and the first BOXB image entries per lane, P and P^-1, the FoV rows' per-sample
+    // operators, the first pass of constant rows — are issued in one batch with the linear term's,
+    // so the whole batch is one round trip; issued block by block, each waited for the one before
+    // (six round trips ahead of the first solve).
+    constexpr int BOXB = 18;
+    constexpr int NE = WNZ * WNZ / 64;
+    constexpr int NL = (MAX_CBF_H * (3 * 15 + 18 + 6) + 63) / 64;
+    const int mb = op.m;
+    const int ng = mb * WNZ;
+    const double* W = opp(buf, op.o_Wbox);
+    const double* wb = opp(buf, op.o_wbox);
+    const int n1 = op.cbf_h * 3 * NZ, n2 = op.cbf_h * 18, n3 = op.cbf_h * 6;
+    const double* s1 = opp(buf, op.o_UZ);
+    const double* s2 = opp(buf, op.o_US);
+    const double* s3 = opp(buf, op.o_wfov);
+    const bool has_c = op.mc > 0;
+    const double* Cs = has_c ? opp(buf, op.o_Cs) : buf;
+    const double* clo = has_c ? opp(buf, op.o_clo) : buf;
+    const double* chi = has_c ? opp(buf, op.o_chi) : buf;
+    double bt[WR][8], bw[WR], bv[BOXB], pi[NE], pp[NE], fo[NL], cr[8];
+    {
+#pragma unroll
+        for (int sl = 0; sl < WR; sl++) {
+            const int r = lane + 64 * sl;
+            const double* src = W + (size_t)(r < mb ? r : 0) * WBOX_ROW + WNZ;
+#pragma unroll
+            for (int k = 0; k < 8; k++) bt[sl][k] = src[k];
+            bw[sl] = wb[r < mb ? r : 0];
+        }
+#pragma unroll
+        for (int b = 0; b < BOXB; b++) {
+            const int f = 64 * b + lane;
+            const int fc = f < ng ? f : 0;
+            bv[b] = W[(size_t)(fc / WNZ) * WBOX_ROW + fc % WNZ];
+        }
+        const double* P16 = opp(buf, op.o_P16);
+        const double* Pi16 = opp(buf, op.o_Pinv16);
+#pragma unroll
+        for (int k = 0; k < NE; k++) {
+            pi[k] = Pi16[lane + 64 * k];
+            pp[k] = P16[lane + 64 * k];
+        }
+#pragma unroll
+        for (int b = 0; b < NL; b++) {
+            const int f = lane + 64 * b;
+            const double* src = f < n1 ? s1 + f : (f < n1 + n2 ? s2 + (f - n1) : s3 + (f < n1 + n2 + n3 ? f - n1 - n2 : 0));
+            fo[b] = *src;
+        }
+        const int ci = lane < op.mc ? lane : 0;
+#pragma unroll
+        for (int k = 0; k < 6; k++) cr[k] = Cs[ci * 6 + k];
+        cr[6] = clo[ci];
+        cr[7] = chi[ci];
+    }
     {
         double kconst0;
         const double q = agent_linear_term_lanes<NZ, 64>(op, buf, args, ai, s0, lane, kconst0);
@@ -105,27 +160,15 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     }
 
     // ---- shared box rows into the image (rows 0 .. mb-1), bounds shifted by Gs s0
-    const int mb = op.m;
     if (grid_mode) gq_slots<64>(args, gq, lane);
     {
-        const double* W = opp(buf, op.o_Wbox);
-        const double* wb = opp(buf, op.o_wbox);
-        // each row's shift coefficients and bounds (rows lane, lane + 64, lane + 128), then the
-        // rows' coefficients in the image layout, BOXB per lane at a time: the loads' indices are
-        // clamped instead of guarded, so they are in flight together (guarded, one row slot's loads
-        // waited for the previous slot's)
-        double bt[WR][8], bw[WR];
 #pragma unroll
-        for (int sl = 0; sl < WR; sl++) {
-            const int r = lane + 64 * sl;
-            const double* src = W + (size_t)(r < mb ? r : 0) * WBOX_ROW + WNZ;
-#pragma unroll
-            for (int k = 0; k < 8; k++) bt[sl][k] = src[k];
-            bw[sl] = wb[r < mb ? r : 0];
+        for (int b = 0; b < BOXB; b++) {
+            const int f = 64 * b + lane;
+            if (f < ng) Gimg[f] = bv[b];
         }
-        constexpr int BOXB = 18;
-        const int ng = mb * WNZ;
-        for (int f0 = 0; f0 < ng; f0 += 64 * BOXB) {
+        // (more than 64 BOXB entries: the rest as before, BOXB per lane at a time, indices clamped)
+        for (int f0 = 64 * BOXB; f0 < ng; f0 += 64 * BOXB) {
             double v[BOXB];
 #pragma unroll
             for (int b = 0; b < BOXB; b++) {
@@ -157,29 +200,32 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     if (grid_mode) gq_states<64>(args, gq, lane);
     if (lane < WNZ) Gimg[WROWS * WNZ + lane] = 0.0;
     zero_row = &Gimg[WROWS * WNZ];
-    const bool infeasible = constant_rows_infeasible<64>(op, buf, s0, lane);
-    das_load_operators<!SLACK>(was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16), lane);
+    // constant rows (constant_rows_infeasible; the first 64 from the batch)
+    bool infeasible;
     {
-        // (one batch of clamped loads over the three arrays, then the stores)
-        const int n1 = op.cbf_h * 3 * NZ, n2 = op.cbf_h * 18, n3 = op.cbf_h * 6;
-        const double* s1 = opp(buf, op.o_UZ);
-        const double* s2 = opp(buf, op.o_US);
-        const double* s3 = opp(buf, op.o_wfov);
-        constexpr int NL = (MAX_CBF_H * (3 * 15 + 18 + 6) + 63) / 64;
-        double v[NL];
+        bool bad = false;
+        if (lane < op.mc) {
+            double v = 0.0;
 #pragma unroll
-        for (int b = 0; b < NL; b++) {
-            const int f = lane + 64 * b;
-            const double* src = f < n1 ? s1 + f : (f < n1 + n2 ? s2 + (f - n1) : s3 + (f < n1 + n2 + n3 ? f - n1 - n2 : 0));
-            v[b] = *src;
+            for (int k = 0; k < 6; k++) v = fma(cr[k], s0[k], v);
+            bad = (v < cr[6] - op.feas_tol) | (v > cr[7] + op.feas_tol);
         }
+        for (int i = lane + 64; i < op.mc; i += 64) {
+            const double lo = clo[i], hi = chi[i];
+            double v = 0.0;
 #pragma unroll
-        for (int b = 0; b < NL; b++) {
-            const int f = lane + 64 * b;
-            if (f < n1) uz_s[f] = v[b];
-            else if (f < n1 + n2) us_s[f - n1] = v[b];
-            else if (f < n1 + n2 + n3) mf_s[f - n1 - n2] = v[b];
+            for (int k = 0; k < 6; k++) v = fma(Cs[i * 6 + k], s0[k], v);
+            bad = bad | (v < lo - op.feas_tol) | (v > hi + op.feas_tol);
         }
+        infeasible = __ballot(bad) != 0ull;
+    }
+    das_store_operators(was, pi, pp, lane);
+#pragma unroll
+    for (int b = 0; b < NL; b++) {
+        const int f = lane + 64 * b;
+        if (f < n1) uz_s[f] = fo[b];
+        else if (f < n1 + n2) us_s[f - n1] = fo[b];
+        else if (f < n1 + n2 + n3) mf_s[f - n1 - n2] = fo[b];
     }
     stamp(args, ai, lane, 1);
 

@@ -268,20 +268,21 @@ class Context:
                   status=None, obj=None, iters=None, status_log=None, iters_log=None,
                   timing=False, comm=None, reserve_steps=0, solve_stride=1, step_timing=True,
                   stream=None, traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0,
-                  cov=None, kernel_clock=None):
+                  cov=None, kernel_clock=None, stamps=None):
         """Closed-loop control steps on the device (mpccbf_run_steps). Returns a dict with the
         table holding the final states ('final', a tensor) and, with timing=True, per-step
         device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms). kernel_clock: a
         (num_steps, W, 2) device tensor (torch.int64, W >= launch_waves(num_agents)) for every
         wave's start / end of every IMPC launch (s_memrealtime, 100 MHz ticks; zero: no wave);
-        kernel_clock_us() turns it into per-launch durations."""
+        kernel_clock_us() turns it into per-launch durations. stamps: the diagnostics builds' phase
+        stamps (as impc_solve; every step overwrites them)."""
         if num_agents is None:
             num_agents = states.shape[0] - agent_first
         b = Batch(num_states=states.shape[0], states=_ptr(states), agent_first=agent_first,
                   num_agents=num_agents, targets=_ptr(targets), refs=_ptr(refs),
                   nb_row_ptr=_ptr(nb_row_ptr), nb_col=_ptr(nb_col), x=_ptr(x),
                   status=_ptr(status), obj=_ptr(obj), iters=_ptr(iters), next_states=None,
-                  knn_k=int(knn_k), knn_radius=float(knn_radius), stamps=None,
+                  knn_k=int(knn_k), knn_radius=float(knn_radius), stamps=_ptr(stamps),
                   traj_t=_ptr(traj_t), pos_std=float(pos_std), vel_std=float(vel_std),
                   noise_seed=int(noise_seed), step_index=int(step_index), cov=_ptr(cov))
         step_ms = np.zeros(max(num_steps, 1), dtype=np.float32) if timing and step_timing else None
