@@ -55,9 +55,10 @@ constexpr double kFeasTol = 1e-6;  // CPLEX default feasibility tolerance (CPLEX
 // reduce-kernel statuses beyond qpcpp::SolveStatus: -1 = the PDIP solves it; capacity errors
 constexpr int RS_SOLVE = -1, RS_CAP_NZ = -2, RS_CAP_ROWS = -3;
 
-// Packed QP (host -> device). Integers: [n, me, mi, nh | H index (i n + j) x nh | eq row ptr
-// (me + 1) | eq cols | in row ptr (mi + 1) | in cols]. Doubles: [c (n) | c0 | H values (nh) | eq rhs
-// (me) | eq values | in lo (mi) | in hi (mi) | in values]. Row pointers are relative to the QP.
+// Packed QP (host -> device; dense_pack.hpp pack_qp). Int words: [n, me, mi, nh | in row ptr
+// (mi + 1, int32) | eq row ptr (me + 1, u16) | Hs index (i << 6 | j, i <= j; nh, u16) | eq cols
+// (u8) | in cols (u8)]. Doubles: [c (n) | c0 | Hs values (nh) | eq rhs (me) | eq values | in lo (mi)
+// | in hi (mi) | in values]. Row pointers are relative to the QP; Hs = (H + H^T) / 2.
 struct DenseBatch {
     const double* dbl;
     const int32_t* ints;
@@ -153,11 +154,11 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         ib = si;
     }
     const int n = ib[0], me = ib[1], mi = ib[2], nh = ib[3];
-    const int32_t* hidx = ib + 4;
-    const int32_t* eptr = hidx + nh;
-    const int32_t* ecol = eptr + me + 1;
-    const int32_t* iptr = ecol + eptr[me];
-    const int32_t* icol = iptr + mi + 1;
+    const int32_t* iptr = ib + 4;
+    const uint16_t* eptr = (const uint16_t*)(iptr + mi + 1);
+    const uint16_t* hidx = eptr + me + 1;
+    const uint8_t* ecol = (const uint8_t*)(hidx + nh);
+    const uint8_t* icol = ecol + eptr[me];
     const double* c = db;
     const double* hval = db + n + 1;
     const double* erhs = hval + nh;
@@ -269,17 +270,17 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         for (int k = eptr[l]; k < eptr[l + 1]; k++) v = fma(eval[k], s.xp[ecol[k]], v);
         if (fabs(v - erhs[l]) > kFeasTol) eq_infeasible = true;
     }
-    // ---- Hs Z and Hs xp, Hs = (H + H^T) / 2: H's nonzeros scattered into a dense n x n image in
-    // LDS (E^T's space, free from here; each entry written once, so no atomics), then lane l forms
-    // row l over j = 0 .. n-1 — a fixed summation order (no dependence on how the hardware orders
-    // LDS atomics), and no lane walks the whole nonzero list (that serial scan of global loads and
-    // divisions cost ~1.7 ms per 4096-QP call)
+    // ---- Hs Z and Hs xp, Hs = (H + H^T) / 2: the packed upper triangle's nonzeros scattered into
+    // a dense n x n image in LDS (E^T's space, free from here; each entry written once, so no
+    // atomics), then lane l forms row l over j = 0 .. n-1 (entry (min, max) of the image) — a fixed
+    // summation order (no dependence on how the hardware orders LDS atomics), and no lane walks the
+    // whole nonzero list (that serial scan of global loads and divisions cost ~1.7 ms per 4096-QP
+    // call)
     for (int e = l; e < n * LDS_S; e += 64) et[e] = 0.0;
     __syncthreads();
     for (int e = l; e < nh; e += 64) {
         const int k = hidx[e];
-        const int i = k / n, j = k - i * n;
-        et[i * LDS_S + j] = hval[e];
+        et[(k >> 6) * LDS_S + (k & 63)] = hval[e];
     }
     __syncthreads();
     if (l < n) {
@@ -287,7 +288,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
 #pragma unroll
         for (int b = 0; b < DENSE_NZ; b++) hzl[b] = 0.0;
         for (int j = 0; j < n; j++) {
-            const double hv = 0.5 * (et[l * LDS_S + j] + et[j * LDS_S + l]);
+            const double hv = l <= j ? et[l * LDS_S + j] : et[j * LDS_S + l];
             hxl = fma(hv, s.xp[j], hxl);
 #pragma unroll
             for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[j * DENSE_NZ + b], hzl[b]);
@@ -759,7 +760,8 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     for (int q0 = 0; q0 < count && e == hipSuccess; q0 += slice) {
         const int q1 = std::min(count, q0 + slice);
         parallel_for(q1 - q0, [&](int k0, int k1) {
-            for (int k = q0 + k0; k < q0 + k1; k++) pack_qp(qps[k], plan[k], h_d + off_d[k], h_i + off_i[k]);
+            for (int k = q0 + k0; k < q0 + k1; k++)
+                if (!plan[k].cap) pack_qp(qps[k], plan[k], h_d + off_d[k], h_i + off_i[k]);
         });
         a.first = q0;
         hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(q1 - q0), dim3(64), lds, s, a);

@@ -20,6 +20,13 @@ constexpr int DENSE_EMAX = 64;  // equalities per QP on the device elimination
 
 inline bool finite_bound(double v) { return std::isfinite(v) && std::fabs(v) < kInf; }
 
+// Hs = (H + H^T) / 2, the only part of H the objective sees: entry (i, j), formed as the device
+// formed it from the full H before the packed form carried one triangle (bit-identical: the sum
+// commutes)
+inline double hs_entry(const double* H, int n, int i, int j) {
+    return 0.5 * (H[(size_t)i * n + j] + H[(size_t)j * n + i]);
+}
+
 // Host half: validation (the reference's invalid_argument cases: NULL pointers, n < 1, m < 0,
 // non-finite H / c, NaN bounds) and the row classification; sizes of the packed form.
 struct PackPlan {
@@ -43,13 +50,11 @@ inline PackPlan plan_qp(const mpccbf_dense_qp& qp) {
     pl.n = n;
     // branch-free scans (vectorised): a flag for a non-finite entry, the nonzero counts
     bool nonfin = false;
-    int nh = 0;
-    for (size_t k = 0; k < (size_t)n * n; k++) {
-        const double v = qp.H[k];
-        nh += v != 0.0;
-        nonfin |= !(std::fabs(v) <= DBL_MAX);
-    }
+    for (size_t k = 0; k < (size_t)n * n; k++) nonfin |= !(std::fabs(qp.H[k]) <= DBL_MAX);
     if (nonfin) return fail("dense QP: H has a non-finite entry");
+    int nh = 0;  // nonzeros of Hs = (H + H^T) / 2 on and above the diagonal (the packed half)
+    for (int i = 0; i < n; i++)
+        for (int j = i; j < n; j++) nh += hs_entry(qp.H, n, i, j) != 0.0;
     pl.nh = nh;
     for (int i = 0; i < n; i++) nonfin |= !(std::fabs(qp.c[i]) <= DBL_MAX);
     if (nonfin) return fail("dense QP: c has a non-finite entry");
@@ -81,22 +86,27 @@ inline PackPlan plan_qp(const mpccbf_dense_qp& qp) {
         }
     }
     pl.cap = n > DENSE_NMAX || pl.me > DENSE_EMAX;
-    pl.ni = 4 + (size_t)pl.nh + (pl.me + 1) + pl.enz + (pl.mi + 1) + pl.inz;
+    if (pl.cap) return pl;  // (reduced on the host: not packed)
+    // int32 words: header, inequality row pointers, then the u16 / u8 arrays (pack_qp)
+    pl.ni = 4 + (size_t)(pl.mi + 1) + (2 * (size_t)(pl.me + 1) + 2 * (size_t)pl.nh + pl.enz + pl.inz + 3) / 4;
     pl.nd = (size_t)n + 1 + pl.nh + pl.me + pl.enz + 2 * (size_t)pl.mi + pl.inz;
     return pl;
 }
 
-// Writes one QP's packed form. Branch-free compaction (each entry written, the cursor advanced by
-// its nonzero flag): a section's cursor may write one entry past its end, so the equality rows are
-// packed before the first inequality entry and each section's leading words after the section
-// before it, and the caller leaves one spare double and int after the QP.
+// Writes one QP's packed form (within capacity: n, me <= 64). Layout, int words: [n, me, mi, nh |
+// in row ptr (mi + 1, int32) | eq row ptr (me + 1, u16) | Hs index (i << 6 | j, i <= j; nh, u16)
+// | eq cols (u8) | in cols (u8)]; doubles: [c (n) | c0 | Hs values (nh) | eq rhs (me) | eq values |
+// in lo (mi) | in hi (mi) | in values]. Branch-free compaction (each entry written, the cursor
+// advanced by its nonzero flag): a section's cursor may write one entry past its end, into a later
+// section, so the sections are packed in memory order (Hs, equality rows, inequality rows) and the
+// caller leaves one spare double and int after the QP.
 inline void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, int32_t* ib) {
     const int n = qp.n;
-    int32_t* hidx = ib + 4;
-    int32_t* eptr = hidx + pl.nh;
-    int32_t* ecol = eptr + pl.me + 1;
-    int32_t* iptr = ecol + pl.enz;
-    int32_t* icol = iptr + pl.mi + 1;
+    int32_t* iptr = ib + 4;
+    uint16_t* eptr = (uint16_t*)(iptr + pl.mi + 1);
+    uint16_t* hidx = eptr + pl.me + 1;
+    uint8_t* ecol = (uint8_t*)(hidx + pl.nh);
+    uint8_t* icol = ecol + pl.enz;
     double* c = db;
     double* hval = db + n + 1;
     double* erhs = hval + pl.nh;
@@ -105,22 +115,23 @@ inline void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, i
     double* ihi = ilo + pl.mi;
     double* ivalv = ihi + pl.mi;
     int h = 0;
-    for (int k = 0; k < n * n; k++) {
-        const double v = qp.H[k];
-        hidx[h] = k;
-        hval[h] = v;
-        h += v != 0.0;
-    }
+    for (int i = 0; i < n; i++)
+        for (int j = i; j < n; j++) {
+            const double v = hs_entry(qp.H, n, i, j);
+            hidx[h] = (uint16_t)(i << 6 | j);
+            hval[h] = v;
+            h += v != 0.0;
+        }
     ib[0] = n;
     ib[1] = pl.me;
     ib[2] = pl.mi;
     ib[3] = pl.nh;
     std::memcpy(c, qp.c, (size_t)n * sizeof(double));
     db[n] = qp.c0;
-    auto row = [&](const double* a, int32_t* col, double* val, int z) {
+    auto row = [&](const double* a, uint8_t* col, double* val, int z) {
         for (int j = 0; j < n; j++) {
             const double v = a[j];
-            col[z] = j;
+            col[z] = (uint8_t)j;
             val[z] = v;
             z += v != 0.0;
         }
@@ -134,15 +145,15 @@ inline void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, i
         if (!(finite_bound(lo) && lo == hi)) continue;
         ez = row(qp.A + (size_t)k * n, ecol, evalv, ez);
         erhs[e] = lo;
-        eptr[++e] = ez;
+        eptr[++e] = (uint16_t)ez;
     }
     for (int i = 0; i < n; i++) {
         const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
         if (!(finite_bound(lo) && lo == hi)) continue;
-        ecol[ez] = i;
+        ecol[ez] = (uint8_t)i;
         evalv[ez++] = 1.0;
         erhs[e] = lo;
-        eptr[++e] = ez;
+        eptr[++e] = (uint16_t)ez;
     }
     // inequality rows (a finite side, then variable bounds as unit rows)
     iptr[0] = 0;
@@ -158,7 +169,7 @@ inline void pack_qp(const mpccbf_dense_qp& qp, const PackPlan& pl, double* db, i
     for (int i = 0; i < n; i++) {
         const double lo = qp.vlo ? qp.vlo[i] : -kInf, hi = qp.vhi ? qp.vhi[i] : kInf;
         if ((finite_bound(lo) && lo == hi) || !(finite_bound(lo) || finite_bound(hi))) continue;
-        icol[rz] = i;
+        icol[rz] = (uint8_t)i;
         ivalv[rz++] = 1.0;
         ilo[r] = lo;
         ihi[r] = hi;
