@@ -20,6 +20,7 @@
 #include "host/operators.hpp"
 #include "kernels/impc.hpp"
 #include "kernels/cbf_control.hpp"
+#include "kernels/fov_cbf.hpp"
 
 namespace mpccbf {
 
@@ -374,6 +375,12 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
     d.cbf_mode = p->cbf_mode;
     d.C = p->num_control_points;
     d.fov_beta = p->fov_beta;
+    {
+        const dev::FovBorder fb = dev::fov_border(p->fov_beta);
+        d.fov_kap = fb.kap;
+        d.fov_sig = fb.sig_left;
+        d.fov_none = fb.none ? 1 : 0;
+    }
     d.fov_Ds = p->fov_Ds;
     d.fov_Rs = p->fov_Rs;
     for (int k = 0; k < 3; k++) d.bbox[k] = p->bbox[k];

@@ -17,7 +17,7 @@ struct FovBorder {
     bool none;
 };
 
-__device__ __forceinline__ FovBorder fov_border(double fov) {
+__host__ __device__ inline FovBorder fov_border(double fov) {
     if (fov < M_PI) return FovBorder{tan(0.5 * fov), 1.0, false};
     if (fov == M_PI) return FovBorder{1.0, 0.0, false};
     if (fabs(fov - 2.0 * M_PI) <= 1e-9 * 2.0 * M_PI) return FovBorder{0.0, 0.0, true};

@@ -29,6 +29,8 @@ struct DevOps {
     // Cholesky factor padded to 16 x 16 with the identity
     int32_t cbf_mode, C;
     double fov_beta, fov_Ds, fov_Rs, bbox[3];
+    double fov_kap, fov_sig;  // fov_border(fov_beta), formed on the host (a device tan per agent
+    int32_t fov_none;         // was ~0.4 us on the FoV kernel's chain)
     int32_t o_VZ, o_VS, o_Wbox, o_P16, o_LP16;
     int32_t o_Pinv16;  // FoV: P^-1 padded to 16 x 16 (dual active-set solve)
     int32_t o_wbox;    // FoV: box rows' candidate weights 1 / sqrt(g P^-1 g) (dual active-set solve)

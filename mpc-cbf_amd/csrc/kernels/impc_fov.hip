@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
     const int C = op.C;
-    const FovBorder fborder = fov_border(op.fov_beta);  // (once per agent, not per row)
+    const FovBorder fborder{op.fov_kap, op.fov_sig, op.fov_none != 0};  // (fov_border, host)
 
     for (int it = 0; it < op.impc_iter; it++) {
         // (keeps the operator tables' loads inside the iteration: hoisted out of it they stay live
