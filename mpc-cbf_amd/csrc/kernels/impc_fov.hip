@@ -23,6 +23,21 @@ namespace dev {
 
 constexpr int FOV_NB_CAP = 16;  // observed neighbours per agent
 
+// Diagnostics build (make setupst): stamps 2 .. 6 mark points inside the setup (after the operator
+// loads' issue, the linear term, the box rows, the neighbour states, the constant rows) instead of
+// the later phases (tools/setup_stamps.py)
+#ifdef MPCCBF_SETUP_STAMPS
+#define SSTAMP(k) stamp(args, ai, lane, k)
+#define PSTAMP(k) \
+    do {          \
+    } while (0)
+#else
+#define SSTAMP(k) \
+    do {          \
+    } while (0)
+#define PSTAMP(k) stamp(args, ai, lane, k)
+#endif
+
 // LDS of the slack rows (slack mode only)
 struct FovSlackLds {
     double Go[WSL_ROWS * WNZ];
@@ -148,6 +163,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         cr[6] = clo[ci];
         cr[7] = chi[ci];
     }
+    SSTAMP(2);
     {
         double kconst0;
         const double q = agent_linear_term_lanes<NZ, 64>(op, buf, args, ai, s0, lane, kconst0);
@@ -159,6 +175,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         if (lane == 0) kconst_s = kconst0;
     }
 
+    SSTAMP(3);
     // ---- shared box rows into the image (rows 0 .. mb-1), bounds shifted by Gs s0
     if (grid_mode) gq_slots<64>(args, gq, lane);
     {
@@ -197,9 +214,11 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             }
         }
     }
+    SSTAMP(4);
     if (grid_mode) gq_states<64>(args, gq, lane);
     if (lane < WNZ) Gimg[WROWS * WNZ + lane] = 0.0;
     zero_row = &Gimg[WROWS * WNZ];
+    SSTAMP(5);
     // constant rows (constant_rows_infeasible; the first 64 from the batch)
     bool infeasible;
     {
@@ -219,6 +238,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         }
         infeasible = __ballot(bad) != 0ull;
     }
+    SSTAMP(6);
     das_store_operators(was, pi, pp, lane);
 #pragma unroll
     for (int b = 0; b < NL; b++) {
@@ -264,7 +284,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         if (lane < nnb) slk->w[lane] = op.slack_cost * pow(op.slack_decay, (double)slk->order[lane]);
         wave_lds_sync();
     }
-    stamp(args, ai, lane, 2);
+    PSTAMP(2);
 
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
@@ -445,7 +465,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         }
         if (lane < WNZ) sc.q[lane] = q_s[lane];
         wave_lds_sync();
-        if (it < 2) stamp(args, ai, lane, 3 + 2 * it);
+        if (it < 2) PSTAMP(3 + 2 * it);
         int st;
         int nit = 0;
         double prs = __builtin_nan(""), drs = __builtin_nan("");
@@ -753,7 +773,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             success = false;
         }
         write_iteration(args, oi, lane, st, objv, nit, prs, drs);
-        if (it < 2) stamp(args, ai, lane, 4 + 2 * it);
+        if (it < 2) PSTAMP(4 + 2 * it);
         wave_lds_sync();
     }
     {
