@@ -26,6 +26,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <condition_variable>
@@ -88,9 +90,13 @@ struct DenseBatch {
     // into LDS with one batch of loads: stage_d / stage_i words (the batch's largest QP; 0: direct)
     int32_t stage_d, stage_i;
     int32_t first;  // dense_reduce_kernel: the slice's first QP (block b reduces QP first + b)
+    long long* dstamps;  // profiling build: QP 0's reduction phase stamps (24 words), else NULL
 };
 
 namespace dev {
+
+// zero rows after the E^T image: the QR's row loops run in unguarded chunks of 8 rows
+constexpr int ET_PAD = 8;
 
 // E^T / H image in dynamic LDS, sized per batch: rows = the batch's largest n, row stride S = the
 // larger of its largest n and equality count, made odd (spread banks); at most 64 x 65 doubles
@@ -104,27 +110,60 @@ struct ReduceLds {
     double xp[DENSE_NMAX];
     double hz[DENSE_NMAX * DENSE_NZ];
     double hx[DENSE_NMAX];
-    double rdiag[DENSE_EMAX], beta[DENSE_EMAX], u[DENSE_EMAX], bp[DENSE_EMAX];
+    double rdiag[DENSE_EMAX], beta[DENSE_EMAX], bp[DENSE_EMAX];
     double P[DENSE_NZ * DENSE_NZ];
-    double L[DENSE_NZ * DENSE_NZ];
+    double Ps[DENSE_NZ * DENSE_NZ];  // symmetrised P (padding: identity), the Cholesky's input
     int32_t perm[DENSE_EMAX];
 };
 
 __device__ __forceinline__ bool fin_bound(double v) { return isfinite(v) && fabs(v) < kInf; }
 
+// sum over rows i = t .. n-1 of the image's columns ca and cb (row stride S) in row order, in
+// unguarded chunks of 8 rows (the rows past n are zero: the image's own zero rows and its ET_PAD
+// pad rows; their +0 terms leave the sum as the plain loop forms it), every chunk's loads first
+__device__ __forceinline__ double col_dot8(const double* __restrict__ et, int S, int t, int n, int ca, int cb) {
+    double acc = 0.0;
+    for (int i0 = t; i0 < n; i0 += 8) {
+        const double* r0 = et + i0 * S;
+        double x[8], y[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            x[u] = r0[u * S + ca];
+            y[u] = r0[u * S + cb];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc = fma(x[u], y[u], acc);
+    }
+    return acc;
+}
+
+
 __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     const int qi = a.first + (int)blockIdx.x;
     const int l = threadIdx.x;
     if (qi >= a.count || (a.hostred && a.hostred[qi])) return;  // (reduced on the host)
+    // profiling build (make prof): shader-clock stamps of the first QP's phases (dense_stamps)
+#ifdef MPCCBF_PDIP_STAMPS
+#define DSTAMP(k)                                                                                 \
+    do {                                                                                          \
+        if (a.dstamps && qi == 0 && l == 0) a.dstamps[k] = (long long)__builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define DSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+    DSTAMP(0);
     __shared__ ReduceLds s;
     extern __shared__ double et[];  // E^T: row i = variable, column c = equality (lane c)
     const int LDS_S = a.lds_stride, NROWS = a.lds_rows;
     const int32_t* ib = a.ints + a.off_i[qi];
     const double* db = a.dbl + a.off_d[qi];
+    DSTAMP(1);
     if (a.stage_d > 0) {
         // the QP's packed words into LDS (after the E^T image): every load issued before any store,
         // 8 per lane in flight, so the bus latency is paid a few times instead of once per read
-        double* sd = et + (size_t)NROWS * LDS_S;
+        double* sd = et + (size_t)(NROWS + ET_PAD) * LDS_S;
         int32_t* si = (int32_t*)(sd + a.stage_d);
         const int nd = (int)(a.off_d[qi + 1] - a.off_d[qi]), ni = (int)(a.off_i[qi + 1] - a.off_i[qi]);
         for (int e0 = 0; e0 < nd; e0 += 8 * 64) {
@@ -171,30 +210,34 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     // (decided only within capacity: beyond it the rows' reduced coefficients are not all formed)
     bool infeasible = false, eq_infeasible = false;
 
+    DSTAMP(2);
     // ---- E^T into LDS (lane c: equality c's row as column c), zero elsewhere
-    for (int e = l; e < NROWS * LDS_S; e += 64) et[e] = 0.0;
+    for (int e = l; e < (NROWS + ET_PAD) * LDS_S; e += 64) et[e] = 0.0;
     __syncthreads();
     if (l < me) {
         for (int k = eptr[l]; k < eptr[l + 1]; k++) et[ecol[k] * LDS_S + l] = eval[k];
         s.perm[l] = l;
     }
     __syncthreads();
+    DSTAMP(3);
     // ---- Householder QR with column pivoting: E^T Pi = Q R (reflection t stored in column t,
     // rows t .. n-1; R's diagonal in rdiag)
     const int tmax = n < me ? n : me;
     int rank = 0;
     double r00 = 0.0;
     for (int t = 0; t < tmax; t++) {
+        if (t == 10) DSTAMP(16);
         double nrm = -1.0;
         if (l >= t && l < me) {
-            nrm = 0.0;
-            for (int i = t; i < n; i++) nrm = fma(et[i * LDS_S + l], et[i * LDS_S + l], nrm);
+            nrm = col_dot8(et, LDS_S, t, n, l, l);
         }
+        if (t == 10) DSTAMP(11);
         const double best = grp_max<64>(nrm);
         const int p = __ffsll((long long)__ballot(nrm == best && l >= t && l < me)) - 1;
         const double sig = sqrt(best);
         if (t == 0) r00 = sig;
         if (!(sig > 1e-12 * r00) || p < 0) break;  // the remaining columns are dependent
+        if (t == 10) DSTAMP(12);
         // swap columns t and p (lane i: row i)
         if (p != t && l < n) {
             const double v = et[l * LDS_S + t];
@@ -207,6 +250,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
             s.perm[p] = q;
         }
         __syncthreads();
+        if (t == 10) DSTAMP(13);
         const double xt = et[t * LDS_S + t];
         const double alpha = xt >= 0.0 ? -sig : sig;
         const double vt = xt - alpha;
@@ -219,41 +263,67 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
             s.beta[t] = bt;
         }
         __syncthreads();
+        if (t == 10) DSTAMP(14);
         // apply to columns t+1 .. me-1 (lane c)
         if (l > t && l < me) {
-            double w = 0.0;
-            for (int i = t; i < n; i++) w = fma(et[i * LDS_S + t], et[i * LDS_S + l], w);
+            double w = col_dot8(et, LDS_S, t, n, t, l);
             w *= bt;
-            for (int i = t; i < n; i++) et[i * LDS_S + l] = fma(-w, et[i * LDS_S + t], et[i * LDS_S + l]);
+            // (8 rows' loads before their stores, the pad rows' zeros included: as a plain loop each
+            // row's store could alias the next row's loads for all the compiler knows, and every
+            // row waited for its own LDS round trip — two thirds of a reflection's time)
+            for (int i0 = t; i0 < n; i0 += 8) {
+                double* r0 = et + i0 * LDS_S;
+                double x[8], y[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    x[u] = r0[u * LDS_S + t];
+                    y[u] = r0[u * LDS_S + l];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) r0[u * LDS_S + l] = fma(-w, x[u], y[u]);
+            }
         }
         __syncthreads();
+        if (t == 10) DSTAMP(15);
         rank = t + 1;
     }
     const int nz = n - rank;
+    DSTAMP(4);
     // ---- particular solution: R11^T u = (Pi^T b)_{1..r}, xp = Q [u; 0]  (minimum norm)
+    // (column-oriented: lane j holds b_j and takes R[t][j] u_t off it once u_t is known, u_t from
+    // lane t by readlane — no reduction and no barrier per step)
     if (l < me) s.bp[l] = erhs[s.perm[l]];
     __syncthreads();
-    for (int t = 0; t < rank; t++) {
-        const double part = (l < t) ? et[l * LDS_S + t] * s.u[l] : 0.0;  // R[l][t] u_l, l < t
-        const double sum = grp_sum<64>(part);
-        if (l == 0) s.u[t] = (s.bp[t] - sum) / s.rdiag[t];
-        __syncthreads();
+    double ul = 0.0;
+    {
+        double bl = l < rank ? s.bp[l] : 0.0;
+        const double rdl = l < rank ? s.rdiag[l] : 1.0;
+        for (int t = 0; t < rank; t++) {
+            const double rt = l < rank ? et[t * LDS_S + l] : 0.0;  // R[t][l] (row t of R, lanes l > t)
+            const double ut = readlane_d(bl / rdl, t);
+            ul = l == t ? ut : ul;
+            bl = l > t ? fma(-rt, ut, bl) : bl;
+        }
     }
+    DSTAMP(5);
     // reflections applied to the vectors [u; 0] and e_{r+j} (lane i: component i)
-    double w = (l < rank) ? s.u[l] : 0.0;
+    double w = (l < rank) ? ul : 0.0;
     double zc[DENSE_NZ];
 #pragma unroll
     for (int j = 0; j < DENSE_NZ; j++) zc[j] = (l == rank + j && j < nz) ? 1.0 : 0.0;
     for (int t = rank - 1; t >= 0; t--) {
         const double vi = (l >= t && l < n) ? et[l * LDS_S + t] : 0.0;
         const double bt = s.beta[t];
-        double d = grp_sum<64>(vi * w);
-        w = fma(-bt * d, vi, w);
+        // the nine reflection coefficients reduced together, stage-major (each value's reduction
+        // tree is grp_sum's: bit-identical; one after the other, each waited for its DPP chain)
+        double d[DENSE_NZ + 1];
+        d[0] = vi * w;
 #pragma unroll
-        for (int j = 0; j < DENSE_NZ; j++) {
-            d = grp_sum<64>(vi * zc[j]);
-            zc[j] = fma(-bt * d, vi, zc[j]);
-        }
+        for (int j = 0; j < DENSE_NZ; j++) d[1 + j] = vi * zc[j];
+        grp_sum_vec<64, DENSE_NZ + 1>(d);
+        w = fma(-bt * d[0], vi, w);
+#pragma unroll
+        for (int j = 0; j < DENSE_NZ; j++) zc[j] = fma(-bt * d[1 + j], vi, zc[j]);
     }
     if (l < DENSE_NMAX) {
         s.xp[l] = l < n ? w : 0.0;
@@ -270,6 +340,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         for (int k = eptr[l]; k < eptr[l + 1]; k++) v = fma(eval[k], s.xp[ecol[k]], v);
         if (fabs(v - erhs[l]) > kFeasTol) eq_infeasible = true;
     }
+    DSTAMP(6);
     // ---- Hs Z and Hs xp, Hs = (H + H^T) / 2: the packed upper triangle's nonzeros scattered into
     // a dense n x n image in LDS (E^T's space, free from here; each entry written once, so no
     // atomics), then lane l forms row l over j = 0 .. n-1 (entry (min, max) of the image) — a fixed
@@ -313,6 +384,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         const bool in = pa < nz && pb < nz;
         const double v = in ? 0.5 * (s.P[pa * DENSE_NZ + pb] + s.P[pb * DENSE_NZ + pa]) : (pa == pb ? 1.0 : 0.0);
         red[l] = v;  // P (padding: identity)
+        s.Ps[l] = v;  // (the Cholesky's copy)
         pmax = in ? fabs(v) : 0.0;
     }
     pmax = grp_max<64>(pmax);
@@ -327,26 +399,42 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     // k0 + q^T y + 1/2 y^T P y: the full-space objective at x = xp + Z y)
     const double k0 = db[n] + grp_sum<64>(l < n ? s.xp[l] * (s.hx[l] + c[l]) : 0.0);
     // Cholesky of P (lane 0, in LDS; nz <= 8): the PDIP's start factor when P is positive definite
+    DSTAMP(7);
     int pd = 0;
     if (l == 0 && nz <= DENSE_NZ) {
-        double* L = s.L;
+        // in registers (unrolled over the padded 8 x 8, guarded by nz) from the LDS copy of P: the
+        // loop over LDS read P back from global memory and kept L in LDS, one round trip per entry
+        double Pm[DENSE_NZ * DENSE_NZ], L[DENSE_NZ * DENSE_NZ];
+#pragma unroll
+        for (int j = 0; j < DENSE_NZ * DENSE_NZ; j++) {
+            Pm[j] = s.Ps[j];
+            L[j] = 0.0;
+        }
         bool ok = nz > 0;
-        for (int j = 0; j < DENSE_NZ * DENSE_NZ; j++) L[j] = 0.0;
-        for (int j = 0; j < nz && ok; j++) {
-            double d = red[j * DENSE_NZ + j];
-            for (int k = 0; k < j; k++) d -= L[j * DENSE_NZ + k] * L[j * DENSE_NZ + k];
-            if (!(d > 0.0)) {
-                ok = false;
-                break;
-            }
-            const double ljj = sqrt(d);
-            L[j * DENSE_NZ + j] = ljj;
-            for (int i = j + 1; i < nz; i++) {
-                double v = red[i * DENSE_NZ + j];
-                for (int k = 0; k < j; k++) v -= L[i * DENSE_NZ + k] * L[j * DENSE_NZ + k];
-                L[i * DENSE_NZ + j] = v / ljj;
+#pragma unroll
+        for (int j = 0; j < DENSE_NZ; j++) {
+            if (j < nz && ok) {
+                double d = Pm[j * DENSE_NZ + j];
+#pragma unroll
+                for (int k = 0; k < j; k++) d -= L[j * DENSE_NZ + k] * L[j * DENSE_NZ + k];
+                if (!(d > 0.0)) {
+                    ok = false;
+                } else {
+                    const double ljj = sqrt(d);
+                    L[j * DENSE_NZ + j] = ljj;
+#pragma unroll
+                    for (int i = j + 1; i < DENSE_NZ; i++) {
+                        if (i < nz) {
+                            double v = Pm[i * DENSE_NZ + j];
+#pragma unroll
+                            for (int k = 0; k < j; k++) v -= L[i * DENSE_NZ + k] * L[j * DENSE_NZ + k];
+                            L[i * DENSE_NZ + j] = v / ljj;
+                        }
+                    }
+                }
             }
         }
+#pragma unroll
         for (int j = 0; j < DENSE_NZ * DENSE_NZ; j++) {
             const int r = j / DENSE_NZ, cc = j % DENSE_NZ;
             red[DENSE_NZ * DENSE_NZ + j] = (ok && r < nz) ? L[j] : (r == cc ? 1.0 : 0.0);  // padding: identity
@@ -355,6 +443,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 1] = k0;
         pd = ok ? 1 : 0;
     }
+    DSTAMP(8);
     // ---- inequality rows in y: g = Z^T a, bounds shifted by a^T xp; constant rows decided here
     int cnt = 0;
     double* rows = red + DQ_HDR;
@@ -399,6 +488,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     }
     infeasible = __ballot(infeasible) != 0ull;
     eq_infeasible = __ballot(eq_infeasible) != 0ull;
+    DSTAMP(9);
     // ---- expansion data and the decision
     double* zx = a.zx + (size_t)qi * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX);
     for (int e = l; e < DENSE_NMAX * DENSE_NZ; e += 64) zx[e] = s.z[e];
@@ -415,7 +505,9 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         a.m[qi] = cnt < DENSE_ROWS ? cnt : DENSE_ROWS;
         a.pd[qi] = pd;
     }
+    DSTAMP(10);
 }
+#undef DSTAMP
 
 template <int NZ, int R>
 __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
@@ -745,9 +837,20 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     a.feas_tol = 1e-6;
     a.lds_rows = nmax;
     a.lds_stride = dev::reduce_stride(nmax, emax);
-    size_t lds = (size_t)a.lds_rows * a.lds_stride * sizeof(double);
+    size_t lds = (size_t)(a.lds_rows + dev::ET_PAD) * a.lds_stride * sizeof(double);
     const size_t stage = (size_t)sd_max * sizeof(double) + (size_t)si_max * sizeof(int32_t);
     a.stage_d = a.stage_i = 0;
+    a.dstamps = nullptr;
+#ifdef MPCCBF_PDIP_STAMPS
+    // profiling build: QP 0's reduction phases, printed to stderr with MPCCBF_DENSE_STAMPS=1
+    static long long* d_stamps = nullptr;
+    const bool want_stamps = std::getenv("MPCCBF_DENSE_STAMPS") != nullptr;
+    if (want_stamps && !d_stamps && hipMalloc(&d_stamps, 24 * sizeof(long long)) != hipSuccess) d_stamps = nullptr;
+    if (want_stamps && d_stamps) {
+        (void)hipMemset(d_stamps, 0, 24 * sizeof(long long));
+        a.dstamps = d_stamps;
+    }
+#endif
     if (lds + stage <= 48 * 1024) {  // (beyond: the kernel reads its QP over the bus where it uses it)
         a.stage_d = sd_max;
         a.stage_i = si_max;
@@ -826,6 +929,18 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         e = hipMemcpyAsync(&yb[b * DENSE_NZ], a.y + (size_t)big[b] * DENSE_NZ, DENSE_NZ * sizeof(double),
                            hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+#ifdef MPCCBF_PDIP_STAMPS
+    if (a.dstamps && e == hipSuccess) {
+        long long h[24];
+        if (hipMemcpy(h, a.dstamps, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+            std::fprintf(stderr, "dense_stamps");
+            for (int k = 1; k <= 10; k++) std::fprintf(stderr, " %lld", h[k] - h[k - 1]);
+            std::fprintf(stderr, " | t10: %lld", h[11] - h[16]);
+            for (int k = 12; k <= 15; k++) std::fprintf(stderr, " %lld", h[k] - h[k - 1]);
+            std::fprintf(stderr, "\n");
+        }
+    }
+#endif
     if (e != hipSuccess) return set_error(MPCCBF_ERR_HIP, std::string("dense QP solve: ") + hipGetErrorString(e));
     const double* x = (const double*)ho;
     double* obj = (double*)(ho + b_x);

@@ -34,14 +34,6 @@ struct WaveAS {
     float wn[WROWS];         // candidate weights 1 / sqrt(g P^-1 g) per image row
 };
 
-// lane l's double as a wave-uniform (scalar) value
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (long long)lo);
-}
-
 // row i of a 16 x 16 LDS matrix stored with row stride 17 times a 16-vector (LDS): every load first
 // (interleaved with the FMAs the compiler waited for each pair of loads in turn), then the same
 // sequential FMA chain

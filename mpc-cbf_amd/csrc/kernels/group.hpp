@@ -90,6 +90,14 @@ __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
     return v;
 }
 
+// lane l's double as a wave-uniform (scalar) value
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)lo);
+}
+
 enum class Op { Sum, Max, Min };
 
 template <Op OP>

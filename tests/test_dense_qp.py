@@ -152,6 +152,38 @@ def test_dense_random_qps_match_oracle(mpclib, oracle):
 
 
 @pytest.mark.gpu
+def test_dense_asymmetric_sparse_h_and_index_edges(mpclib, oracle):
+    """The packed form carries Hs = (H + H^T)/2's upper triangle with u16 indices (i << 6 | j) and u8
+    columns: an asymmetric H (a random antisymmetric part, entries with H_ij = -H_ji whose Hs entry
+    is zero) solves as its symmetric part; a sparse block-diagonal H; the index edges at 64 variables
+    (i = j = 63, u8 column 63) with 58 equalities and two fixed variables. Against the oracle's
+    dense solve of the same QP with Hs given explicitly."""
+    rng = np.random.default_rng(41)
+    cases = []
+    q = _random_qp(rng, 64, 58, 30, 0, 2)
+    K = rng.standard_normal((64, 64))
+    q["H"] = q["H"] + (K - K.T)
+    cases.append(q)
+    q = _random_qp(rng, 20, 14, 12, 0, 0)
+    Hs = q["H"].copy()
+    Hb = np.zeros_like(Hs)
+    for b0 in range(0, 20, 5):  # block-diagonal part of Hs (positive definite blocks)
+        Hb[b0:b0 + 5, b0:b0 + 5] = Hs[b0:b0 + 5, b0:b0 + 5]
+    A5 = np.zeros_like(Hs)
+    A5[0, 19], A5[19, 0] = 3.0, -3.0  # antisymmetric pair: Hs zero there
+    q["H"] = Hb + A5
+    cases.append(q)
+    st, xs, obj = mpclib.dense_qp_solve_batch(cases)
+    for k, q in enumerate(cases):
+        hs = 0.5 * (q["H"] + q["H"].T)
+        r = oracle.solve_dense_qp(dict(n=q["c"].shape[0], H=hs, c=q["c"], c0=q["c0"], A=q["A"], lo=q["lo"],
+                                       hi=q["hi"], vlo=q["vlo"], vhi=q["vhi"]))
+        assert st[k] == r["status"] == mpclib.OPTIMAL, (k, st[k], r["status"])
+        assert abs(obj[k] - r["obj"]) <= 1e-6 * max(1.0, abs(r["obj"])), (k, obj[k], r["obj"])
+        np.testing.assert_allclose(xs[k], r["x"], atol=1e-5)
+
+
+@pytest.mark.gpu
 def test_dense_inconsistent_and_dependent_equalities(mpclib):
     """Dependent equalities with consistent right-hand sides are dropped by the pivoted QR's
     rank test; inconsistent ones make the QP INFEASIBLE; more equalities than variables."""
