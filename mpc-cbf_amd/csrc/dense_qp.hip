@@ -95,8 +95,8 @@ struct DenseBatch {
 
 namespace dev {
 
-// zero rows after the E^T image: the QR's row loops run in unguarded chunks of 8 rows
-constexpr int ET_PAD = 8;
+// zero rows after the E^T image: the QR's row loops run in unguarded chunks of ET_PAD rows
+constexpr int ET_PAD = 16;
 
 // E^T / H image in dynamic LDS, sized per batch: rows = the batch's largest n, row stride S = the
 // larger of its largest n and equality count, made odd (spread banks); at most 64 x 65 doubles
@@ -119,20 +119,20 @@ struct ReduceLds {
 __device__ __forceinline__ bool fin_bound(double v) { return isfinite(v) && fabs(v) < kInf; }
 
 // sum over rows i = t .. n-1 of the image's columns ca and cb (row stride S) in row order, in
-// unguarded chunks of 8 rows (the rows past n are zero: the image's own zero rows and its ET_PAD
-// pad rows; their +0 terms leave the sum as the plain loop forms it), every chunk's loads first
-__device__ __forceinline__ double col_dot8(const double* __restrict__ et, int S, int t, int n, int ca, int cb) {
+// unguarded chunks of ET_PAD rows (the rows past n are zero: the image's own zero rows and its
+// ET_PAD pad rows; their +0 terms leave the sum as the plain loop forms it), every chunk's loads first
+__device__ __forceinline__ double col_dot_pad(const double* __restrict__ et, int S, int t, int n, int ca, int cb) {
     double acc = 0.0;
-    for (int i0 = t; i0 < n; i0 += 8) {
+    for (int i0 = t; i0 < n; i0 += ET_PAD) {
         const double* r0 = et + i0 * S;
-        double x[8], y[8];
+        double x[ET_PAD], y[ET_PAD];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < ET_PAD; u++) {
             x[u] = r0[u * S + ca];
             y[u] = r0[u * S + cb];
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) acc = fma(x[u], y[u], acc);
+        for (int u = 0; u < ET_PAD; u++) acc = fma(x[u], y[u], acc);
     }
     return acc;
 }
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         if (t == 10) DSTAMP(16);
         double nrm = -1.0;
         if (l >= t && l < me) {
-            nrm = col_dot8(et, LDS_S, t, n, l, l);
+            nrm = col_dot_pad(et, LDS_S, t, n, l, l);
         }
         if (t == 10) DSTAMP(11);
         const double best = grp_max<64>(nrm);
@@ -266,21 +266,24 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         if (t == 10) DSTAMP(14);
         // apply to columns t+1 .. me-1 (lane c)
         if (l > t && l < me) {
-            double w = col_dot8(et, LDS_S, t, n, t, l);
+            double w = col_dot_pad(et, LDS_S, t, n, t, l);
             w *= bt;
-            // (8 rows' loads before their stores, the pad rows' zeros included: as a plain loop each
+#ifdef MPCCBF_PDIP_STAMPS
+            if (t == 10 && l == t + 1 && a.dstamps && qi == 0) a.dstamps[17] = (long long)__builtin_amdgcn_s_memtime();
+#endif
+            // (ET_PAD rows' loads before their stores, the pad rows' zeros included: as a plain loop each
             // row's store could alias the next row's loads for all the compiler knows, and every
             // row waited for its own LDS round trip — two thirds of a reflection's time)
-            for (int i0 = t; i0 < n; i0 += 8) {
+            for (int i0 = t; i0 < n; i0 += ET_PAD) {
                 double* r0 = et + i0 * LDS_S;
-                double x[8], y[8];
+                double x[ET_PAD], y[ET_PAD];
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
+                for (int u = 0; u < ET_PAD; u++) {
                     x[u] = r0[u * LDS_S + t];
                     y[u] = r0[u * LDS_S + l];
                 }
 #pragma unroll
-                for (int u = 0; u < 8; u++) r0[u * LDS_S + l] = fma(-w, x[u], y[u]);
+                for (int u = 0; u < ET_PAD; u++) r0[u * LDS_S + l] = fma(-w, x[u], y[u]);
             }
         }
         __syncthreads();
@@ -936,6 +939,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
             std::fprintf(stderr, "dense_stamps");
             for (int k = 1; k <= 10; k++) std::fprintf(stderr, " %lld", h[k] - h[k - 1]);
             std::fprintf(stderr, " | t10: %lld", h[11] - h[16]);
+            std::fprintf(stderr, " (w loop %lld)", h[17] - h[14]);
             for (int k = 12; k <= 15; k++) std::fprintf(stderr, " %lld", h[k] - h[k - 1]);
             std::fprintf(stderr, "\n");
         }
