@@ -225,12 +225,14 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     const int tmax = n < me ? n : me;
     int rank = 0;
     double r00 = 0.0;
+    // column norms over rows t .. n-1: reflection t's update forms the next step's in its row loop
+    // from the values it stores (the same sum in the same row order: the separate loop over LDS
+    // was a fifth of a reflection)
+    double nrm_next = 0.0;
     for (int t = 0; t < tmax; t++) {
         if (t == 10) DSTAMP(16);
         double nrm = -1.0;
-        if (l >= t && l < me) {
-            nrm = col_dot_pad(et, LDS_S, t, n, l, l);
-        }
+        if (l >= t && l < me) nrm = t == 0 ? col_dot_pad(et, LDS_S, t, n, l, l) : nrm_next;
         if (t == 10) DSTAMP(11);
         const double best = grp_max<64>(nrm);
         const int p = __ffsll((long long)__ballot(nrm == best && l >= t && l < me)) - 1;
@@ -274,6 +276,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
             // (ET_PAD rows' loads before their stores, the pad rows' zeros included: as a plain loop each
             // row's store could alias the next row's loads for all the compiler knows, and every
             // row waited for its own LDS round trip — two thirds of a reflection's time)
+            double acc = 0.0;
             for (int i0 = t; i0 < n; i0 += ET_PAD) {
                 double* r0 = et + i0 * LDS_S;
                 double x[ET_PAD], y[ET_PAD];
@@ -283,8 +286,13 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
                     y[u] = r0[u * LDS_S + l];
                 }
 #pragma unroll
-                for (int u = 0; u < ET_PAD; u++) r0[u * LDS_S + l] = fma(-w, x[u], y[u]);
+                for (int u = 0; u < ET_PAD; u++) {
+                    const double v = fma(-w, x[u], y[u]);
+                    r0[u * LDS_S + l] = v;
+                    acc = fma(i0 + u > t ? v : 0.0, v, acc);  // (rows t+1 .. : the next norm)
+                }
             }
+            nrm_next = acc;
         }
         __syncthreads();
         if (t == 10) DSTAMP(15);
