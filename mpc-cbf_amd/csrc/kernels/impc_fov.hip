@@ -28,14 +28,14 @@ constexpr int FOV_NB_CAP = 16;  // observed neighbours per agent
 // the later phases (tools/setup_stamps.py)
 #ifdef MPCCBF_SETUP_STAMPS
 #define SSTAMP(k) stamp(args, ai, lane, k)
-#define PSTAMP(k) \
+#define PHSTAMP(k) \
     do {          \
     } while (0)
 #else
 #define SSTAMP(k) \
     do {          \
     } while (0)
-#define PSTAMP(k) stamp(args, ai, lane, k)
+#define PHSTAMP(k) stamp(args, ai, lane, k)
 #endif
 
 // LDS of the slack rows (slack mode only)
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         if (lane < nnb) slk->w[lane] = op.slack_cost * pow(op.slack_decay, (double)slk->order[lane]);
         wave_lds_sync();
     }
-    PSTAMP(2);
+    PHSTAMP(2);
 
     bool have_curve = false, success = true;
     const PdipCfg cfg{op.maxit, op.tol};
@@ -465,7 +465,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         }
         if (lane < WNZ) sc.q[lane] = q_s[lane];
         wave_lds_sync();
-        if (it < 2) PSTAMP(3 + 2 * it);
+        if (it < 2) PHSTAMP(3 + 2 * it);
         int st;
         int nit = 0;
         double prs = __builtin_nan(""), drs = __builtin_nan("");
@@ -773,7 +773,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
             success = false;
         }
         write_iteration(args, oi, lane, st, objv, nit, prs, drs);
-        if (it < 2) PSTAMP(4 + 2 * it);
+        if (it < 2) PHSTAMP(4 + 2 * it);
         wave_lds_sync();
     }
     {
