@@ -95,8 +95,9 @@ struct DenseBatch {
 
 namespace dev {
 
-// zero rows after the E^T image: the QR's row loops run in unguarded chunks of ET_PAD rows
-constexpr int ET_PAD = 16;
+// zero rows after the E^T image: the QR's row loops run in unguarded chunks of ET_PAD rows (16
+// took the kernel to 141 registers, three waves per SIMD, for no gain in the QR)
+constexpr int ET_PAD = 8;
 
 // E^T / H image in dynamic LDS, sized per batch: rows = the batch's largest n, row stride S = the
 // larger of its largest n and equality count, made odd (spread banks); at most 64 x 65 doubles
@@ -166,27 +167,23 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         double* sd = et + (size_t)(NROWS + ET_PAD) * LDS_S;
         int32_t* si = (int32_t*)(sd + a.stage_d);
         const int nd = (int)(a.off_d[qi + 1] - a.off_d[qi]), ni = (int)(a.off_i[qi + 1] - a.off_i[qi]);
-        for (int e0 = 0; e0 < nd; e0 += 8 * 64) {
+        // (doubles and ints in the same pass, 512 of each: 16 loads per lane in flight — two bus
+        // round trips for a typical QP where separate passes took three)
+        for (int e0 = 0; e0 < nd || e0 < ni; e0 += 8 * 64) {
             double v[8];
+            int32_t w[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int e = e0 + u * 64 + l;
                 v[u] = db[e < nd ? e : 0];
+                w[u] = ib[e < ni ? e : 0];
             }
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (e0 + u * 64 + l < nd) sd[e0 + u * 64 + l] = v[u];
-        }
-        for (int e0 = 0; e0 < ni; e0 += 8 * 64) {
-            int32_t v[8];
 #pragma unroll
             for (int u = 0; u < 8; u++) {
                 const int e = e0 + u * 64 + l;
-                v[u] = ib[e < ni ? e : 0];
+                if (e < nd) sd[e] = v[u];
+                if (e < ni) si[e] = w[u];
             }
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-                if (e0 + u * 64 + l < ni) si[e0 + u * 64 + l] = v[u];
         }
         __syncthreads();
         db = sd;
