@@ -175,7 +175,8 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
                               WaveAS& ws, const double* __restrict__ P, const double* __restrict__ Pinv,
                               double tol, int maxstep, bool want_rd, int lane, double& rp_out,
                               double& rd_out, int& steps, double& tlow, int* cand = nullptr,
-                              int nfirst = 0, int nrows = WROWS, long long* dbg = nullptr) {
+                              int nfirst = 0, int nrows = WROWS, long long* dbg = nullptr,
+                              bool want_rp = true) {
     (void)dbg;
 #ifdef MPCCBF_PDIP_STAMPS  // profiling build: shader-clock stamps of the solve's first steps
 #define WSTAMP(kk, cond)                                                              \
@@ -303,7 +304,7 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         WSTAMP(steps == 0 ? 2 : 8, steps <= 1);
         // converged: no side violated beyond add_tol (m = the scaled primal residual, reduced once)
         if (__ballot(vb > add_tol) == 0ull) {
-            m = grp_max<64>(vb);
+            if (want_rp) m = grp_max<64>(vb);  // (only for the caller's primal-residual output)
             break;
         }
         if (!have_wn) {  // first violation: form the weights and scan again

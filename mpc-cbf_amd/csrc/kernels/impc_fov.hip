@@ -684,7 +684,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
                 if (op.dual_as > 0)
                     das = das_solve_wave(image_rows(mtot), Gimg, sc, was, opp(buf, op.o_P16), opp(buf, op.o_Pinv16),
                                          op.tol, 2 * op.dual_as, args.dual_res != nullptr, lane, drp, drd, dsteps,
-                                         dtlow, nullptr, mtot, mtot, dbg);
+                                         dtlow, nullptr, mtot, mtot, dbg, args.primal_res != nullptr);
             } else if (pattern_ok) {
                 if (lv) slk->rowl[c_me] = lane;
                 das = run_patterns(SLK_PATTERNS);
