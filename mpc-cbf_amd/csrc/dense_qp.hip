@@ -122,9 +122,10 @@ __device__ __forceinline__ bool fin_bound(double v) { return isfinite(v) && fabs
 // sum over rows i = t .. n-1 of the image's columns ca and cb (row stride S) in row order, in
 // unguarded chunks of ET_PAD rows (the rows past n are zero: the image's own zero rows and its
 // ET_PAD pad rows; their +0 terms leave the sum as the plain loop forms it), every chunk's loads first
-__device__ __forceinline__ double col_dot_pad(const double* __restrict__ et, int S, int t, int n, int ca, int cb) {
+__device__ __forceinline__ double col_dot_pad(const double* __restrict__ et, int S, int t, int n, int ca, int cb,
+                                              int step = ET_PAD) {
     double acc = 0.0;
-    for (int i0 = t; i0 < n; i0 += ET_PAD) {
+    for (int i0 = t; i0 < n; i0 += step) {
         const double* r0 = et + i0 * S;
         double x[ET_PAD], y[ET_PAD];
 #pragma unroll
@@ -226,13 +227,21 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     // from the values it stores (the same sum in the same row order: the separate loop over LDS
     // was a fifth of a reflection)
     double nrm_next = 0.0;
+    // up to 32 equalities: two lanes per column (lanes 2c, 2c+1: alternate ET_PAD-row chunks, the
+    // partial sums joined by one DPP move), halving every row loop's chain and loads
+    const bool pair = me <= 32;
+    const int cq = pair ? (l >> 1) : l;     // this lane's column
+    const int h0 = pair ? (l & 1) * ET_PAD : 0;  // its first chunk's row offset
+    const int cstep = pair ? 2 * ET_PAD : ET_PAD;
+    auto join = [&](double v) { return pair ? v + dpp_mov<DPP_XOR1>(v) : v; };
     for (int t = 0; t < tmax; t++) {
         if (t == 10) DSTAMP(16);
         double nrm = -1.0;
-        if (l >= t && l < me) nrm = t == 0 ? col_dot_pad(et, LDS_S, t, n, l, l) : nrm_next;
+        if (cq >= t && cq < me) nrm = t == 0 ? join(col_dot_pad(et, LDS_S, t + h0, n, cq, cq, cstep)) : nrm_next;
         if (t == 10) DSTAMP(11);
         const double best = grp_max<64>(nrm);
-        const int p = __ffsll((long long)__ballot(nrm == best && l >= t && l < me)) - 1;
+        const int pl = __ffsll((long long)__ballot(nrm == best && cq >= t && cq < me)) - 1;
+        const int p = pl < 0 ? -1 : (pair ? pl >> 1 : pl);
         const double sig = sqrt(best);
         if (t == 0) r00 = sig;
         if (!(sig > 1e-12 * r00) || p < 0) break;  // the remaining columns are dependent
@@ -264,32 +273,33 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         __syncthreads();
         if (t == 10) DSTAMP(14);
         // apply to columns t+1 .. me-1 (lane c)
-        if (l > t && l < me) {
-            double w = col_dot_pad(et, LDS_S, t, n, t, l);
+        if (cq > t && cq < me) {
+            double w = join(col_dot_pad(et, LDS_S, t + h0, n, t, cq, cstep));
             w *= bt;
 #ifdef MPCCBF_PDIP_STAMPS
-            if (t == 10 && l == t + 1 && a.dstamps && qi == 0) a.dstamps[17] = (long long)__builtin_amdgcn_s_memtime();
+            if (t == 10 && l == (pair ? 2 * (t + 1) : t + 1) && a.dstamps && qi == 0)
+                a.dstamps[17] = (long long)__builtin_amdgcn_s_memtime();
 #endif
             // (ET_PAD rows' loads before their stores, the pad rows' zeros included: as a plain loop each
             // row's store could alias the next row's loads for all the compiler knows, and every
             // row waited for its own LDS round trip — two thirds of a reflection's time)
             double acc = 0.0;
-            for (int i0 = t; i0 < n; i0 += ET_PAD) {
+            for (int i0 = t + h0; i0 < n; i0 += cstep) {
                 double* r0 = et + i0 * LDS_S;
                 double x[ET_PAD], y[ET_PAD];
 #pragma unroll
                 for (int u = 0; u < ET_PAD; u++) {
                     x[u] = r0[u * LDS_S + t];
-                    y[u] = r0[u * LDS_S + l];
+                    y[u] = r0[u * LDS_S + cq];
                 }
 #pragma unroll
                 for (int u = 0; u < ET_PAD; u++) {
                     const double v = fma(-w, x[u], y[u]);
-                    r0[u * LDS_S + l] = v;
+                    r0[u * LDS_S + cq] = v;
                     acc = fma(i0 + u > t ? v : 0.0, v, acc);  // (rows t+1 .. : the next norm)
                 }
             }
-            nrm_next = acc;
+            nrm_next = join(acc);
         }
         __syncthreads();
         if (t == 10) DSTAMP(15);
