@@ -360,16 +360,18 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
     }
     DSTAMP(6);
     // ---- Hs Z and Hs xp, Hs = (H + H^T) / 2: the packed upper triangle's nonzeros scattered into
-    // a dense n x n image in LDS (E^T's space, free from here; each entry written once, so no
-    // atomics), then lane l forms row l over j = 0 .. n-1 (entry (min, max) of the image) — a fixed
+    // a dense n x n image in LDS (E^T's space, free from here; both triangles, each entry written
+    // by one lane, so no atomics), then lane l forms row l over j = 0 .. n-1 — a fixed
     // summation order (no dependence on how the hardware orders LDS atomics), and no lane walks the
     // whole nonzero list (that serial scan of global loads and divisions cost ~1.7 ms per 4096-QP
     // call)
     for (int e = l; e < n * LDS_S; e += 64) et[e] = 0.0;
     __syncthreads();
     for (int e = l; e < nh; e += 64) {
-        const int k = hidx[e];
-        et[(k >> 6) * LDS_S + (k & 63)] = hval[e];
+        const int k = hidx[e], i = k >> 6, j = k & 63;
+        const double v = hval[e];
+        et[i * LDS_S + j] = v;  // (both triangles: row l of the image is then read along j,
+        et[j * LDS_S + i] = v;  // consecutive lanes on consecutive words)
     }
     __syncthreads();
     if (l < n) {
@@ -377,7 +379,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
 #pragma unroll
         for (int b = 0; b < DENSE_NZ; b++) hzl[b] = 0.0;
         for (int j = 0; j < n; j++) {
-            const double hv = l <= j ? et[l * LDS_S + j] : et[j * LDS_S + l];
+            const double hv = et[j * LDS_S + l];
             hxl = fma(hv, s.xp[j], hxl);
 #pragma unroll
             for (int b = 0; b < DENSE_NZ; b++) hzl[b] = fma(hv, s.z[j * DENSE_NZ + b], hzl[b]);
