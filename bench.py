@@ -68,8 +68,6 @@ def parse(argv=None):
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--das-warm", type=int, default=0,
                     help="mpccbf_options.das_warm_steps (0 = default 3; < 0 = no IMPC iteration-1 warm start)")
-    ap.add_argument("--cpu-baseline-agents", type=int, default=-1,
-                    help="agents in the CPU-oracle sample (default: sized for ~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--loop", choices=["native", "python"], default="native",
                     help="native: mpccbf_run_steps (C++ loop, RCCL); python: one call per step")
@@ -631,7 +629,7 @@ def main():
         if trace_res is not None:
             res["closed_loop"] = closed_loop_metrics(trace_res, targets_h, cfg, fov)
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h)
+            res["cpu_baseline"] = cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h, trace_res)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -737,52 +735,87 @@ def pmc_traffic(kname: str, workload: str):
     return pmc_lookup(kname, workload, "hbm_bytes_per_launch_corrected")
 
 
-def cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h=None):
+def cpu_threads() -> tuple[int, int]:
+    """(threads used, CPUs in this process's affinity set): the affinity set, capped by
+    OMP_NUM_THREADS when set (the GPU box sets it to the job's CPU share, while its affinity set and
+    os.cpu_count() show the whole machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(aff, omp) if omp > 0 else aff), aff
+
+
+def cpu_baseline(cfg, states_h, targets_h, args, radius, cov_h=None, trace=None):
     """The oracle (CPU restatement of the reference assembly + dense QP solve, standing in for
-    CPLEX which cannot run here) on a bounded sample of the same workload: on the host cores
-    (thread pool, `cores`) and on 1 thread (CPLEX Threads=1, CPLEX.cpp:158)."""
+    CPLEX which cannot run here) timed on the states of the GPU's own timed steps: the closed-loop
+    trace's state tables at up to 6 step indices spread over the timed range (its first and last
+    step included), the whole swarm per sampled step on a thread pool (one agent per task, CPLEX
+    Threads=1 per solve, CPLEX.cpp:118) — per-step wall times give the p99 step latency — plus one
+    bounded single-thread sample (~5 s) of the first timed step. Without a trace (--no-trace,
+    multi-rank shares) the initial swarm stands in and the line says so."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
     from mpccbf import swarm
     p = O.make_params(cfg)
     refs = swarm.refs_from_targets(targets_h, cfg["k_hor"])
-    if cfg.get("cbf_mode", 0) == 1:
-        rp, col = swarm.fov_csr(states_h, args.knn, radius, cfg["fov_beta"])
-    elif args.neighbours == "all":
-        n_ = len(states_h)
-        rp = np.arange(n_ + 1, dtype=np.int32) * (n_ - 1)
-        col = np.array([j for a in range(n_) for j in range(n_) if j != a], dtype=np.int32)
-    else:
-        rp, col = swarm.knn_csr(states_h, args.knn, radius)
     n = len(states_h)
-    count = args.cpu_baseline_agents if args.cpu_baseline_agents > 0 else None
-    if count is None:
-        # calibrate on 32 agents, then size the sample for ~10 s
+
+    def lists(st):
+        if cfg.get("cbf_mode", 0) == 1:
+            return swarm.fov_csr(st, args.knn, radius, cfg["fov_beta"])
+        if args.neighbours == "all":
+            rp_ = np.arange(n + 1, dtype=np.int32) * (n - 1)
+            col_ = np.array([j for a in range(n) for j in range(n) if j != a], dtype=np.int32)
+            return rp_, col_
+        return swarm.knn_csr(st, args.knn, radius)
+
+    # the timed steps' state tables: trace index s = the state the QPs of control step s are built from
+    if trace is not None:
+        nt = trace["traj"].shape[1] - 1
+        first_t = args.warmup
+        idx = sorted({int(round(v)) for v in np.linspace(first_t, nt - 1, num=min(6, nt - first_t))})
+        tables = [(s, np.ascontiguousarray(trace["traj"][:, s, :])) for s in idx]
+        src = f"states of timed control steps {idx} (closed-loop trace; timed range {first_t}..{nt - 1})"
+    else:
+        tables = [(0, np.ascontiguousarray(states_h))]
+        src = "the initial swarm (no closed-loop trace in this run)"
+    threads, aff = cpu_threads()
+    step_ms, solved, total_s = [], 0, 0.0
+    for s, st in tables:
+        rp, col = lists(st)
         t = time.perf_counter()
-        r = O.impc_batch(p, states_h, refs, rp, col, 0, 32, 1, covs=cov_h)
-        dt = (time.perf_counter() - t) / 32
-        count = int(min(n, max(64, 10.0 / max(dt, 1e-6))))
+        r = O.impc_batch(p, st, refs, rp, col, 0, n, threads, covs=cov_h)
+        dt = time.perf_counter() - t
+        step_ms.append(1e3 * dt)
+        solved += r["solved"]
+        total_s += dt
+    # one thread on the first sampled step: a bounded sample sized for ~5 s
+    s0, st0 = tables[0]
+    rp, col = lists(st0)
     t = time.perf_counter()
-    r = O.impc_batch(p, states_h, refs, rp, col, 0, count, 1, covs=cov_h)
-    dt = time.perf_counter() - t
-    # the same sample on a thread pool, one agent per task (CPLEX Threads=1 per solve), over the
-    # host cores this job may use (16 on the GPU box: OMP_NUM_THREADS; os.cpu_count() shows the
-    # whole machine there)
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16, os.cpu_count() or 1))
+    O.impc_batch(p, st0, refs, rp, col, 0, min(n, 32), 1, covs=cov_h)
+    per = (time.perf_counter() - t) / min(n, 32)
+    count = int(min(n, max(64, 5.0 / max(per, 1e-6))))
     t = time.perf_counter()
-    rm = O.impc_batch(p, states_h, refs, rp, col, 0, count, threads, covs=cov_h)
-    dtm = time.perf_counter() - t
+    r1 = O.impc_batch(p, st0, refs, rp, col, 0, count, 1, covs=cov_h)
+    dt1 = time.perf_counter() - t
     model = ""
     try:
         model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
     except (OSError, StopIteration):
         pass
-    return {"value": rm["solved"] / dtm, "unit": "QP/s", "cores": threads, "kind": "port",
-            "single_core_value": r["solved"] / dt,
+    return {"value": solved / total_s, "unit": "QP/s", "cores": threads, "kind": "port",
+            "affinity_cpus": aff,
+            "p99_step_ms": float(np.percentile(step_ms, 99)),
+            "step_ms": [round(v, 2) for v in step_ms],
+            "steps_sampled": [s for s, _ in tables],
+            "single_core_value": r1["solved"] / dt1,
             "cpu": model,
-            "sample": f"first {count} agents of the same swarm/step, {r['solved']} QPs: {dtm:.2f} s on "
-                      f"{threads} threads (one agent per task), {dt:.1f} s on 1 thread "
-                      f"(oracle/ CPU restatement; CPLEX unavailable)"}
+            "sample": f"all {n} agents at each sampled step, {solved} QPs: {total_s:.2f} s on {threads} threads "
+                      f"(one agent per task); {src}; 1 thread: first {count} agents of step {s0}, "
+                      f"{r1['solved']} QPs in {dt1:.1f} s (oracle/ CPU restatement; CPLEX unavailable)"}
 
 
 if __name__ == "__main__":

@@ -28,7 +28,6 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
                        hipStream_t s);
 const char* impc_kernel_name(const DevOps& op, int variant, int n);
 int impc_clock_waves(const DevOps& op, int variant, int n);
-void impc_set_device_simds(int simds);
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
 hipError_t launch_fov_rows_eval(int count, const double* ego, const double* nb, double fov, double Ds, double Rs,
                                 double bbx, double bby, double* vor, double* rows, hipStream_t s);
@@ -213,12 +212,14 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
     if (fb) {
         q_this = c->defer + (size_t)c->defer_parity * (c->defer_cap + 2);
         a.defer_clear = c->defer + (size_t)(c->defer_parity ^ 1) * (c->defer_cap + 2);
-        c->defer_parity ^= 1;
     }
     a.defer = q_this;
     if (ev0) HIP_TRY(hipEventRecord(ev0, stream));
     hipError_t e = c->dev.cbf_mode == 1 ? launch_impc_fov(c->dev, c->dbuf, a, stream)
                                         : launch_impc(c->dev, c->dbuf, a, c->variant, stream);
+    // the queues alternate only once the main launch is enqueued: a launch that failed zeroed no
+    // header, so the next call must append to this step's queue again (zeroed by the launch before)
+    if (e == hipSuccess && fb) c->defer_parity ^= 1;
     if (e == hipSuccess && fb) {
         ImpcArgs f = a;
         f.defer = nullptr;
@@ -300,17 +301,18 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
             if (!(o.lo[i] > -1e300 && o.hi[i] < 1e300)) ok = false;  // the layout is two-sided only
         }
         const int rpd = std::max(per[0], std::max(per[1], per[2]));
-        if (ok && rpd <= 16) {
-            std::vector<double> B((size_t)DIM * 16 * SEP_ROW, 0.0);
-            for (int dd = 0; dd < DIM; dd++)
-                for (int l = 0; l < 16; l++) {
-                    B[((size_t)dd * 16 + l) * SEP_ROW + 8] = -1.0;  // inert row: 0 in [-1, 1]
-                    B[((size_t)dd * 16 + l) * SEP_ROW + 9] = 1.0;
-                }
+        const int sb = (rpd + 15) / 16;  // row slots per lane and channel
+        if (ok && sb <= 2) {
+            std::vector<double> B((size_t)DIM * sb * 16 * SEP_ROW, 0.0);
+            for (size_t r = 0; r < (size_t)DIM * sb * 16; r++) {
+                B[r * SEP_ROW + 8] = -1.0;  // inert row: 0 in [-1, 1]
+                B[r * SEP_ROW + 9] = 1.0;
+            }
             int fill[DIM] = {0, 0, 0};
             for (int i = 0; i < o.G.r; i++) {
-                const int dd = o.row_dim[i], l = fill[dd]++;
-                double* r = &B[((size_t)dd * 16 + l) * SEP_ROW];
+                const int dd = o.row_dim[i], f = fill[dd]++;
+                // slot f / 16, lane f % 16 (sb = 1: row f of the channel in lane f)
+                double* r = &B[((size_t)(dd * sb + f / 16) * 16 + f % 16) * SEP_ROW];
                 r[0] = o.G(i, dd * o.nzd);
                 r[1] = o.G(i, dd * o.nzd + 1);
                 for (int s = 0; s < SD; s++) r[2 + s] = o.Gs(i, s);
@@ -331,6 +333,7 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
             d.sep = 1;
             d.nzd = o.nzd;
             d.sep_rows_per_dim = rpd;
+            d.sep_sb = sb;
         }
     }
     pack(v, d.o_Z, o.Z);
@@ -489,10 +492,13 @@ int mpccbf_create(const mpccbf_params* p, const mpccbf_options* opt, mpccbf_ctx*
 #endif
     c->variant = 0;
     hipError_t e = hipSetDevice(c->device);
+    d.wide_max = 1024;
     if (e == hipSuccess) {
-        // share-adaptive layout: one agent per wave up to one agent per SIMD (4 per CU)
+        // share-adaptive layout: one agent per wave up to one agent per SIMD (4 per CU) of this
+        // context's device (kept in the context: no process-wide state shared by contexts)
         hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess) impc_set_device_simds(4 * prop.multiProcessorCount);
+        if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
+            d.wide_max = 4 * prop.multiProcessorCount;
     }
     if (e == hipSuccess) e = hipMalloc(&c->dbuf, v.size() * sizeof(double));
     if (e == hipSuccess) e = hipMemcpy(c->dbuf, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice);

@@ -19,9 +19,11 @@ struct DevOps {
     int32_t maxit;
     double tol;
     double feas_tol;  // absolute row-violation tolerance for constant rows / single-row checks
-    // separable layout (impc_sep_kernel): per channel d and lane l, row l of channel d as
-    // [g0, g1, Gs(6), lo, hi] (SEP_ROW doubles), 16 rows per channel (unused: inert g = 0, [-1, 1])
-    int32_t sep, nzd, sep_rows_per_dim;
+    // separable layout (impc_sep_kernel): per channel d, slot k < sep_sb and lane l, row k * 16 + l
+    // of channel d as [g0, g1, Gs(6), lo, hi] (SEP_ROW doubles) at ((d * sep_sb + k) * 16 + l);
+    // 16 * sep_sb rows per channel (unused: inert g = 0, [-1, 1]); sep_sb = 1 up to 16 rows per
+    // channel (K <= 15 at base_config.json), 2 up to 32 (K = 16 .. 31)
+    int32_t sep, nzd, sep_rows_per_dim, sep_sb;
     int32_t o_Gsep;
     int32_t o_Pinv;  // separable layout: per-channel inverse 2x2 blocks of Pr, (a, b, c) x 3
     // FoV controller (cbf_mode 1, impc_fov_kernel): Voronoi operators VZ (C x 2 x nz), VS (C x 2 x 6),
@@ -69,6 +71,9 @@ struct DevOps {
     // the operator buffer's prefix [0, hot) holds every operator of the separable collision kernels
     // (staged in LDS by impc_wide_kernel)
     int32_t hot;
+    // share-adaptive layout: agents per launch up to which the one-agent-per-wave kernel is the
+    // default (one wave per SIMD: 4 x the device's CUs, set per context at mpccbf_create)
+    int32_t wide_max;
 };
 
 constexpr int WBOX_ROW = 16 + 6 + 2;

@@ -188,10 +188,10 @@ __global__ void __launch_bounds__(256) impc_kernel(const DevOps op, const double
 // Slack mode: a lane builds the CBF rows of its neighbour (list position jn, -1: none) itself
 // (slot k = sample k), so all rows of one slack variable live in the lane that owns it. Filtered
 // rows stay inert (ccv = 0). Returns whether some row of this lane is live.
-template <int CB>
+template <int SB, int CB>
 __device__ bool lane_cbf_rows(const DevOps& op, const double* buf, const ImpcArgs& args, int it,
                               const double (&s0)[6], const double (&y)[SEP_NZ], bool grid_mode,
-                              const int32_t* nbl, int nb0, int jn, SepRows<1, CB>& rw) {
+                              const int32_t* nbl, int nb0, int jn, SepRows<SB, CB>& rw) {
     const double* UZ = opp(buf, op.o_UZ);
     const double* US = opp(buf, op.o_US);
     const int nk = (it == 0) ? 1 : op.cbf_h;
@@ -509,7 +509,8 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     // per row [g0, g1, Gs(6), lo, hi], two-sided; unused rows inert: g = 0, Gs = 0, [-1, 1])
     if (grid_mode) gq_slots<G>(args, gq, gl);
     SepRows<SB, CB> rw_reg;  // (the fallback launch: rows in LDS)
-    SepRows<SB, CB>& rw = pick_rows<QUEUE>(rw_reg, rows_lds);
+    // (rows in LDS: the fallback launch, and two box slots per lane, where in registers they spill)
+    SepRows<SB, CB>& rw = pick_rows<QUEUE || (SB > 1)>(rw_reg, rows_lds);
     {
         const double* B = opp(buf, op.o_Gsep);
 #pragma unroll
@@ -610,7 +611,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                                                    gl, jn, wslack);
                 slack_overflow = nlive > G;
             }
-            live = grp_ballot<G>(lane_cbf_rows<CB>(op, buf, args, it, sx, y, grid_mode, nbs.idx, nb0, jn, rw)) != 0ull;
+            live = grp_ballot<G>(lane_cbf_rows<SB, CB>(op, buf, args, it, sx, y, grid_mode, nbs.idx, nb0, jn, rw)) != 0ull;
         } else {
             double sx[6];  // the state again (not kept in registers across the solves)
             load_state_lds(s0k, sx);
@@ -869,7 +870,7 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
     // set's warm-start side ids and their count (not in slack mode) | linear term and constant, the
     // agent index, the residuals
     __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 10];
-    __shared__ SepRowsLds<SB, CB> rows_lds[QUEUE ? BS : 1];
+    __shared__ SepRowsLds<SB, CB> rows_lds[(QUEUE || SB > 1) ? BS : 1];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     lds_poison();
@@ -879,7 +880,7 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
         const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * GPB + gib;
         if (ai >= args.num_agents) return;
         impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
-                                                   nb_scratch[gib], keep_all[gib]);
+                                                   nb_scratch[gib], keep_all[gib], rows_lds);
         kclock_end<BS>(args);
     } else {
         // one queue entry per group (no grid-stride loop: carried across iterations the agent's
@@ -1175,11 +1176,6 @@ static bool impc_wide_ok(const DevOps& op) {
            op.dual_as > 0 && op.cbf_h <= MAX_CBF_H && op.hot > 0 && op.hot <= dev::WIDE_OPS;
 }
 
-// Agents per launch up to which the default layout is the wide kernel: one wave per agent at one
-// wave per SIMD fills the chip once at 4 x CUs agents
-static int g_wide_max = 1024;
-void impc_set_device_simds(int simds) { g_wide_max = simds > 0 ? simds : 1024; }
-
 static hipError_t launch_impc_wide(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s) {
     constexpr int BS = 256, WPB = BS / 64;
     const int blocks = (a.num_agents + WPB - 1) / WPB;
@@ -1196,7 +1192,14 @@ static hipError_t launch_impc_wide(const DevOps& op, const double* buf, const Im
 constexpr int VARIANT_SEP16 = 4, VARIANT_WIDE = 5;
 static bool sep_variant(int variant) { return variant == 0 || variant == VARIANT_SEP16; }
 static bool use_wide(const DevOps& op, int variant, int n) {
-    return impc_wide_ok(op) && (variant == VARIANT_WIDE || (variant == 0 && n <= g_wide_max));
+    return impc_wide_ok(op) && (variant == VARIANT_WIDE || (variant == 0 && n <= op.wide_max));
+}
+
+// Row slots per lane and channel of the separable slack kernel (1: up to 16 box rows per channel,
+// 2: up to 32, e.g. K = 16 as in the reference's instance files); 0: no slack instantiation fits
+static int slack_sb(const DevOps& op) {
+    if (!(op.sep && op.nzd == SEP_NZD_HOST && op.cbf_h <= 2)) return 0;
+    return op.sep_rows_per_dim <= 16 ? 1 : (op.sep_rows_per_dim <= 32 ? 2 : 0);
 }
 
 // The separable layout's lean main launch (fast start + dual active set; everything else deferred)
@@ -1214,7 +1217,10 @@ static bool sep_lean(const DevOps& op, int variant, int n) {
 hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide,
                                 hipStream_t s) {
     if (a.num_agents <= 0 || !a.queue) return hipSuccess;
-    if (op.slack_mode) return launch_impc_sep_t<1, 2, true, 64, true>(op, buf, a, s);
+    if (op.slack_mode) {
+        if (slack_sb(op) == 2) return launch_impc_sep_t<2, 2, true, 64, true>(op, buf, a, s);
+        return launch_impc_sep_t<1, 2, true, 64, true>(op, buf, a, s);
+    }
     if (wide) return launch_impc_sep_t<1, 8, false, 64, true>(op, buf, a, s);
     return launch_impc_sep_t<1, 1, false, 64, true>(op, buf, a, s);
 }
@@ -1229,7 +1235,7 @@ bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k) { return csr ||
 bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k, int n) {
     // slack mode: more than 16 neighbours only from caller lists (grid mode takes knn_k <= 16,
     // impc_enqueue)
-    if (op.slack_mode) return op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2 && csr;
+    if (op.slack_mode) return slack_sb(op) > 0 && csr;
     if (use_wide(op, variant, n) || sep_lean(op, variant, n)) return true;
     if (!(sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)) return false;
     return impc_rows_may_exceed(op, csr, knn_k);
@@ -1241,16 +1247,18 @@ int impc_clock_waves(const DevOps& op, int variant, int n) {
     if (n <= 0 || op.cbf_mode != 0) return 0;
     if (use_wide(op, variant, n)) return ((n + 3) / 4) * 4;  // 256-thread blocks, one agent per wave
     const bool sep = op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16;
-    if (op.slack_mode ? (sep && op.cbf_h <= 2) : (sep && sep_variant(variant)))
+    if (op.slack_mode && slack_sb(op) == 2) return ((n + 7) / 8) * 2;  // 128-thread blocks of 8 groups
+    if (op.slack_mode ? slack_sb(op) > 0 : (sep && sep_variant(variant)))
         return ((n + 15) / 16) * 4;  // 256-thread blocks of 16 groups
     return 0;
 }
 
 // Instantiation launch_impc picks for (operators, variant, agents per launch); nullptr if none fits.
 const char* impc_kernel_name(const DevOps& op, int variant, int n) {
-    if (op.slack_mode)  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2
-        return (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
-                   ? "impc_sep_kernel<1,2,true,256>" : nullptr;
+    if (op.slack_mode) {  // slack variables: separable layout, one lane per neighbour, cbf_h <= 2
+        const int sb = slack_sb(op);
+        return sb == 1 ? "impc_sep_kernel<1,2,true,256>" : (sb == 2 ? "impc_sep_kernel<2,2,true,128>" : nullptr);
+    }
     if (use_wide(op, variant, n)) return "impc_wide_kernel<256>";
     if (sep_lean(op, variant, n)) return "impc_sep_kernel<1,1,false,256,false,true>";
     if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false,256>";
@@ -1266,8 +1274,10 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
                        hipStream_t s) {
     if (a.num_agents <= 0) return hipSuccess;
     if (op.slack_mode) {
-        if (op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16 && op.cbf_h <= 2)
-            return launch_impc_sep_t<1, 2, true>(op, buf, a, s);
+        const int sb = slack_sb(op);
+        if (sb == 1) return launch_impc_sep_t<1, 2, true>(op, buf, a, s);
+        // (two box slots per lane: 128-thread blocks, the 256-thread block's LDS is past 160 KB)
+        if (sb == 2) return launch_impc_sep_t<2, 2, true, 128>(op, buf, a, s);
         return hipErrorInvalidValue;
     }
     if (use_wide(op, variant, a.num_agents)) return launch_impc_wide(op, buf, a, s);

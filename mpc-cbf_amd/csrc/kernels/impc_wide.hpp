@@ -253,9 +253,12 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
         }
         if (outer == 0) WST(7);
         if (outer == 0 && __ballot(nanv) != 0ull) return 0;
-        // the candidate: the largest normalised violation (as a float bit pattern; 0: none), its
-        // lowest lane on ties. Converged when no side is violated beyond add_tol (every score 0)
-        const unsigned key = eb > 0.0 ? __float_as_uint((float)eb) : 0u;
+        // the candidate: the largest normalised violation (as a float bit pattern), its lowest lane
+        // on ties. A side violated beyond add_tol keys at least 1 — also when its score rounds to 0
+        // in float (a weight w = 0 from a row norm beyond the float range) — so the solve is
+        // converged exactly when every key is 0 (das_wave's rule)
+        const bool viol = vb > add_tol;
+        const unsigned key = viol ? max(__float_as_uint((float)fmax(eb, 0.0)), 1u) : 0u;
         const unsigned kmax = (unsigned)uni_i((int)wave_max_u32(key));
         if (outer == 0) WST(8);
         if (kmax == 0u) {
@@ -263,6 +266,9 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
             break;
         }
         if (steps >= maxstep) return 0;
+        // the best candidate's score is 0 or denormal in float: no usable rule (the 16-lane
+        // pipeline solves it, deferred)
+        if (kmax == 1u) return 0;
         const int owner = __ffsll((long long)__ballot(key == kmax)) - 1;
         if (owner < 0) return 0;
         if (gl == owner) wide_stage(rw, pi, sb, gl, cand);

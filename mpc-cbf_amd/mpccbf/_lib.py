@@ -278,6 +278,13 @@ class Context:
         stamps (as impc_solve; every step overwrites them)."""
         if num_agents is None:
             num_agents = states.shape[0] - agent_first
+        if kernel_clock is not None:
+            # the library writes num_steps x W x 2 uint64 words from the base pointer: a shorter,
+            # narrower or strided tensor would be written out of bounds (W itself is checked
+            # against the launch's waves by mpccbf_run_steps)
+            if (kernel_clock.dim() != 3 or not kernel_clock.is_contiguous() or kernel_clock.element_size() != 8
+                    or kernel_clock.shape[0] < num_steps or kernel_clock.shape[2] != 2):
+                raise ValueError("kernel_clock must be a contiguous (>= num_steps, W, 2) tensor of 8-byte elements")
         b = Batch(num_states=states.shape[0], states=_ptr(states), agent_first=agent_first,
                   num_agents=num_agents, targets=_ptr(targets), refs=_ptr(refs),
                   nb_row_ptr=_ptr(nb_row_ptr), nb_col=_ptr(nb_col), x=_ptr(x),

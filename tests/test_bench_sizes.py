@@ -62,3 +62,22 @@ def test_default_uneven_world_falls_back_to_weak(bench, world):
     assert (total, per, first) == (4096 * world, 4096, 4096) and a.agents_total <= 0
     a = bench.parse(["--workload", "fov"])
     assert bench.workload_sizes(a, world, 0)[:2] == (512 * world, 512)
+
+
+def test_cpu_baseline_samples_timed_steps(bench, monkeypatch):
+    """cpu_baseline times the oracle on the trace's state tables of the timed steps (first and last
+    included), reports the per-step wall times, their p99 and the threads actually used."""
+    import numpy as np
+    from mpccbf import swarm
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(16)
+    traj = np.repeat(states[:, None, :], 9, axis=1)  # warm-up 3 + 5 timed steps (+ the initial table)
+    traj[:, :, 0] += np.arange(9)[None, :] * 0.01
+    a = bench.parse(["--warmup", "3", "--steps", "5"])
+    bench.workload_sizes(a, 1, 0)
+    cb = bench.cpu_baseline(cfg, states, targets, a, 3.0 * cfg["d_min"], None, dict(traj=traj))
+    assert cb["steps_sampled"][0] == 3 and cb["steps_sampled"][-1] == 7
+    assert len(cb["step_ms"]) == len(cb["steps_sampled"])
+    assert cb["cores"] == min(2, cb["affinity_cpus"])
+    assert cb["p99_step_ms"] <= max(cb["step_ms"]) + 1e-9 and cb["value"] > 0

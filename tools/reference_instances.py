@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--order", default="gauss_seidel")
     ap.add_argument("--out", default="")
     ap.add_argument("--modes", default="base,own")
+    ap.add_argument("--only", default="", help="comma-separated instance names (default: all 16)")
     args = ap.parse_args()
     from mpccbf import instances, metrics, sim
 
@@ -29,7 +30,8 @@ def main():
            "modes": {"base": "base_config.json overlaid (preprocess.py:21): the reference's runs",
                      "own": "the instance file's own parameters, missing keys from the base config"},
            "instances": {}}
-    for mode, name in [(m, nm) for m in args.modes.split(",") for nm in instances.names()]:
+    names = args.only.split(",") if args.only else instances.names()
+    for mode, name in [(m, nm) for m in args.modes.split(",") for nm in names]:
         cfg, states, targets, shape, kind, noise = instances.instance(name, preprocess=mode)
         t0 = time.perf_counter()
         try:
