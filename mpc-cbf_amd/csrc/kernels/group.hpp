@@ -28,6 +28,17 @@ __device__ __forceinline__ int lane_bits_opaque() {
     return r;
 }
 
+// A pointer into this block's LDS (a __shared__ array reached through a generic pointer) as a
+// volatile LDS-address-space pointer: reads and writes through it are ds_read / ds_write, never
+// re-used from registers. (A volatile generic pointer compiles to flat accesses with the
+// system-coherence bits, whose waits also wait for every global load in flight.)
+template <class T>
+using lds_vptr = volatile __attribute__((address_space(3))) T*;
+template <class T>
+__device__ __forceinline__ lds_vptr<T> lds_vol(T* p) {
+    return (lds_vptr<T>)p;
+}
+
 constexpr int DPP_XOR1 = 0xB1;         // quad_perm(1,0,3,2)
 constexpr int DPP_XOR2 = 0x4E;         // quad_perm(2,3,0,1)
 constexpr int DPP_HALF_MIRROR = 0x141; // row_half_mirror

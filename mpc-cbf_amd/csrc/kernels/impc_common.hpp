@@ -660,6 +660,9 @@ __device__ int stage_cbf_rows(const DevOps& op, const double* buf, const ImpcArg
                     npy = ns[1];
                     nvx = ns[3];
                     nvy = ns[4];
+                    // (keeps the two branches' reads apart: merged, the LDS and global reads
+                    // became one flat load through a selected pointer)
+                    asm volatile("" : "+v"(npx), "+v"(npy), "+v"(nvx), "+v"(nvy));
                 }
                 safety_cbf(e, npx, npy, nvx, nvy, op.d_min, a, b);
                 // max / min of -a^T u over the acceleration box at sample k (those box rows
@@ -767,6 +770,9 @@ __device__ int stage_cbf_rows_pairs(const DevOps& op, const double* buf, const I
                     npy = ns[1];
                     nvx = ns[3];
                     nvy = ns[4];
+                    // (keeps the two branches' reads apart: merged, the LDS and global reads
+                    // became one flat load through a selected pointer)
+                    asm volatile("" : "+v"(npx), "+v"(npy), "+v"(nvx), "+v"(nvy));
                 }
                 safety_cbf(e, npx, npy, nvx, nvy, op.d_min, a, b);
                 double bmax = 0.0, bmin = 0.0;
@@ -1041,9 +1047,9 @@ __device__ __forceinline__ void grid_clear(const ImpcArgs& args) {
 // wave on a shared counter serialised ~2,000 atomics and delayed the waves' first loads. Collision
 // kernels only: in the FoV kernels any clock code at the start moved the register allocation into
 // 36-108 B/lane of scratch
-__device__ __forceinline__ volatile unsigned long long* kclock_lds() {
+__device__ __forceinline__ lds_vptr<unsigned long long> kclock_lds() {
     __shared__ unsigned long long t0[16];  // one per wave of a block (<= 1024 threads)
-    return t0;
+    return lds_vol(t0);
 }
 __device__ __forceinline__ void kclock_start(const ImpcArgs& args) {
     (void)args;

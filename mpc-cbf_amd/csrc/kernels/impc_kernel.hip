@@ -457,16 +457,19 @@ struct SepRowsLds {
     double pad[(sizeof(SepRows<SB, CB>) / 8) % 2 == 0 ? 1 : 2];
 };
 
+// (lds: this group's 16 entries, one per lane)
 template <bool LDS, int SB, int CB>
 __device__ __forceinline__ SepRows<SB, CB>& pick_rows(SepRows<SB, CB>& reg, SepRowsLds<SB, CB>* lds) {
-    if constexpr (LDS) return lds[threadIdx.x].r;
+    if constexpr (LDS) return lds[threadIdx.x & 15u].r;
     else return reg;
 }
 
+// (force-inlined: instantiated by two kernels, an out-of-line call would copy the kernel arguments
+// to the stack at every launch's start)
 template <int SB, int CB, bool SLACK, bool QUEUE, bool LEAN = false>
-__device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
+__device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
                                const int ai, const int gl, double* stage, double* red, NbScratch& nbs,
-                               double* keep, SepRowsLds<SB, CB>* rows_lds = nullptr) {
+                               double* keep, SepRowsLds<SB, CB>* rows_lds = nullptr, double* bconst = nullptr) {
     constexpr int G = 16;
     constexpr int NZ = SEP_NZ;
     constexpr int cap = CB * G;  // CBF rows per agent
@@ -501,8 +504,8 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     auto agent = [&]() -> int { return ai; };
     double res[2];
 #else
-    auto agent = [&]() -> int { return *(volatile int*)(qk + NZ + 1); };
-    volatile double* res = qk + NZ + 2;
+    auto agent = [&]() -> int { return *lds_vol((int*)(qk + NZ + 1)); };
+    lds_vptr<double> res = lds_vol(qk + NZ + 2);
 #endif
 
     // ---- box rows: channel d, slot k -> row k * G + gl of that channel (packed by the host:
@@ -529,6 +532,18 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     }
     if (grid_mode) gq_states<G>(args, gq, gl);
     const bool infeasible = constant_rows_infeasible<G>(op, buf, s0, gl);
+    // the box rows' violation scales and candidate weights, formed once for both IMPC iterations'
+    // active-set solves (bconst: [2 SEP_D SB sides][16] doubles, then [SEP_D SB rows][16] floats)
+    double* bsc = nullptr;
+    float* bw = nullptr;
+#ifdef MPCCBF_NO_BOXC  // (A/B build: the constants formed by each solve)
+    bconst = nullptr;
+#endif
+    if (!SLACK && bconst != nullptr) {
+        bsc = bconst;
+        bw = (float*)(bconst + 16 * 2 * SEP_D * SB);
+        sep_box_consts<SB, CB>(rw, opp(buf, op.o_Pinv), bsc, bw);
+    }
     stamp(args, ai, gl, 1);
 
     int nb0 = 0, nnb = 0;
@@ -681,7 +696,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
             const int k0 = warm_count(it);
             const int r = sep_dual_as<G, SB, CB>(rw, live, opp(buf, op.o_Pr), Pi, q, yu, op.tol, op.dual_as, stage, y,
                                                  prs, drs, nit, nullptr, true, tl, nullptr, k0, act,
-                                                 it == 0 ? act : nullptr);
+                                                 it == 0 ? act : nullptr, nullptr, bsc, bw);
             if (r > 0) {
                 st = ST_OPTIMAL;
             } else if (r < 0 && tl > 10.0 * op.feas_tol) {
@@ -752,7 +767,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
                                                       ca, dbg, wslack, &vslack, red, &warm,
                                                       (attempt == 0 && warm_try) ? warm_delta : 0.0,
                                                       SLACK ? nullptr : stage, k0, SLACK ? nullptr : act,
-                                                      (!SLACK && attempt == 0 && it == 0) ? act : nullptr);
+                                                      (!SLACK && attempt == 0 && it == 0) ? act : nullptr, bsc, bw);
                 total += po.iters;
                 ((attempt == 0 && warm_try) ? tr_warm : tr_cold) += po.iters;
                 if (po.status == ST_OPTIMAL) break;
@@ -831,7 +846,7 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
         }
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {
-            objv = reduced_objective<NZ>(op, buf, q, y, qk[NZ]);
+            objv = sep_objective(opp(buf, op.o_Pr), q, y, qk[NZ]);
             if constexpr (SLACK) objv += grp_sum<G>(live ? wslack * vslack : 0.0);  // + w^T v
 #pragma unroll
             for (int i = 0; i < NZ; i++) ykeep[16 * i] = y[i];
@@ -852,25 +867,39 @@ __device__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf,
     stamp(args, ai, gl, 7);
 }
 
+// LDS of the separable pipeline per agent (doubles): CBF-row staging / the dual active set's
+// scratch, and the kept solution | warm duals | state | warm-start side ids | linear term
+template <int SB, int CB, bool SLACK>
+constexpr int sep_stage_doubles() {
+    return SLACK ? sep_pol_doubles<SB, CB>() + 16
+                 : (CB * 16 * (SEP_NZ + 1) > sep_pol_doubles<SB, CB>() ? CB * 16 * (SEP_NZ + 1)
+                                                                      : sep_pol_doubles<SB, CB>());
+}
+template <int SB, bool SLACK, bool LEAN>
+constexpr int sep_keep_doubles() {
+    return 16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 10;
+}
+
 // QUEUE = false: one agent per 16-lane group. QUEUE = true (fallback launch): the agents the main
 // launch deferred (args.queue: [count, blocks done, agents...]), one per group (the grid covers
 // every agent of the batch); the last block to finish empties the queue for the next step.
-template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = false>
+template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = false, bool LOOP = false>
 __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
                                                        const ImpcArgs args) {
     constexpr int GPB = BS / 16;
     // CBF-row staging, reused as the dual active set's scratch (sep_pol_doubles)
-    constexpr int STAGE = CB * 16 * (SEP_NZ + 1) > sep_pol_doubles<SB, CB>() ? CB * 16 * (SEP_NZ + 1)
-                                                                             : sep_pol_doubles<SB, CB>();
     // (slack mode: the slack-pattern active set's scratch + its multipliers, sep_slack_patterns)
-    __shared__ double stage_all[GPB][SLACK ? sep_pol_doubles<SB, CB>() + 16 : STAGE];
+    __shared__ double stage_all[GPB][sep_stage_doubles<SB, CB, SLACK>()];
     __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
     // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
     // set's warm-start side ids and their count (not in slack mode) | linear term and constant, the
     // agent index, the residuals
-    __shared__ double keep_all[GPB][16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 10];
-    __shared__ SepRowsLds<SB, CB> rows_lds[(QUEUE || SB > 1) ? BS : 1];
+    __shared__ double keep_all[GPB][sep_keep_doubles<SB, SLACK, LEAN>()];
+    constexpr bool rows_lds_per_lane = QUEUE || SB > 1;
+    __shared__ SepRowsLds<SB, CB> rows_lds[rows_lds_per_lane ? BS : 1];
+    // the box rows' constants per agent (sep_box_consts; not in slack mode)
+    __shared__ double bconst_all[SLACK ? 1 : GPB][SLACK ? 1 : 16 * 2 * SEP_D * SB + 8 * SEP_D * SB];
     const int gl = threadIdx.x & 15;
     const int gib = threadIdx.x / 16;
     lds_poison();
@@ -880,17 +909,32 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
         const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * GPB + gib;
         if (ai >= args.num_agents) return;
         impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
-                                                   nb_scratch[gib], keep_all[gib], rows_lds);
+                                                   nb_scratch[gib], keep_all[gib], rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
+                                                   SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
         kclock_end<BS>(args);
     } else {
-        // one queue entry per group (no grid-stride loop: carried across iterations the agent's
-        // state spills, 0 -> 352 B/lane); groups beyond the queue's length leave at once. The
+        // one queue entry per group, the grid covering every agent of the batch (LOOP: entries k,
+        // k + groups, ... per group from a grid of a few blocks — where deferrals are rare, so that
+        // an empty queue costs a small launch; carried across iterations, the pipeline's registers
+        // spill, on that rare path only). Groups beyond the queue's length leave at once. The
         // queue's header is zeroed by the main launch after next (the queues alternate by step
         // parity), so no block has to find out that it is the last one
-        const int k = blockIdx.x * GPB + gib;
-        if (k < args.queue[0])
-            impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
-                                                nb_scratch[gib], keep_all[gib], rows_lds);
+        const int k0 = blockIdx.x * GPB + gib;
+        if constexpr (LOOP) {
+            const int nq = args.queue[0];
+            for (int k = k0; k < nq; k += (int)gridDim.x * GPB) {
+                impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib],
+                                                    red_all[gib], nb_scratch[gib], keep_all[gib],
+                                                    rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
+                                                    SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
+                wave_lds_sync();  // (the group's LDS is rewritten by its next entry)
+            }
+        } else if (k0 < args.queue[0]) {
+            impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k0], gl, stage_all[gib], red_all[gib],
+                                                nb_scratch[gib], keep_all[gib],
+                                                rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
+                                                SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
+        }
     }
 }
 
@@ -1119,9 +1163,15 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
 // The operators (the buffer's hot prefix, DevOps::hot doubles) are staged into LDS once per block,
 // while the agents' state loads are in flight: every operator read of the agent chain is then an
 // LDS read (~100 cycles) instead of a scalar / vector memory round trip (~1,000 cycles under load).
+// (MPCCBF_WIDE_WPE: diagnostics builds with N waves per SIMD, registers capped at 512 / N)
+#ifdef MPCCBF_WIDE_WPE
+#define WIDE_WPE_ATTR __attribute__((amdgpu_waves_per_eu(MPCCBF_WIDE_WPE, MPCCBF_WIDE_WPE)))
+#else
+#define WIDE_WPE_ATTR
+#endif
 template <int BS>
-__global__ void __launch_bounds__(BS) impc_wide_kernel(const DevOps op, const double* __restrict__ buf,
-                                                        const ImpcArgs args) {
+__global__ void __launch_bounds__(BS) WIDE_WPE_ATTR impc_wide_kernel(const DevOps op, const double* __restrict__ buf,
+                                                                      const ImpcArgs args) {
     constexpr int WPB = BS / 64;
     constexpr int PER = WIDE_OPS / BS;
     __shared__ WideLds lds_all[WPB];
@@ -1149,6 +1199,10 @@ __global__ void __launch_bounds__(BS) impc_wide_kernel(const DevOps op, const do
 
 }  // namespace dev
 
+bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k);
+// blocks of the looping capacity launch (64 threads, 4 queue walkers each)
+constexpr int FALLBACK_LOOP_BLOCKS = 16;
+
 template <int NZ, int G, int R>
 static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                 hipStream_t s) {
@@ -1159,13 +1213,14 @@ static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcA
     return hipGetLastError();
 }
 
-template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false, bool LEAN = false>
+template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false, bool LEAN = false, bool LOOP = false>
 static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                     hipStream_t s) {
     constexpr int GPB = BS / 16;
     int blocks = (a.num_agents + GPB - 1) / GPB;
-    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE, LEAN>), dim3(blocks), dim3(BS), 0, s, op, buf,
-                       a);
+    if (LOOP) blocks = blocks < FALLBACK_LOOP_BLOCKS ? blocks : FALLBACK_LOOP_BLOCKS;
+    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE, LEAN, LOOP>), dim3(blocks), dim3(BS), 0, s, op,
+                       buf, a);
     return hipGetLastError();
 }
 
@@ -1214,7 +1269,9 @@ static bool sep_lean(const DevOps& op, int variant, int n) {
 //   otherwise — the full separable pipeline (dual active set, PDIP attempts, phase 1): with 16 CBF
 //   row slots when no agent can exceed them, else 8 slots per lane (128 rows). Agents beyond
 //   that report ERROR.
-hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide,
+//   rare — the one-agent-per-wave main launch when its 16 CBF lanes cannot be exceeded: only what
+//   its active set does not settle — a grid of FALLBACK_LOOP_BLOCKS blocks walks the queue.
+hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide, bool rare,
                                 hipStream_t s) {
     if (a.num_agents <= 0 || !a.queue) return hipSuccess;
     if (op.slack_mode) {
@@ -1222,7 +1279,14 @@ hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcA
         return launch_impc_sep_t<1, 2, true, 64, true>(op, buf, a, s);
     }
     if (wide) return launch_impc_sep_t<1, 8, false, 64, true>(op, buf, a, s);
+    if (rare) return launch_impc_sep_t<1, 1, false, 64, true, false, true>(op, buf, a, s);
     return launch_impc_sep_t<1, 1, false, 64, true>(op, buf, a, s);
+}
+
+// Whether the agents launch_impc defers are rare (the one-agent-per-wave kernel with at most 16
+// CBF rows per agent: only QPs its dual active set does not settle)
+bool impc_defer_rare(const DevOps& op, int variant, bool csr, int knn_k, int n) {
+    return use_wide(op, variant, n) && !impc_rows_may_exceed(op, csr, knn_k) && !op.slack_mode;
 }
 
 // Whether some agent can exceed the default separable kernel's 16 CBF row slots (caller lists,

@@ -334,6 +334,46 @@ __device__ bool sep_polish(const SepRows<SB, CB>& rw, bool has_cbf, const double
     return sep_eqp_finish<G, SB, CB, false>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm);
 }
 
+// reduced_objective (1/2 y^T P y + q^T y + k) with P block-diagonal by channel: the same sums in
+// the same order without the off-block terms, which add fma(0, y_j, s) = s — so bit-identical —
+// from 12 entries of P instead of 36
+__device__ __forceinline__ double sep_objective(const double* __restrict__ Pr, const double (&q)[SEP_NZ],
+                                                const double (&y)[SEP_NZ], double kconst) {
+    double v = kconst;
+#pragma unroll
+    for (int i = 0; i < SEP_NZ; i++) {
+        const int o = 2 * (i / 2);
+        const double pyi = fma(Pr[i * SEP_NZ + o + 1], y[o + 1], fma(Pr[i * SEP_NZ + o], y[o], 0.0));
+        v = fma(y[i], 0.5 * pyi + q[i], v);
+    }
+    return v;
+}
+
+// The box rows' constants of one agent, the same for both IMPC iterations (the rows' bounds are
+// shifted by the state, their coefficients and P^-1 fixed): per side the violation scale
+// 1 / (1 + |bound|) (bsc[s * 16 + lane], s = 2 (d SB + kk) + upper) and per row the candidate weight
+// 1 / sqrt(g P^-1 g) (bw[r * 16 + lane], r = d SB + kk) — sep_dual_as's own arithmetic, formed once
+// per agent into the group's LDS instead of at the start of every solve.
+template <int SB, int CB>
+__device__ __forceinline__ void sep_box_consts(const SepRows<SB, CB>& rw, const double* __restrict__ Pinv,
+                                               double* __restrict__ bsc, float* __restrict__ bw) {
+    const int gl = lane_bits_opaque<15>();
+    double pi[SEP_D][3];
+    sep_pinv(Pinv, pi);
+    int s = 0, r = 0;
+#pragma unroll
+    for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+        for (int kk = 0; kk < SB; kk++, r++) {
+            bsc[s * 16 + gl] = rcp(1.0 + fabs(rw.blo[d][kk]));
+            bsc[(s + 1) * 16 + gl] = rcp(1.0 + fabs(rw.bhi[d][kk]));
+            s += 2;
+            const double g0 = rw.bg[d][kk][0], g1 = rw.bg[d][kk][1];
+            const double n2 = fma(fma(pi[d][0], g0, 2.0 * pi[d][1] * g1), g0, pi[d][2] * g1 * g1);
+            bw[r * 16 + gl] = rsqrtf((float)fmax(n2, 1e-30));
+        }
+}
+
 // K = G_A P^-1 G_A^T of the k staged rows of pol (packed upper, identity beyond k)
 template <int NR>
 __device__ __forceinline__ void sep_gram(const double* __restrict__ pol, int k, double (&K)[Sym<NR>::P]) {
@@ -391,7 +431,8 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                            double* __restrict__ pol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
                            int& steps, SepWarm<SB>* warm, bool want_rd, double& tlow,
                            long long* dbg = nullptr, int k0 = 0, const double* __restrict__ warm_ids = nullptr,
-                           double* __restrict__ save = nullptr, double* __restrict__ mult = nullptr) {
+                           double* __restrict__ save = nullptr, double* __restrict__ mult = nullptr,
+                           const double* __restrict__ box_sc = nullptr, const float* __restrict__ box_w = nullptr) {
     static_assert(G == 16, "rows of pol are copied one column per lane");
     (void)dbg;
     GSTAMP(0, true);
@@ -412,13 +453,21 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     constexpr int NS = 2 * SEP_D * SB + CB;
     double sc[NS];  // violation scale 1 / (1 + |bound|) per side
     {
+        // the box sides' from the agent's constants (sep_box_consts: the same values, formed once
+        // for both IMPC iterations) when given
         int s = 0;
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
             for (int kk = 0; kk < SB; kk++) {
-                sc[s++] = rcp(1.0 + fabs(rw.blo[d][kk]));
-                sc[s++] = rcp(1.0 + fabs(rw.bhi[d][kk]));
+                if (box_sc != nullptr) {
+                    sc[s] = box_sc[s * 16 + gl];
+                    sc[s + 1] = box_sc[(s + 1) * 16 + gl];
+                } else {
+                    sc[s] = rcp(1.0 + fabs(rw.blo[d][kk]));
+                    sc[s + 1] = rcp(1.0 + fabs(rw.bhi[d][kk]));
+                }
+                s += 2;
             }
 #pragma unroll
         for (int c = 0; c < CB; c++) sc[s++] = rcp(1.0 + fabs(rw.chi[c]));
@@ -430,13 +479,16 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     // where this rule needs 4-8 (tools/das_sim.py, the same QPs in numpy). One weight per row
     // (both sides of a box row share it), formed once per solve into the scratch after the
     // staged rows (wrow[r * 16 + lane]); inert rows (g = 0) are never violated.
+    // (the box rows' weights from the agent's constants, box_w, when given)
     float* wrow = (float*)(pol + (POL_K + 1) * 16);
+    const float* __restrict__ wbox = box_w != nullptr ? box_w : wrow;
     {
         int r = 0;
 #pragma unroll
         for (int d = 0; d < SEP_D; d++)
 #pragma unroll
             for (int kk = 0; kk < SB; kk++, r++) {
+                if (box_w != nullptr) continue;
                 const double g0 = rw.bg[d][kk][0], g1 = rw.bg[d][kk][1];
                 const double n2 = fma(fma(pi[d][0], g0, 2.0 * pi[d][1] * g1), g0, pi[d][2] * g1 * g1);
                 wrow[r * 16 + gl] = rsqrtf((float)fmax(n2, 1e-30));
@@ -528,7 +580,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #pragma unroll
                 for (int kk = 0; kk < SB; kk++, r++) {
                     const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
-                    const double w = (double)wrow[r * 16 + gl];
+                    const double w = (double)wbox[r * 16 + gl];
                     const double al = rw.blo[d][kk] - t, vl = al * sc[s];
                     const double el = vl > add_tol ? al * w : -1.0;
                     if (el > eb) eb = el, sb = s;
@@ -565,6 +617,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         if (gl == owner) sep_stage_side<SB, CB>(rw, pi, sb, gl, cand);
         wave_lds_sync();
         GSTAMP(3, outer == 0);
+        GSTAMP(7, outer == 1);  // (the second step's: stamps 7, 4, 11, 5, 14)
         if (k == 0) {
             // first side of an empty active set: z = P^-1 n_p, the step reaches it (no factor yet),
             // and L = (sqrt(g_p P^-1 g_p))
@@ -637,7 +690,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                     rho[i] = s * dl[i];
                 }
             }
-            GSTAMP(4, outer == 0);
+            GSTAMP(4, steps == 2);
             double nw = 0.0, vv = 0.0, vp = 0.0;
 #pragma unroll
             for (int j = 0; j < SEP_NZ; j++) {
@@ -679,6 +732,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 return -1;
             }
             const double t = fmin(t1, t2);
+            GSTAMP(11, steps == 2);
             if (full) {
                 // primal direction z = P^-1 (n_p - N_A r), n = sign * g (rows re-read: the
                 // compiler barrier keeps them from staying live across the substitutions)
@@ -704,7 +758,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 u[i] = i < k ? fma(-t, sgn[i] * rho[i], u[i]) : u[i];
             up += t;
             wave_lds_sync();  // every lane has read the rows it is about to move
-            GSTAMP(5, outer == 0);
+            GSTAMP(5, steps == 2);
             if (t2 <= t1) {  // the candidate joins: L gains the row L^-1 c, diagonal sqrt(zn)
                 if (k == POL_K) return 0;
                 pol[k * 16 + gl] = cand[gl];
@@ -719,7 +773,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 }
                 k++;
                 wave_lds_sync();
-                GSTAMP(6, outer == 0);
+                GSTAMP(14, steps == 2);
                 break;
             }
             // side l leaves: the rows above it move down (one column per lane); K refactored
@@ -738,15 +792,19 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     // P y + q + G_A^T lam (lam = sign * u), checked whether or not the caller stores it (the
     // updates hold stationarity by construction, so the check only guards against rounding); a
     // non-finite iterate gives up
-    (void)want_rd;
-    {
+    // An empty active set returns the unconstrained minimiser -P^-1 q itself (finite: q and the
+    // rows were checked finite; P^-1 from the host), whose residual is that 2 x 2 solve's
+    // rounding: evaluated only when the caller stores it
+    if (k > 0) {
         bool nf = false;
 #pragma unroll
         for (int j = 0; j < SEP_NZ; j++) nf = nf || !isfinite(y[j]);
         if (grp_ballot<G>(nf) != 0ull) return 0;
     }
     double rd = 0.0, qn = 0.0;
-    if (k == 0) {  // (group-uniform) the unconstrained minimiser, most QPs: P y + q alone
+    if (k == 0 && !want_rd) {
+        // (rd = 0: not stored, and below the tolerance by construction)
+    } else if (k == 0) {  // (group-uniform) the unconstrained minimiser, most QPs: P y + q alone
 #pragma unroll
         for (int o = 0; o < SEP_NZ; o++) {
             const int d = o / 2;
@@ -850,7 +908,8 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                                   double wv_cost = 0.0, double* v_out = nullptr, double* red = nullptr,
                                   SepWarm<SB>* warm = nullptr, double warm_delta = 0.0,
                                   double* pol = nullptr, int das_k0 = 0, const double* das_ids = nullptr,
-                                  double* das_save = nullptr) {
+                                  double* das_save = nullptr, const double* box_sc = nullptr,
+                                  const float* box_w = nullptr) {
     (void)dbg;
     const bool slk = SLACK && has_cbf;  // group-uniform
     GSTAMP(12, true);
@@ -926,7 +985,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 double yg[SEP_NZ], rpg = 0.0, rdg = 0.0, tlg = 0.0;
                 const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, Pinv, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
                                                      rdg, as_steps, nullptr, cfg.want_rd, tlg, dbg, das_k0, das_ids,
-                                                     das_save);
+                                                     das_save, nullptr, box_sc, box_w);
                 if (r != 0) {
                     PdipOut fo{r > 0 ? ST_OPTIMAL : ST_UNKNOWN, as_steps};
 #pragma unroll

@@ -9,7 +9,7 @@ so the effective parameters of every instance are the base config's; start veloc
 
 parse_config() reads the sections like common/parsing.hpp:20-214 (same keys, same validation
 messages) into the dict mpccbf.Context takes; overlay() is preprocess.py:21; instance() returns one
-instance of tests/golden/reference_instances.json (the 16 baseline instances, transcribed as data
+instance of mpccbf/data/reference_instances.json (the 16 baseline instances, transcribed as data
 by tests/golden/make_reference_instances.py) ready for mpccbf.sim.Simulator.
 """
 from __future__ import annotations
@@ -21,8 +21,8 @@ import numpy as np
 
 from . import swarm
 
-FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests", "golden",
-                       "reference_instances.json")
+# the instances as data beside the package (written by tests/golden/make_reference_instances.py)
+FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "reference_instances.json")
 
 
 def _req(js: dict, *path):

@@ -1,4 +1,4 @@
-"""Transcribe the reference's own experiment instances as data (tests/golden/reference_instances.json).
+"""Transcribe the reference's own experiment instances as data (mpc-cbf_amd/mpccbf/data/reference_instances.json).
 
 Source: /root/reference/workspace/experiments/config/baseline/{2r,3r,5r,6r,8r}/*.json (the 16
 instances the example reads, MPCCBFFormationControl_example.cpp:43-44,97-117; CI runs 2r/line.json,
@@ -14,7 +14,8 @@ import json
 import os
 
 REF = "/root/reference/workspace/experiments/config"
-OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "reference_instances.json")
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "mpc-cbf_amd", "mpccbf", "data",
+                   "reference_instances.json")
 
 
 def main():

@@ -200,6 +200,50 @@ def test_separable_and_dense_layouts_agree(mpclib):
     assert np.nanmax(np.abs(res[0]["x"] - res[3]["x"])) <= 1e-6
 
 
+@pytest.mark.parametrize("scale,steps", [(1.0, 25), (0.55, 12), (0.42, 6)])
+def test_wide_and_16lane_layouts_agree(mpclib, scale, steps):
+    """The share-adaptive default picks the one-agent-per-wave kernel (variant 5) up to one agent
+    per SIMD and the 16-lane kernel (variant 4) beyond, so the same QPs must not depend on the
+    layout: on a closed-loop-evolved 1024-agent table (both layouts run from the same states),
+    equal statuses, objectives within 1e-7 relative and control points within 1e-6 (the two
+    layouts' active-set paths can differ — float-keyed vs double candidate scores — and reach the
+    same optimum through different factor updates: measured up to 1.6e-8)."""
+    torch = _torch()
+    dev = torch.device("cuda", 0)
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(1024, seed=21)
+    states[:, :2] *= scale
+    tg = torch.tensor(targets, device=dev)
+    # evolve the table with the default kernel (the bench's noise), then solve it with both layouts
+    ctx = mpclib.Context(cfg)
+    cur = torch.tensor(states, device=dev)
+    alt = torch.empty_like(cur)
+    out = ctx.alloc_outputs(len(states))
+    traj_t = torch.full((len(states),), -1.0, dtype=torch.float64, device=dev)
+    r = ctx.run_steps(cur, alt, steps, targets=tg, knn_k=8, knn_radius=6.0, x=out["x"], obj=out["obj"],
+                      traj_t=traj_t, pos_std=0.001, vel_std=0.01, noise_seed=7)
+    table = r["final"].clone()
+    res, names = {}, {}
+    for variant in (4, 5):
+        c = mpclib.Context(cfg)
+        c.set_variant(variant)
+        o = c.alloc_outputs(len(states))
+        c.impc_solve(table, targets=tg, knn_k=8, knn_radius=6.0, **o)
+        torch.cuda.synchronize()
+        res[variant] = {k: v.cpu().numpy() for k, v in o.items()}
+        names[variant] = c.kernel_name
+    assert names == {4: "impc_sep_kernel<1,1,false,256>", 5: "impc_wide_kernel<256>"}, names
+    a, b = res[4], res[5]
+    np.testing.assert_array_equal(a["status"], b["status"])
+    ok = a["status"] == 0
+    assert ok.sum() > 0
+    err = np.abs(a["obj"][ok] - b["obj"][ok]) / np.maximum(1.0, np.abs(a["obj"][ok]))
+    assert err.max() <= 1e-7, err.max()
+    assert np.nanmax(np.abs(a["x"] - b["x"])) <= 1e-6, np.nanmax(np.abs(a["x"] - b["x"]))
+    if scale < 1.0:  # (the crowded tables have active CBF rows: the solves are not all fast starts)
+        assert np.count_nonzero(a["iters"] > 0) > 10
+
+
 def test_nb_out_written_by_every_collision_kernel(mpclib):
     """mpccbf_batch.nb_out (the neighbour list each agent's QPs were built from) from the generic
     dense-layout kernel (variant 3) equals the separable kernels' (variants 4 and 5) on the same

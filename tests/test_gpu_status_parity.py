@@ -86,11 +86,17 @@ def test_regression_cases_match_oracle(mpclib):
                       lists={0: np.arange(1, n, dtype=np.int32)})
 
 
-@pytest.mark.parametrize("snaps", [(16, 20, 27)])
-def test_bench_workload_statuses_match_oracle(mpclib, snaps):
+@pytest.mark.parametrize("n,snaps,kernel", [
+    (4096, (16, 20, 27), "impc_sep_kernel<1,1,false,256>"),
+    # config 4's rank share: the default variant runs the one-agent-per-wave kernel, whose
+    # deferrals (more active sides, the PDIP, phase 1) go to the capacity launch
+    (1024, (16, 20, 27, 40), "impc_wide_kernel<256>")])
+def test_bench_workload_statuses_match_oracle(mpclib, n, snaps, kernel):
+    """Every non-OPTIMAL agent and a seeded sample of 256 OPTIMAL ones of the closed-loop-evolved
+    swarm against the oracle, at the launch size of config 3 (the 16-lane kernel) and of config
+    4's rank share (the default variant's one-agent-per-wave kernel)."""
     torch = _torch()
     cfg = swarm.config(15)
-    n = 4096
     states_h, targets_h = swarm.lattice_swarm(n)
     dev = torch.device("cuda", 0)
     ctx = mpclib.Context(cfg)
@@ -123,6 +129,7 @@ def test_bench_workload_statuses_match_oracle(mpclib, snaps):
             advance(1)
             saved[b] = (st_in, out["obj"].cpu().numpy().copy())
     torch.cuda.synchronize()
+    assert ctx.kernel_name == kernel, ctx.kernel_name
     slog = status_log.cpu().numpy()
     ilog = iters_log.cpu().numpy()
     attempted = ~((slog == 5) & (ilog == 0))

@@ -50,7 +50,10 @@ def main():
         ok, makespan, hit = metrics.instance_success(traj, targets, 1.0, shape, kind)
         st = np.array(s.status_log)
         fin = np.linalg.norm(traj[:, -1, :2] - targets[:, :2], axis=1)
+        # first step at which some robot's iteration-0 QP turns from OPTIMAL to INFEASIBLE
+        tr = np.argwhere((st[:-1, :, 0] == 0) & (st[1:, :, 0] == 3))
         r = {"robots": len(states), "steps": len(st), "success": bool(ok),
+             "first_opt_to_infeasible_step": int(tr[0, 0] + 1) if len(tr) else None,
              "makespan_records": None if not np.isfinite(makespan) else int(makespan),
              "first_collision": hit, "min_pair_distance_m": metrics.min_pair_distance(traj),
              "goals_reached_at_end": int(np.sum(fin <= 1.0)), "max_final_goal_dist_m": float(fin.max()),

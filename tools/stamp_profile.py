@@ -83,13 +83,18 @@ for v in VARIANTS:
                  ("scan 2", 6, 8), ("dual residual", 8, 9), ("exit", 9, 10)]
         names0 = [("solver entry", 12, 13), ("call", 13, 0), ("init", 0, 1),
                   ("scan/fast start", 1, 2), ("converged", 2, 9), ("exit", 9, 10)]
+        # the second step (k = 1 -> 2, the general step with substitutions) of two-step solves
+        names2 = [("solver entry", 12, 13), ("call", 13, 0), ("init", 0, 1),
+                  ("scan 1/fast start", 1, 2), ("stage 1", 2, 3), ("first side", 3, 6),
+                  ("scan 2", 6, 8), ("stage 2", 8, 7), ("subst v, rho", 7, 4), ("step lengths", 4, 11),
+                  ("update y, u", 11, 5), ("join", 5, 14), ("scan 3 + rd", 14, 9), ("exit", 9, 10)]
         for nstep in (0, 1, 2):
             m = (ps[:, 15] == 1) & (its0 == nstep) & (ps[:, 10] > 0)
             if m.sum() == 0:
                 continue
             print(f"variant {v}: dual active-set solves with {nstep} step(s): {m.sum()} agents, "
                   f"cycles entry->exit mean {np.mean(ps[m, 10] - ps[m, 12]):.0f}")
-            for name, a, b in (names0 if nstep == 0 else names):
+            for name, a, b in (names0 if nstep == 0 else (names2 if nstep == 2 else names)):
                 d = ps[m, b] - ps[m, a]
                 print(f"   {name:15s} mean {d.mean():7.0f}  p50 {np.median(d):7.0f} cycles")
     if PDIP and v == 0 and FOV:  # the wave dual active set's stamps (das_wave.hpp, solve 0)
