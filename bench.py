@@ -68,6 +68,8 @@ def parse(argv=None):
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--das-warm", type=int, default=0,
                     help="mpccbf_options.das_warm_steps (0 = default 3; < 0 = no IMPC iteration-1 warm start)")
+    ap.add_argument("--lean", action="store_true",
+                    help="diagnostics: mpccbf_options.lean (main launch without the PDIP; a fallback launch per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--loop", choices=["native", "python"], default="native",
                     help="native: mpccbf_run_steps (C++ loop, RCCL); python: one call per step")
@@ -270,7 +272,7 @@ def main():
     # neighbour-estimate covariances (FoV slack weights): the FoV example's 0.1 I for everyone
     cov_h = np.tile([0.1, 0.0, 0.1], (total, 1)) if (fov and args.slack) else None
     cov = None if cov_h is None else torch.tensor(cov_h, dtype=torch.float64, device=dev)
-    ctx = Context(cfg, device=local, das_warm_steps=args.das_warm)
+    ctx = Context(cfg, device=local, das_warm_steps=args.das_warm, lean=args.lean)
     ctx.set_variant(args.variant)
 
     targets = torch.tensor(targets_h[first:first + per], dtype=torch.float64, device=dev)

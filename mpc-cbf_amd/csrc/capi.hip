@@ -31,9 +31,8 @@ int impc_clock_waves(const DevOps& op, int variant, int n);
 hipError_t launch_impc_fov(const DevOps& op, const double* buf, const ImpcArgs& a, hipStream_t s);
 hipError_t launch_fov_rows_eval(int count, const double* ego, const double* nb, double fov, double Ds, double Rs,
                                 double bbx, double bby, double* vor, double* rows, hipStream_t s);
-hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide, bool rare,
+hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide,
                                 hipStream_t s);
-bool impc_defer_rare(const DevOps& op, int variant, bool csr, int knn_k, int n);
 bool impc_may_defer(const DevOps& op, int variant, bool csr, int knn_k, int n);
 bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k);
 int launch_neighbors(const double* states, int num_states, int first, int num_agents, int k,
@@ -227,8 +226,7 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
         f.defer_clear = nullptr;
         f.kclock = nullptr;  // (the clock is the main launch's)
         f.queue = q_this;
-        e = launch_impc_fallback(c->dev, c->dbuf, f, impc_rows_may_exceed(c->dev, !grid, b->knn_k),
-                                 impc_defer_rare(c->dev, c->variant, !grid, b->knn_k, b->num_agents), stream);
+        e = launch_impc_fallback(c->dev, c->dbuf, f, impc_rows_may_exceed(c->dev, !grid, b->knn_k), stream);
         // (a queue the fallback never read is zeroed by the main launch after next)
     }
     if (e == hipSuccess && ev1) e = hipEventRecord(ev1, stream);

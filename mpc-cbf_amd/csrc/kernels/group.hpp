@@ -85,6 +85,15 @@ template <int CTRL>
 __device__ __forceinline__ unsigned dpp_u32(unsigned v) {
     return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
 }
+// max over a 16-lane row (every lane ends with it): DPP moves fused into v_max_u32
+__device__ __forceinline__ unsigned row_max_u32(unsigned v) {
+    v = max(v, dpp_u32<DPP_XOR1>(v));
+    v = max(v, dpp_u32<DPP_XOR2>(v));
+    v = max(v, dpp_u32<DPP_HALF_MIRROR>(v));
+    v = max(v, dpp_u32<DPP_MIRROR>(v));
+    return v;
+}
+
 __device__ __forceinline__ unsigned wave_max_u32(unsigned v) {
     v = max(v, dpp_u32<DPP_XOR1>(v));
     v = max(v, dpp_u32<DPP_XOR2>(v));

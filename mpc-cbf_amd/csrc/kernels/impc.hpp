@@ -82,8 +82,10 @@ constexpr int SEP_ROW = 10;
 constexpr int SEP_NZD_HOST = 2;  // reduced variables per channel the separable kernel handles
 
 // Spatial hash of agent positions (uniform cells of edge `radius`) with fixed-capacity buckets:
-// bucket h holds the state rows slots[j*T + h], j < cnt[h], in insertion order (slot-major: the
-// first slots of all buckets are one dense T-word plane, so the table's touched lines stay few)
+// bucket h holds the state rows slots[h * GRID_CAP + j], j < cnt[h], in insertion order
+// (bucket-major, round 6: a query touches one line of a cell's entries and two of its slot states;
+// slot-major, the one-agent-per-wave query's unconditional loads of the 3 x 3 cells' 7 inline
+// slots touched 63 entry lines and 63 state lines in 7 planes)
 // (cnt[h] > GRID_CAP: overflow, an agent reading that bucket scans the whole state table
 // instead, so the neighbour sets never depend on the capacity). Filled by atomics, so no
 // scan: mpccbf_run_steps rotates three tables (read this step | filled with this step's next
@@ -92,11 +94,15 @@ constexpr int GRID_CAP = 64;
 // The first GRID_SST slots of every bucket also carry their row's planar state (px, py, vx, vy):
 // a query reads the 3 x 3 cells' counts, entries and states in one round trip (impc_wide.hpp)
 constexpr int GRID_SST = 7;
+constexpr int GRID_SSTR = 8;  // slot states per bucket in the state plane (GRID_SST, padded to 256 B)
+// bucket h's slot j in the entry table and in the state plane (double4 index)
+__host__ __device__ inline uint32_t grid_slot_at(uint32_t h, uint32_t j) { return h * (uint32_t)GRID_CAP + j; }
+__host__ __device__ inline uint32_t grid_sst_at(uint32_t h, uint32_t j) { return h * (uint32_t)GRID_SSTR + j; }
 
 struct GridArgs {
     const uint32_t* cnt;   // T bucket counts of the table read this step
-    const uint32_t* slots; // GRID_CAP x T state rows (slot-major)
-    const double* sst;     // GRID_SST x T x 4: slot j < GRID_SST's (px, py, vx, vy) (slot-major)
+    const uint32_t* slots; // T x GRID_CAP state rows (bucket-major, grid_slot_at)
+    const double* sst;     // T x GRID_SSTR x 4: slot j < GRID_SST's (px, py, vx, vy) (grid_sst_at)
     uint32_t* ins_cnt;     // table of the next step (NULL: none): next_states rows are inserted
     uint32_t* ins_slots;
     double* ins_sst;
@@ -122,10 +128,9 @@ __host__ __device__ inline uint32_t cell_hash(long long cx, long long cy, uint32
 __device__ inline void grid_insert(const GridArgs& g, double x, double y, double vx, double vy, uint32_t row) {
     const uint32_t h = cell_hash((long long)floor(x * g.inv_cell), (long long)floor(y * g.inv_cell), g.mask);
     const uint32_t j = atomicAdd(&g.ins_cnt[h], 1u);
-    const size_t e = (size_t)j * (g.mask + 1u) + h;
-    if (j < (uint32_t)GRID_CAP) g.ins_slots[e] = row;
+    if (j < (uint32_t)GRID_CAP) g.ins_slots[grid_slot_at(h, j)] = row;
     if (j < (uint32_t)GRID_SST) {
-        double4* d = reinterpret_cast<double4*>(g.ins_sst) + e;
+        double4* d = reinterpret_cast<double4*>(g.ins_sst) + grid_sst_at(h, j);
         *d = make_double4(x, y, vx, vy);
     }
 }

@@ -90,7 +90,7 @@ __device__ __forceinline__ int grid_neighbors_stream(const ImpcArgs& args, int s
                 uint32_t e = 0;
 #pragma unroll
                 for (int c = 0; c < 9; c++)  // the cell whose range holds t
-                    if (off[c] <= t && t - off[c] < nc[c]) e = (t - off[c]) * (gr.mask + 1u) + hs[c];
+                    if (off[c] <= t && t - off[c] < nc[c]) e = grid_slot_at(hs[c], t - off[c]);
                 j = (int)gr.slots[e];
             }
             nx = args.states[(size_t)j * 6];
@@ -209,7 +209,7 @@ __device__ __forceinline__ uint32_t gq_entry(const GridArgs& gr, const GridQuery
 #pragma unroll
     for (int c = 0; c < 9; c++) {  // the cell whose range holds t
         const uint32_t u = t - q.off[c];
-        e = ((q.off[c] <= t) & (u < q.nc[c])) ? u * (gr.mask + 1u) + q.hs[c] : e;
+        e = ((q.off[c] <= t) & (u < q.nc[c])) ? grid_slot_at(q.hs[c], u) : e;
     }
     return (t < q.total && !q.full) ? e : 0u;
 }
@@ -841,6 +841,15 @@ __device__ __forceinline__ double normal_sample(uint64_t seed, int64_t step, int
     return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
 }
 
+// The closed-loop noise draws of the kept curve's next state (normal_sample(..., comp, 0), comp =
+// lane < 6), formed at the start of the agent (they depend on the seed, step and agent alone: the
+// transcendental chain overlaps the setup's loads instead of closing the agent) into noise0[0..6)
+__device__ __forceinline__ void early_noise(const ImpcArgs& args, int ai, int gl, double* noise0) {
+    if (args.traj_t == nullptr || gl >= 6) return;
+    const double sd = gl < 3 ? args.pos_std : args.vel_std;
+    if (sd > 0.0) noise0[gl] = normal_sample(args.noise_seed, args.step_index, args.agent_first + ai, gl);
+}
+
 // Component comp (0..2 position x/y/yaw, 3..5 velocity) at parameter t of a piecewise Bezier
 // curve (SingleParameterPiecewiseCurve::eval, SingleParameterPiecewiseCurve.cpp:94-127:
 // lower_bound piece lookup, local parameter min(T, t - cum[i-1]); Bezier::eval with the
@@ -911,7 +920,7 @@ template <int NZ, int G, bool FIXED = true, bool AZE = true>
 __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const double* buf,
                                                     const ImpcArgs& args, int ai, int gl,
                                                     const double (&s0)[6], const double (&yk)[NZ],
-                                                    bool have_curve) {
+                                                    bool have_curve, const double* noise0 = nullptr) {
     const bool sim = args.traj_t != nullptr;
     const double t_stored = sim ? args.traj_t[ai] : 0.0;  // (loaded here: in flight during the x rows)
     // this step's control points x = Xs s0 + Z y to args.x, XU rows per lane at a time (their loads
@@ -974,7 +983,8 @@ __device__ __forceinline__ void write_agent_outputs(const DevOps& op, const doub
                     args.substeps[((size_t)ai * op.nsub + k - 1) * 6 + gl] = u;
                 }
             }
-            if (sd > 0.0) v = fma(sd, normal_sample(args.noise_seed, args.step_index, agent, gl), v);
+            if (sd > 0.0)
+                v = fma(sd, noise0 != nullptr ? noise0[gl] : normal_sample(args.noise_seed, args.step_index, agent, gl), v);
         } else {
             // no trajectory yet: hold the position at zero velocity, with each sub-step's noise
             // added to the previous sub-step's state (example :210-216): the position draws
@@ -1087,7 +1097,15 @@ __device__ __forceinline__ void stamp(const ImpcArgs& args, int ai, int gl, int 
 __device__ __forceinline__ void write_nb_out(const ImpcArgs& args, int ai, int gl, bool grid_mode,
                                              const NbScratch& nbs, int nb0, int nnb) {
     if (!args.nb_out || gl >= 16) return;
-    const int v = gl < nnb ? (grid_mode ? nbs.idx[gl] : args.nb_col[nb0 + gl]) : -1;
+    int v = -1;
+    if (gl < nnb) {
+        if (grid_mode) {
+            v = nbs.idx[gl];
+        } else {
+            v = args.nb_col[nb0 + gl];
+            asm volatile("" : "+v"(v));  // (the two reads kept apart: merged, one flat load)
+        }
+    }
     args.nb_out[(size_t)ai * 16 + gl] = v;
 }
 

@@ -62,6 +62,9 @@ __device__ __forceinline__ void nb_position(const ImpcArgs& args, const NbScratc
         const int nbi = args.nb_col[nb0 + i];
         px = args.states[(size_t)nbi * 6];
         py = args.states[(size_t)nbi * 6 + 1];
+        // (keeps the two branches' reads apart: merged, the LDS and global reads became one flat
+        // load through a selected pointer)
+        asm volatile("" : "+v"(px), "+v"(py));
     }
 }
 
@@ -91,6 +94,8 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     double s0[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) s0[k] = args.states[(size_t)self * 6 + k];
+    __shared__ double noise0[8];  // the next state's noise draws, while the state is in flight
+    early_noise(args, ai, lane, noise0);
     // grid mode: the neighbour query's loads are staged between the setup's (gq_*; the state
     // arrives before the branch, else the join waits for every load in flight)
     const bool grid_mode = args.nb_row_ptr == nullptr;
@@ -264,7 +269,13 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         // weight of neighbour i is slack_cost * decay^{idx[i]}, idx = the sorted list of indices
         // (the reference's indexing, kept). Unknown covariances (args.cov == NULL) are infinite.
         if (lane < nnb) {
-            const int nbi = grid_mode ? nb_scratch.idx[lane] : args.nb_col[nb0 + lane];
+            int nbi;
+            if (grid_mode) {
+                nbi = nb_scratch.idx[lane];
+            } else {
+                nbi = args.nb_col[nb0 + lane];
+                asm volatile("" : "+v"(nbi));  // (the two reads kept apart: merged, one flat load)
+            }
             const double* cv = args.cov ? args.cov + (size_t)nbi * 3 : nullptr;
             slk->dist[lane] = cv ? distance_to_ellipse(s0[0], s0[1], args.states[(size_t)nbi * 6],
                                                        args.states[(size_t)nbi * 6 + 1], cv[0], cv[1], cv[2])
@@ -780,7 +791,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         double yk[NZ];
 #pragma unroll
         for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
-        write_agent_outputs<NZ, 64, !SLACK, false>(op, buf, args, ai, lane, s0, yk, have_curve);
+        write_agent_outputs<NZ, 64, !SLACK, false>(op, buf, args, ai, lane, s0, yk, have_curve, noise0);
     }
     // (diagnostics; here, not after the query: there it pushed the kernel into scratch)
     write_nb_out(args, ai, lane, grid_mode, nb_scratch, nb0, nnb);

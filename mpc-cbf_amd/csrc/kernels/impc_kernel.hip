@@ -457,6 +457,19 @@ struct SepRowsLds {
     double pad[(sizeof(SepRows<SB, CB>) / 8) % 2 == 0 ? 1 : 2];
 };
 
+// LDS of the separable pipeline per agent (doubles): CBF-row staging / the dual active set's
+// scratch, and the kept solution | warm duals | state | warm-start side ids | linear term
+template <int SB, int CB, bool SLACK>
+constexpr int sep_stage_doubles() {
+    return SLACK ? sep_pol_doubles<SB, CB>() + 16
+                 : (CB * 16 * (SEP_NZ + 1) > sep_pol_doubles<SB, CB>() ? CB * 16 * (SEP_NZ + 1)
+                                                                      : sep_pol_doubles<SB, CB>());
+}
+template <int SB, bool SLACK, bool LEAN>
+constexpr int sep_keep_doubles() {
+    return 16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 10 + 6;
+}
+
 // (lds: this group's 16 entries, one per lane)
 template <bool LDS, int SB, int CB>
 __device__ __forceinline__ SepRows<SB, CB>& pick_rows(SepRows<SB, CB>& reg, SepRowsLds<SB, CB>* lds) {
@@ -466,8 +479,10 @@ __device__ __forceinline__ SepRows<SB, CB>& pick_rows(SepRows<SB, CB>& reg, SepR
 
 // (force-inlined: instantiated by two kernels, an out-of-line call would copy the kernel arguments
 // to the stack at every launch's start)
-template <int SB, int CB, bool SLACK, bool QUEUE, bool LEAN = false>
-__device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
+// INPL (with LEAN): an agent the lean solve does not settle is not deferred to the fallback launch;
+// the function returns true and the caller runs the full pipeline for it in place
+template <int SB, int CB, bool SLACK, bool QUEUE, bool LEAN = false, bool INPL = false>
+__device__ __forceinline__ bool impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
                                const int ai, const int gl, double* stage, double* red, NbScratch& nbs,
                                double* keep, SepRowsLds<SB, CB>* rows_lds = nullptr, double* bconst = nullptr) {
     constexpr int G = 16;
@@ -479,6 +494,9 @@ __device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* _
     double s0[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) s0[i] = args.states[(size_t)self * 6 + i];
+    // the next state's noise draws, while the state is in flight (the keep area's last 6 doubles)
+    double* const noise0 = keep + sep_keep_doubles<SB, SLACK, LEAN>() - 6;
+    early_noise(args, ai, gl, noise0);
     // grid mode: the neighbour query's loads are staged between the setup's (gq_*)
     const bool grid_mode = args.nb_row_ptr == nullptr;
     GridQuery<G> gq;
@@ -556,7 +574,7 @@ __device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* _
     write_nb_out(args, ai, gl, grid_mode, nbs, nb0, nnb);
     if (SLACK && !QUEUE && nnb > G && args.defer) {  // slack mode: beyond one lane per neighbour
         defer_agent(args, agent(), gl);
-        return;
+        return false;
     }
     const bool nb_overflow = nnb < 0 || (SLACK && !QUEUE && nnb > G);
     if (nb_overflow) nnb = 0;
@@ -655,8 +673,22 @@ __device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* _
         if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
         if (count > cap && args.defer) {  // beyond this instantiation: the fallback launch solves it
             defer_agent(args, agent(), gl);
-            return;
+            return false;
         }
+#ifdef MPCCBF_PDIP_STAMPS  // (profiling build: the solve phase's parts around the solver, slots 16 ..)
+        long long* const dbgs = (args.stamps && it == 0)
+                                    ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)ai * 32
+                                    : nullptr;
+#define SSTAMP(k)                                                                \
+    do {                                                                         \
+        if (dbgs) dbgs[k] = (long long)__builtin_amdgcn_s_memtime();             \
+    } while (0)
+#else
+#define SSTAMP(k) \
+    do {          \
+    } while (0)
+#endif
+        SSTAMP(16);
         int st;
         int nit = 0;
         if (gl == 0) res[0] = res[1] = __builtin_nan("");
@@ -674,6 +706,7 @@ __device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* _
             nfin = nfin || !isfinite(rw.chi[c]) || !isfinite(rw.cg[c][0]) || !isfinite(rw.cg[c][1]) ||
                    !isfinite(rw.cg[c][2]) || !isfinite(rw.cg[c][3]);
         const bool nonfinite = grp_ballot<G>(nfin) != 0ull;
+        SSTAMP(17);
         if (count > cap || nb_overflow || slack_overflow || nonfinite) {
             st = ST_ERROR;
         } else if (infeasible || row_infeasible) {
@@ -704,14 +737,15 @@ __device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* _
                 prs = tl;
                 drs = __builtin_nan("");
             } else {
+                if constexpr (INPL) return true;  // (the caller's full pipeline solves it)
                 defer_agent(args, agent(), gl);
-                return;
+                return false;
             }
             if (gl == 0) res[0] = prs, res[1] = drs;
         } else {
 #ifdef MPCCBF_PDIP_STAMPS
             long long* dbg = (args.stamps && it == 0)
-                                 ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)agent() * 16
+                                 ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP + (size_t)agent() * 32
                                  : nullptr;
 #elif defined(MPCCBF_SOLVE_TRACE)  // per-step (rp, mu, alpha, rd) of the first solve + phase 1
             long long* dbg = args.stamps ? (long long*)args.stamps + (size_t)args.num_agents * NSTAMP +
@@ -762,6 +796,7 @@ __device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* _
                 ca.robust = attempt == 2;
                 ca.dual_as = attempt == 0 ? op.dual_as : 0;
                 ca.want_rd = args.dual_res != nullptr;
+                ca.want_rp = args.primal_res != nullptr;
                 const int k0 = attempt == 0 ? warm_count(it) : 0;
                 po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_Pinv), q, y,
                                                       ca, dbg, wslack, &vslack, red, &warm,
@@ -844,58 +879,53 @@ __device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* _
             (void)tr_warm, (void)tr_cold;
 #endif
         }
+        SSTAMP(18);
         double objv = __builtin_nan("");
         if (st == ST_OPTIMAL) {
             objv = sep_objective(opp(buf, op.o_Pr), q, y, qk[NZ]);
             if constexpr (SLACK) objv += grp_sum<G>(live ? wslack * vslack : 0.0);  // + w^T v
+            SSTAMP(19);
 #pragma unroll
             for (int i = 0; i < NZ; i++) ykeep[16 * i] = y[i];
             have_curve = true;
         } else {
             success = false;
         }
+        SSTAMP(20);
         write_iteration(args, oi, gl, st, objv, nit, res[0], res[1]);
+        SSTAMP(21);
         if (it == 0) steps0 = nit;
         if (it < 2) stamp(args, ai, gl, 4 + 2 * it);
         wave_lds_sync();
+#undef SSTAMP
     }
     double yk[NZ], sx[6];
 #pragma unroll
     for (int i = 0; i < NZ; i++) yk[i] = ykeep[16 * i];
     load_state_lds(s0k, sx);
-    write_agent_outputs<NZ, G>(op, buf, args, agent(), gl, sx, yk, have_curve);
+    write_agent_outputs<NZ, G>(op, buf, args, agent(), gl, sx, yk, have_curve, noise0);
     stamp(args, ai, gl, 7);
-}
-
-// LDS of the separable pipeline per agent (doubles): CBF-row staging / the dual active set's
-// scratch, and the kept solution | warm duals | state | warm-start side ids | linear term
-template <int SB, int CB, bool SLACK>
-constexpr int sep_stage_doubles() {
-    return SLACK ? sep_pol_doubles<SB, CB>() + 16
-                 : (CB * 16 * (SEP_NZ + 1) > sep_pol_doubles<SB, CB>() ? CB * 16 * (SEP_NZ + 1)
-                                                                      : sep_pol_doubles<SB, CB>());
-}
-template <int SB, bool SLACK, bool LEAN>
-constexpr int sep_keep_doubles() {
-    return 16 * (SEP_NZ + (LEAN ? 0 : 2 * SEP_D * SB)) + 8 + (SLACK ? 0 : POL_K + 1) + 10;
+    return false;
 }
 
 // QUEUE = false: one agent per 16-lane group. QUEUE = true (fallback launch): the agents the main
 // launch deferred (args.queue: [count, blocks done, agents...]), one per group (the grid covers
 // every agent of the batch); the last block to finish empties the queue for the next step.
-template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = false, bool LOOP = false>
+// INPL (with LEAN, main launch): the lean pipeline first; an agent it does not settle runs the
+// full pipeline in place after it (no fallback launch)
+template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = false, bool INPL = false>
 __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
                                                        const ImpcArgs args) {
     constexpr int GPB = BS / 16;
     // CBF-row staging, reused as the dual active set's scratch (sep_pol_doubles)
     // (slack mode: the slack-pattern active set's scratch + its multipliers, sep_slack_patterns)
     __shared__ double stage_all[GPB][sep_stage_doubles<SB, CB, SLACK>()];
-    __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
+    __shared__ double red_all[GPB][LEAN && !INPL ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
     // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
     // set's warm-start side ids and their count (not in slack mode) | linear term and constant, the
     // agent index, the residuals
-    __shared__ double keep_all[GPB][sep_keep_doubles<SB, SLACK, LEAN>()];
+    __shared__ double keep_all[GPB][sep_keep_doubles<SB, SLACK, LEAN && !INPL>()];
     constexpr bool rows_lds_per_lane = QUEUE || SB > 1;
     __shared__ SepRowsLds<SB, CB> rows_lds[rows_lds_per_lane ? BS : 1];
     // the box rows' constants per agent (sep_box_consts; not in slack mode)
@@ -908,33 +938,31 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
         grid_clear<BS>(args);
         const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * GPB + gib;
         if (ai >= args.num_agents) return;
-        impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
-                                                   nb_scratch[gib], keep_all[gib], rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
-                                                   SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
+        const bool full = impc_sep_agent<SB, CB, SLACK, false, LEAN, INPL>(
+            op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib], keep_all[gib],
+            rows_lds + (rows_lds_per_lane ? gib * 16 : 0), SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
+        if constexpr (INPL) {
+            if (full) {
+                wave_lds_sync();
+                impc_sep_agent<SB, CB, SLACK, false>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
+                                                     nb_scratch[gib], keep_all[gib],
+                                                     rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
+                                                     SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
+            }
+        }
         kclock_end<BS>(args);
     } else {
-        // one queue entry per group, the grid covering every agent of the batch (LOOP: entries k,
-        // k + groups, ... per group from a grid of a few blocks — where deferrals are rare, so that
-        // an empty queue costs a small launch; carried across iterations, the pipeline's registers
-        // spill, on that rare path only). Groups beyond the queue's length leave at once. The
-        // queue's header is zeroed by the main launch after next (the queues alternate by step
-        // parity), so no block has to find out that it is the last one
-        const int k0 = blockIdx.x * GPB + gib;
-        if constexpr (LOOP) {
-            const int nq = args.queue[0];
-            for (int k = k0; k < nq; k += (int)gridDim.x * GPB) {
-                impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib],
-                                                    red_all[gib], nb_scratch[gib], keep_all[gib],
-                                                    rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
-                                                    SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
-                wave_lds_sync();  // (the group's LDS is rewritten by its next entry)
-            }
-        } else if (k0 < args.queue[0]) {
-            impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k0], gl, stage_all[gib], red_all[gib],
+        // one queue entry per group (no grid-stride loop: carried across iterations the agent's
+        // state spills, 0 -> 372 B/lane, and a 16-block grid saved 0.2 us of the empty launch,
+        // r06d); groups beyond the queue's length leave at once. The queue's header is zeroed by
+        // the main launch after next (the queues alternate by step parity), so no block has to
+        // find out that it is the last one
+        const int k = blockIdx.x * GPB + gib;
+        if (k < args.queue[0])
+            impc_sep_agent<SB, CB, SLACK, true>(op, buf, args, args.queue[2 + k], gl, stage_all[gib], red_all[gib],
                                                 nb_scratch[gib], keep_all[gib],
                                                 rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
                                                 SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
-        }
     }
 }
 
@@ -957,6 +985,7 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
     double s0[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) s0[i] = args.states[(size_t)self * 6 + i];
+    early_noise(args, ai, gl, L.noise);  // (while the state is in flight)
     const bool grid_mode = args.nb_row_ptr == nullptr;
     WideQuery gq;
     WideCells gc;
@@ -1156,7 +1185,7 @@ __device__ void impc_wide_agent(const DevOps& op, const double* __restrict__ buf
     }
     write_iteration(args, (size_t)ai * op.impc_iter, gl, st_w0, obj_w0, nit_w0, prs_w0, drs_w0);
     if (op.impc_iter > 1) write_iteration(args, (size_t)ai * op.impc_iter + 1, gl, st_w1, obj_w1, nit_w1, prs_w1, drs_w1);
-    write_agent_outputs<NZ, 64>(op, buf, args, ai, gl, s0, yk, have_curve);
+    write_agent_outputs<NZ, 64>(op, buf, args, ai, gl, s0, yk, have_curve, L.noise);
     stamp(args, ai, gl, 7);
 }
 
@@ -1199,10 +1228,6 @@ __global__ void __launch_bounds__(BS) WIDE_WPE_ATTR impc_wide_kernel(const DevOp
 
 }  // namespace dev
 
-bool impc_rows_may_exceed(const DevOps& op, bool csr, int knn_k);
-// blocks of the looping capacity launch (64 threads, 4 queue walkers each)
-constexpr int FALLBACK_LOOP_BLOCKS = 16;
-
 template <int NZ, int G, int R>
 static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                 hipStream_t s) {
@@ -1213,13 +1238,12 @@ static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcA
     return hipGetLastError();
 }
 
-template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false, bool LEAN = false, bool LOOP = false>
+template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false, bool LEAN = false, bool INPL = false>
 static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                     hipStream_t s) {
     constexpr int GPB = BS / 16;
     int blocks = (a.num_agents + GPB - 1) / GPB;
-    if (LOOP) blocks = blocks < FALLBACK_LOOP_BLOCKS ? blocks : FALLBACK_LOOP_BLOCKS;
-    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE, LEAN, LOOP>), dim3(blocks), dim3(BS), 0, s, op,
+    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE, LEAN, INPL>), dim3(blocks), dim3(BS), 0, s, op,
                        buf, a);
     return hipGetLastError();
 }
@@ -1243,9 +1267,13 @@ static hipError_t launch_impc_wide(const DevOps& op, const double* buf, const Im
 //       4's rank share) the one-agent-per-wave kernel (its fallback as a second launch); beyond,
 //       the 16-lane kernel (4 agents per wave: one wave per SIMD covers 4 x as many agents);
 //   VARIANT_SEP16 — the 16-lane kernel at any count (the layout of rounds 1-4);
-//   VARIANT_WIDE — the one-agent-per-wave kernel at any count.
-constexpr int VARIANT_SEP16 = 4, VARIANT_WIDE = 5;
-static bool sep_variant(int variant) { return variant == 0 || variant == VARIANT_SEP16; }
+//   VARIANT_WIDE — the one-agent-per-wave kernel at any count;
+//   VARIANT_SEP16_INPL — the 16-lane kernel running the lean pipeline (fast start + dual active
+//       set), the full pipeline in place only for the agents it does not settle.
+constexpr int VARIANT_SEP16 = 4, VARIANT_WIDE = 5, VARIANT_SEP16_INPL = 6;
+static bool sep_variant(int variant) {
+    return variant == 0 || variant == VARIANT_SEP16 || variant == VARIANT_SEP16_INPL;
+}
 static bool use_wide(const DevOps& op, int variant, int n) {
     return impc_wide_ok(op) && (variant == VARIANT_WIDE || (variant == 0 && n <= op.wide_max));
 }
@@ -1269,9 +1297,7 @@ static bool sep_lean(const DevOps& op, int variant, int n) {
 //   otherwise — the full separable pipeline (dual active set, PDIP attempts, phase 1): with 16 CBF
 //   row slots when no agent can exceed them, else 8 slots per lane (128 rows). Agents beyond
 //   that report ERROR.
-//   rare — the one-agent-per-wave main launch when its 16 CBF lanes cannot be exceeded: only what
-//   its active set does not settle — a grid of FALLBACK_LOOP_BLOCKS blocks walks the queue.
-hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide, bool rare,
+hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcArgs& a, bool wide,
                                 hipStream_t s) {
     if (a.num_agents <= 0 || !a.queue) return hipSuccess;
     if (op.slack_mode) {
@@ -1279,14 +1305,7 @@ hipError_t launch_impc_fallback(const DevOps& op, const double* buf, const ImpcA
         return launch_impc_sep_t<1, 2, true, 64, true>(op, buf, a, s);
     }
     if (wide) return launch_impc_sep_t<1, 8, false, 64, true>(op, buf, a, s);
-    if (rare) return launch_impc_sep_t<1, 1, false, 64, true, false, true>(op, buf, a, s);
     return launch_impc_sep_t<1, 1, false, 64, true>(op, buf, a, s);
-}
-
-// Whether the agents launch_impc defers are rare (the one-agent-per-wave kernel with at most 16
-// CBF rows per agent: only QPs its dual active set does not settle)
-bool impc_defer_rare(const DevOps& op, int variant, bool csr, int knn_k, int n) {
-    return use_wide(op, variant, n) && !impc_rows_may_exceed(op, csr, knn_k) && !op.slack_mode;
 }
 
 // Whether some agent can exceed the default separable kernel's 16 CBF row slots (caller lists,
@@ -1325,7 +1344,9 @@ const char* impc_kernel_name(const DevOps& op, int variant, int n) {
     }
     if (use_wide(op, variant, n)) return "impc_wide_kernel<256>";
     if (sep_lean(op, variant, n)) return "impc_sep_kernel<1,1,false,256,false,true>";
-    if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) return "impc_sep_kernel<1,1,false,256>";
+    if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)
+        return variant == VARIANT_SEP16_INPL ? "impc_sep_kernel<1,1,false,256,false,true,true>"
+                                             : "impc_sep_kernel<1,1,false,256>";
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
         if (variant == 1 && op.m < 64) return "impc_kernel<6,64,1>";
@@ -1346,8 +1367,10 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
     }
     if (use_wide(op, variant, a.num_agents)) return launch_impc_wide(op, buf, a, s);
     if (sep_lean(op, variant, a.num_agents)) return launch_impc_sep_t<1, 1, false, 256, false, true>(op, buf, a, s);
-    if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)
+    if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) {
+        if (variant == VARIANT_SEP16_INPL) return launch_impc_sep_t<1, 1, false, 256, false, true, true>(op, buf, a, s);
         return launch_impc_sep_t<1, 1, false>(op, buf, a, s);
+    }
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return launch_impc_t<6, 16, 4>(op, buf, a, s);
         if (variant == 1 && op.m < 64) return launch_impc_t<6, 64, 1>(op, buf, a, s);

@@ -485,6 +485,7 @@ struct WideLds {
     double stage[W_CBF * W_ROW];        // this iteration's kept CBF rows, compacted
     double smp[MAX_CBF_H * 9];          // per CBF sample k: ego state (6) | U_k s0 (3)
     double act[POL_K + 1];              // iteration 0's final active set: side ids | count
+    double noise[8];                    // the next state's noise draws (early_noise)
 };
 
 // ---- neighbour query on the wave (grid mode) -------------------------------------------------
@@ -508,10 +509,9 @@ __device__ __forceinline__ void wn_issue(const ImpcArgs& args, double px, double
     const int t = gl < 9 * GRID_SST ? gl : 0;
     const int c = t / GRID_SST, js = t - c * GRID_SST;
     q.h = cell_hash(cx + (c % 3) - 1, cy + (c / 3) - 1, gr.mask);
-    const size_t e = (size_t)js * (gr.mask + 1u) + q.h;
     q.n = gr.cnt[q.h];
-    q.j = (int)gr.slots[e];
-    const double4 v = reinterpret_cast<const double4*>(gr.sst)[e];
+    q.j = (int)gr.slots[grid_slot_at(q.h, (uint32_t)js)];
+    const double4 v = reinterpret_cast<const double4*>(gr.sst)[grid_sst_at(q.h, (uint32_t)js)];
     q.st[0] = v.x;
     q.st[1] = v.y;
     q.st[2] = v.z;
@@ -554,7 +554,7 @@ __device__ __forceinline__ int wn_more(const GridArgs& gr, const WideCells& c, u
     for (int k = 0; k < 9; k++) {
         const uint32_t u = t - c.off[k];
         const uint32_t extra = c.nc[k] > (uint32_t)GRID_SST ? c.nc[k] - GRID_SST : 0u;
-        e = ((c.off[k] <= t) & (u < extra)) ? (u + GRID_SST) * (gr.mask + 1u) + c.hs[k] : e;
+        e = ((c.off[k] <= t) & (u < extra)) ? grid_slot_at(c.hs[k], u + GRID_SST) : e;
     }
     return (int)gr.slots[e];
 }

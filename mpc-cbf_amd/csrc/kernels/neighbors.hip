@@ -263,10 +263,10 @@ __global__ void __launch_bounds__(256) grid_insert_kernel(const double* __restri
 
 static size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 
-// one table: bucket counts (T) | slots (GRID_CAP x T, slot-major) | slot states (GRID_SST x T x 4)
+// one table: bucket counts (T) | slots (T x GRID_CAP, bucket-major) | slot states (T x GRID_SSTR x 4)
 size_t grid_table_bytes(int num_states) {
     const uint32_t T = grid_table_size(num_states);
-    return al256((size_t)T * 4) + al256((size_t)T * GRID_CAP * 4) + (size_t)T * GRID_SST * 32;
+    return al256((size_t)T * 4) + al256((size_t)T * GRID_CAP * 4) + (size_t)T * GRID_SSTR * 32;
 }
 
 void grid_table_carve(void* base, int num_states, uint32_t** cnt, uint32_t** slots, double** sst) {

@@ -127,8 +127,10 @@ struct PdipCfg {
     // pdip_solve_sep (no slack variables): when the unconstrained minimiser violates a row, the
     // dual active-set method (sep_dual_as) with at most this many steps first; 0: off
     int dual_as = 0;
-    // sep_dual_as: evaluate the returned point's dual residual (PdipOut::rd; else 0)
+    // sep_dual_as: evaluate the returned point's dual residual (PdipOut::rd; else 0) / its scaled
+    // primal residual (PdipOut::rp; else 0)
     bool want_rd = true;
+    bool want_rp = true;
 };
 
 struct PdipOut {

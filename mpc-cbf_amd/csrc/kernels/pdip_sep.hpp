@@ -159,17 +159,17 @@ __device__ __forceinline__ void sep_stage_side(const SepRows<SB, CB>& rw, const 
 // construction, not re-evaluated where registers are short — and the multipliers as the next
 // warm start's box duals) when every row holds at y to tol and every multiplier has its side's
 // sign. sc: the sides' violation scales 1 / (1 + |bound|) (box lower, upper per slot, then CBF).
-template <int G, int SB, int CB, bool RD>
+template <int G, int SB, int CB, bool RD, int NR = POL_K>
 __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                                const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], int k,
                                const double* __restrict__ pol, const double (&sc)[2 * SEP_D * SB + CB],
                                double tol, double (&yo)[SEP_NZ], double& rp_out, double& rd_out,
                                SepWarm<SB>* warm, double* __restrict__ mult = nullptr) {
     const int gl = lane_bits_opaque<G - 1>();
-    using S6 = Sym<POL_K>;
-    double K[S6::P], rhs[POL_K], dk[POL_K], lam[POL_K];
+    using S6 = Sym<NR>;
+    double K[S6::P], rhs[NR], dk[NR], lam[NR];
 #pragma unroll
-    for (int i = 0; i < POL_K; i++) {
+    for (int i = 0; i < NR; i++) {
         const bool ai = i < k;
         const double* ri = pol + (ai ? i : 0) * 16;
         double t = 0.0;
@@ -177,7 +177,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
         for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], yu[j], t);
         rhs[i] = ai ? t - ri[POL_B] : 0.0;
 #pragma unroll
-        for (int j = i; j < POL_K; j++) {
+        for (int j = i; j < NR; j++) {
             const double* wj = pol + (j < k ? j : 0) * 16 + POL_W;
             double v = 0.0;
 #pragma unroll
@@ -185,13 +185,13 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
             K[S6::idx(i, j)] = (ai && j < k) ? v : (i == j ? 1.0 : 0.0);
         }
     }
-    const bool okf = chol_packed<POL_K>(K, dk);
-    chol_solve<POL_K>(K, dk, rhs, lam);
+    const bool okf = chol_packed<NR>(K, dk);
+    chol_solve<NR>(K, dk, rhs, lam);
     double y[SEP_NZ], lmax = 0.0;
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
 #pragma unroll
-    for (int i = 0; i < POL_K; i++) {  // (lam_i = 0 beyond k: the padded rows read row 0)
+    for (int i = 0; i < NR; i++) {  // (lam_i = 0 beyond k: the padded rows read row 0)
         const double* wi = pol + (i < k ? i : 0) * 16 + POL_W;
 #pragma unroll
         for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-lam[i], wi[j], y[j]);
@@ -199,7 +199,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
     }
     bool bad = !okf;
 #pragma unroll
-    for (int i = 0; i < POL_K; i++)
+    for (int i = 0; i < NR; i++)
         bad = bad || (i < k && !(pol[(i < k ? i : 0) * 16 + POL_SGN] * lam[i] >= -1e-9 * (1.0 + lmax)));
     // every row at y (scaled violation, as the PDIP's primal residual)
     double rp = 0.0;
@@ -231,7 +231,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
                 const int o = 2 * d + h;
                 double v = fma(P[o * 6 + 2 * d], y[2 * d], fma(P[o * 6 + 2 * d + 1], y[2 * d + 1], q[o]));
 #pragma unroll
-                for (int i = 0; i < POL_K; i++) v = fma(lam[i], pol[(i < k ? i : 0) * 16 + o], v);
+                for (int i = 0; i < NR; i++) v = fma(lam[i], pol[(i < k ? i : 0) * 16 + o], v);
                 rd = fmax(rd, fabs(v));
                 qn = fmax(qn, fabs(q[o]));
             }
@@ -248,7 +248,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
                     const double il = (double)((2 * (d * SB + kk)) * 16 + gl), iu = il + 16.0;
                     double ml = 0.0, mu = 0.0;
 #pragma unroll
-                    for (int i = 0; i < POL_K; i++) {
+                    for (int i = 0; i < NR; i++) {
                         const double id = i < k ? pol[(i < k ? i : 0) * 16 + POL_ID] : -1.0;
                         ml = id == il ? -lam[i] : ml;
                         mu = id == iu ? lam[i] : mu;
@@ -260,7 +260,7 @@ __device__ bool sep_eqp_finish(const SepRows<SB, CB>& rw, bool has_cbf, const do
         if (mult != nullptr) {  // the active sides' multipliers (>= 0) and ids (sep_dual_as)
             double ui = 0.0;
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) ui = gl == i ? pol[(i < k ? i : 0) * 16 + POL_SGN] * lam[i] : ui;
+            for (int i = 0; i < NR; i++) ui = gl == i ? pol[(i < k ? i : 0) * 16 + POL_SGN] * lam[i] : ui;
             if (gl < k) {
                 mult[gl] = ui;
                 mult[8 + gl] = pol[gl * 16 + POL_ID];
@@ -425,6 +425,13 @@ __device__ __forceinline__ void sep_gram(const double* __restrict__ pol, int k, 
 // sides is a valid start, so a side whose slot now holds another row only costs steps.
 // save: at convergence the final active set's side ids are written there (lane 0; their count
 // at save[POL_K]).
+// Active sides the dual active set's factor holds (L, multipliers, substitutions): DAS_K <= POL_K
+// (the staged-row layout); a QP that needs more gives up to the PDIP. (MPCCBF_DAS_K: A/B builds)
+#ifndef MPCCBF_DAS_K
+#define MPCCBF_DAS_K 4
+#endif
+constexpr int DK = MPCCBF_DAS_K;
+static_assert(DK >= 1 && DK <= POL_K, "the factor holds at most POL_K staged rows");
 template <int G, int SB, int CB>
 __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                            const double* __restrict__ Pinv, const double (&q)[SEP_NZ], const double (&yu)[SEP_NZ], double tol, int maxstep,
@@ -432,7 +439,8 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                            int& steps, SepWarm<SB>* warm, bool want_rd, double& tlow,
                            long long* dbg = nullptr, int k0 = 0, const double* __restrict__ warm_ids = nullptr,
                            double* __restrict__ save = nullptr, double* __restrict__ mult = nullptr,
-                           const double* __restrict__ box_sc = nullptr, const float* __restrict__ box_w = nullptr) {
+                           const double* __restrict__ box_sc = nullptr, const float* __restrict__ box_w = nullptr,
+                           bool want_rp = true) {
     static_assert(G == 16, "rows of pol are copied one column per lane");
     (void)dbg;
     GSTAMP(0, true);
@@ -501,52 +509,52 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             wrow[r * 16 + gl] = rsqrtf((float)fmax(n2, 1e-30));
         }
     }
-    double y[SEP_NZ], u[POL_K];
+    double y[SEP_NZ], u[DK];
 #pragma unroll
     for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
 #pragma unroll
-    for (int i = 0; i < POL_K; i++) u[i] = 0.0;
+    for (int i = 0; i < DK; i++) u[i] = 0.0;
     int k = 0;
     steps = 0;
     const double add_tol = 0.1 * tol;
     double* cand = pol + POL_K * 16;
-    using S6 = Sym<POL_K>;
-    double L[S6::P], dl[POL_K];  // chol_packed layout of K's factor (identity beyond k), 1 / diagonal
+    using S6 = Sym<DK>;
+    double L[S6::P], dl[DK];  // chol_packed layout of K's factor (identity beyond k), 1 / diagonal
 #pragma unroll
-    for (int i = 0; i < POL_K; i++) {
+    for (int i = 0; i < DK; i++) {
         dl[i] = 1.0;
 #pragma unroll
-        for (int j = i; j < POL_K; j++) L[S6::idx(i, j)] = i == j ? 1.0 : 0.0;
+        for (int j = i; j < DK; j++) L[S6::idx(i, j)] = i == j ? 1.0 : 0.0;
     }
     if (k0 > 0) {
         // the EQP on the given sides: lam = K^-1 (G_A yu - b_A), y = yu - P^-1 G_A^T lam; start
         // there when every multiplier u_i = sign_i lam_i >= 0 (group-uniform: LDS rows)
-        double rhs[POL_K], lam[POL_K];
+        double rhs[DK], lam[DK];
         for (int i = 0; i < k0; i++) {
             const int id = (int)warm_ids[i];
             if ((id & 15) == gl) sep_stage_side<SB, CB>(rw, pi, id >> 4, gl, pol + i * 16);
         }
         wave_lds_sync();
-        sep_gram<POL_K>(pol, k0, L);
+        sep_gram<DK>(pol, k0, L);
 #pragma unroll
-        for (int i = 0; i < POL_K; i++) {
+        for (int i = 0; i < DK; i++) {
             const double* ri = pol + (i < k0 ? i : 0) * 16;
             double t = 0.0;
 #pragma unroll
             for (int j = 0; j < SEP_NZ; j++) t = fma(ri[j], yu[j], t);
             rhs[i] = i < k0 ? t - ri[POL_B] : 0.0;
         }
-        bool ok = chol_packed<POL_K>(L, dl);
-        chol_solve<POL_K>(L, dl, rhs, lam);
+        bool ok = chol_packed<DK>(L, dl);
+        chol_solve<DK>(L, dl, rhs, lam);
 #pragma unroll
-        for (int i = 0; i < POL_K; i++) {
+        for (int i = 0; i < DK; i++) {
             const double* ri = pol + (i < k0 ? i : 0) * 16;
             u[i] = i < k0 ? ri[POL_SGN] * lam[i] : 0.0;
             ok = ok && (i >= k0 || (u[i] >= 0.0 && isfinite(u[i])));
         }
         if (ok) {
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) {
+            for (int i = 0; i < DK; i++) {
                 const double* wi = pol + (i < k0 ? i : 0) * 16 + POL_W;
 #pragma unroll
                 for (int j = 0; j < SEP_NZ; j++) y[j] = fma(i < k0 ? -lam[i] : 0.0, wi[j], y[j]);
@@ -554,11 +562,11 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             k = k0;
         } else {  // cold: empty active set, identity factor
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) {
+            for (int i = 0; i < DK; i++) {
                 u[i] = 0.0;
                 dl[i] = 1.0;
 #pragma unroll
-                for (int j = i; j < POL_K; j++) L[S6::idx(i, j)] = i == j ? 1.0 : 0.0;
+                for (int j = i; j < DK; j++) L[S6::idx(i, j)] = i == j ? 1.0 : 0.0;
             }
         }
     }
@@ -570,6 +578,61 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         // ties): the side violated beyond the tolerance with the largest normalised violation. A
         // NaN row or iterate (a NaN state, target or neighbour state) shows as a NaN violation on
         // the first scan: give up, the caller's finiteness checks decide.
+#ifndef MPCCBF_SCAN_F64
+        // keys: a violated side's normalised violation as a float bit pattern (at least 1: a score
+        // that rounds to 0 in float still counts as violated), 0 for the others — the wide
+        // kernel's rule (impc_wide.hpp): the group max is one u32 DPP reduction, the lane's best
+        // side the first of its largest key; the scaled violation vb is reduced only when the
+        // caller stores the primal residual
+        unsigned kb = 0u;
+        double vb = -1.0;
+        int sb = 0;
+        bool nanv = false;
+        {
+            int s = 0, r = 0;
+#pragma unroll
+            for (int d = 0; d < SEP_D; d++)
+#pragma unroll
+                for (int kk = 0; kk < SB; kk++, r++) {
+                    const double t = rw.bg[d][kk][0] * y[2 * d] + rw.bg[d][kk][1] * y[2 * d + 1];
+                    const double w = (double)wbox[r * 16 + gl];
+                    const double al = rw.blo[d][kk] - t, vl = al * sc[s];
+                    const unsigned kl = vl > add_tol ? max(__float_as_uint((float)(al * w)), 1u) : 0u;
+                    if (kl > kb) kb = kl, sb = s;
+                    s++;
+                    const double au = t - rw.bhi[d][kk], vu = au * sc[s];
+                    const unsigned ku = vu > add_tol ? max(__float_as_uint((float)(au * w)), 1u) : 0u;
+                    if (ku > kb) kb = ku, sb = s;
+                    s++;
+                    nanv = nanv || vl != vl || vu != vu;
+                    vb = fmax(vb, fmax(vl, vu));
+                }
+            if (has_cbf) {
+#pragma unroll
+                for (int c = 0; c < CB; c++, s++, r++) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) t = fma(rw.cg[c][j], y[j], t);
+                    const double ac = t - rw.chi[c], vc = ac * sc[s];
+                    const unsigned kc =
+                        vc > add_tol ? max(__float_as_uint((float)(ac * (double)wrow[r * 16 + gl])), 1u) : 0u;
+                    if (kc > kb) kb = kc, sb = s;
+                    nanv = nanv || vc != vc;
+                    vb = fmax(vb, vc);
+                }
+            }
+        }
+        if (outer == 0 && grp_ballot<G>(nanv) != 0ull) return 0;
+        const unsigned kmax = row_max_u32(kb);
+        GSTAMP(2 + 6 * outer, outer < 2);
+        if (kmax == 0u) {
+            m = want_rp ? grp_max<G>(vb) : 0.0;
+            break;
+        }
+        if (steps >= maxstep) return 0;
+        if (kmax == 1u) return 0;  // the best score is 0 or denormal in float: no usable rule (PDIP)
+        const int owner = __ffsll((long long)grp_ballot<G>(kb == kmax)) - 1;
+#else  // (A/B build: double scores, two interleaved max reductions)
         double vb = -1.0, eb = -1.0;
         int sb = 0;
         bool nanv = false;
@@ -614,6 +677,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         if (!(m > add_tol)) break;
         if (steps >= maxstep) return 0;
         const int owner = __ffsll((long long)grp_ballot<G>(eb == em)) - 1;
+#endif
         if (gl == owner) sep_stage_side<SB, CB>(rw, pi, sb, gl, cand);
         wave_lds_sync();
         GSTAMP(3, outer == 0);
@@ -656,14 +720,14 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #ifndef MPCCBF_NO_KW
             int kw = 0;
 #pragma unroll
-            for (int i = 1; i <= POL_K; i++) kw += __ballot(k >= i) != 0ull ? 1 : 0;
+            for (int i = 1; i <= DK; i++) kw += __ballot(k >= i) != 0ull ? 1 : 0;
 #else  // comparison build: every row
-            constexpr int kw = POL_K;
+            constexpr int kw = DK;
 #endif
             // v = L^-1 (sp c), c_i = g_i P^-1 g_p: the forward substitution fused with the dots
-            double v[POL_K], sgn[POL_K];
+            double v[DK], sgn[DK];
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) {
+            for (int i = 0; i < DK; i++) {
                 v[i] = 0.0;
                 sgn[i] = 0.0;
                 if (i < kw) {
@@ -679,14 +743,14 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 }
             }
             // rho = L^-T v = K^-1 G_A P^-1 n_p: the active multipliers' change per unit step
-            double rho[POL_K];
+            double rho[DK];
 #pragma unroll
-            for (int i = POL_K - 1; i >= 0; i--) {
+            for (int i = DK - 1; i >= 0; i--) {
                 rho[i] = 0.0;
                 if (i < kw) {
                     double s = v[i];
 #pragma unroll
-                    for (int mm = i + 1; mm < POL_K; mm++) s = fma(-L[S6::idx(i, mm)], rho[mm], s);
+                    for (int mm = i + 1; mm < DK; mm++) s = fma(-L[S6::idx(i, mm)], rho[mm], s);
                     rho[i] = s * dl[i];
                 }
             }
@@ -698,7 +762,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 vp = fma(gp[j], y[j], vp);
             }
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) vv = fma(v[i], v[i], vv);
+            for (int i = 0; i < DK; i++) vv = fma(v[i], v[i], vv);
             const double zn = nw - vv;  // n_p z: the Schur complement of K in [K c; c^T nw]
             vp = sp * (vp - cand[POL_B]);
             // dual step: the first active multiplier to reach zero (smallest u_i / r_i, compared
@@ -706,7 +770,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             double un = 1.0, rn = 0.0;  // (un / rn = +inf until a blocking multiplier is found)
             int l = -1;
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) {
+            for (int i = 0; i < DK; i++) {
                 const double r = sgn[i] * rho[i];
                 const bool better = i < k && r > 0.0 && u[i] * rn < un * r;
                 un = better ? u[i] : un;
@@ -721,7 +785,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 // t* >= -sum lam b / sum lam = (n_p y - b_p) / (1 - sum r) (active sides exact at y)
                 double lsum = 1.0;
 #pragma unroll
-                for (int i = 0; i < POL_K; i++) {
+                for (int i = 0; i < DK; i++) {
                     const double r = sgn[i] * rho[i];
                     lsum += (i < k && r < 0.0) ? -r : 0.0;
                 }
@@ -742,7 +806,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 #pragma unroll
                 for (int j = 0; j < SEP_NZ; j++) z[j] = sp * cand[POL_W + j];
 #pragma unroll
-                for (int i = 0; i < POL_K; i++) {
+                for (int i = 0; i < DK; i++) {
                     if (i < kw) {
                         const double* wi = pol + (i < k ? i : 0) * 16 + POL_W;
                         const double ri = i < k ? rho[i] : 0.0;
@@ -754,21 +818,21 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 for (int j = 0; j < SEP_NZ; j++) y[j] = fma(-t, z[j], y[j]);
             }
 #pragma unroll
-            for (int i = 0; i < POL_K; i++)
+            for (int i = 0; i < DK; i++)
                 u[i] = i < k ? fma(-t, sgn[i] * rho[i], u[i]) : u[i];
             up += t;
             wave_lds_sync();  // every lane has read the rows it is about to move
             GSTAMP(5, steps == 2);
             if (t2 <= t1) {  // the candidate joins: L gains the row L^-1 c, diagonal sqrt(zn)
-                if (k == POL_K) return 0;
+                if (k == DK) return 0;
                 pol[k * 16 + gl] = cand[gl];
                 const double rz = rsqrt(zn);
 #pragma unroll
-                for (int i = 0; i < POL_K; i++) {
+                for (int i = 0; i < DK; i++) {
                     u[i] = i == k ? up : u[i];
                     dl[i] = i == k ? rz : dl[i];
 #pragma unroll
-                    for (int j = i; j < POL_K; j++)
+                    for (int j = i; j < DK; j++)
                         if (j == k) L[S6::idx(i, j)] = i < k ? sp * v[i] : (i == k ? zn * rz : L[S6::idx(i, j)]);
                 }
                 k++;
@@ -778,14 +842,14 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             }
             // side l leaves: the rows above it move down (one column per lane); K refactored
 #pragma unroll
-            for (int i = 0; i < POL_K - 1; i++)
+            for (int i = 0; i < DK - 1; i++)
                 if (i >= l && i < k - 1) pol[i * 16 + gl] = pol[(i + 1) * 16 + gl];
 #pragma unroll
-            for (int i = 0; i < POL_K; i++) u[i] = i >= l ? (i + 1 < POL_K ? u[i + 1] : 0.0) : u[i];
+            for (int i = 0; i < DK; i++) u[i] = i >= l ? (i + 1 < DK ? u[i + 1] : 0.0) : u[i];
             k--;
             wave_lds_sync();
-            sep_gram<POL_K>(pol, k, L);
-            if (!chol_packed<POL_K>(L, dl)) return 0;
+            sep_gram<DK>(pol, k, L);
+            if (!chol_packed<DK>(L, dl)) return 0;
         }
     }
     // converged: primal residual = the last scan's worst violation; the iterate's dual residual
@@ -816,7 +880,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         // row's entries read once
         int kw = 0;
 #pragma unroll
-        for (int i = 1; i <= POL_K; i++) kw += __ballot(k >= i) != 0ull ? 1 : 0;
+        for (int i = 1; i <= DK; i++) kw += __ballot(k >= i) != 0ull ? 1 : 0;
         double r[SEP_NZ];
 #pragma unroll
         for (int o = 0; o < SEP_NZ; o++) {
@@ -824,7 +888,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             r[o] = fma(pb[o][0], y[2 * d], fma(pb[o][1], y[2 * d + 1], q[o]));
         }
 #pragma unroll
-        for (int i = 0; i < POL_K; i++) {
+        for (int i = 0; i < DK; i++) {
             if (i < kw) {
                 const double* ri = pol + (i < k ? i : 0) * 16;
                 const double li = i < k ? ri[POL_SGN] * u[i] : 0.0;
@@ -847,7 +911,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     };
     if (!(rd <= tol)) {
         // rounding accumulated over the steps: the active set's equality QP, re-solved exactly
-        const bool ok = sep_eqp_finish<G, SB, CB, true>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm,
+        const bool ok = sep_eqp_finish<G, SB, CB, true, DK>(rw, has_cbf, P, q, yu, k, pol, sc, tol, yo, rp_out, rd_out, warm,
                                                         mult);
         if (ok) save_sides();
         wave_lds_sync();
@@ -865,7 +929,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                 const double il = (double)((2 * (d * SB + kk)) * 16 + gl), iu = il + 16.0;
                 double ml = 0.0, mu = 0.0;
 #pragma unroll
-                for (int i = 0; i < POL_K; i++) {
+                for (int i = 0; i < DK; i++) {
                     const double id = i < k ? pol[(i < k ? i : 0) * 16 + POL_ID] : -1.0;
                     ml = id == il ? u[i] : ml;
                     mu = id == iu ? u[i] : mu;
@@ -879,7 +943,7 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
                             // mult[8 .. 8 + k): their side ids (POL_ID)
         double ui = 0.0;
 #pragma unroll
-        for (int i = 0; i < POL_K; i++) ui = gl == i ? u[i] : ui;
+        for (int i = 0; i < DK; i++) ui = gl == i ? u[i] : ui;
         if (gl < k) {
             mult[gl] = ui;
             mult[8 + gl] = pol[gl * 16 + POL_ID];
@@ -901,6 +965,14 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
 // of the scalar v-block d): the group still reduces the same 20 values, with
 //   M_xy -= u u^T / d,  rhs_xy -= u rhs_v / d,   u = -sum_rows D g,  d = sum_rows D + D_bound,
 // and dv = (rhs_v - u^T dy) / d is recovered lane-locally after each solve.
+template <int G, int SB, int CB, bool SLACK>
+__device__ PdipOut pdip_solve_sep_ip(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
+                                     const double* __restrict__ Pinv, const double (&q)[SEP_NZ],
+                                     double (&y)[SEP_NZ], const PdipCfg cfg, long long* dbg, double wv_cost,
+                                     double* v_out, double* red, SepWarm<SB>* warm, double warm_delta, double* pol,
+                                     int as_steps);
+// (pdip_solve_sep_ip stays inline: as an out-of-line call — operands by reference or by value —
+// the caller kept its rows and loop state in scratch around it, 392-784 B/lane across the hot path)
 template <int G, int SB, int CB, bool SLACK = false>
 __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const double* __restrict__ P,
                                   const double* __restrict__ Pinv, const double (&q)[SEP_NZ],
@@ -911,15 +983,9 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                                   double* das_save = nullptr, const double* box_sc = nullptr,
                                   const float* box_w = nullptr) {
     (void)dbg;
-    const bool slk = SLACK && has_cbf;  // group-uniform
     GSTAMP(12, true);
-    // slack variable, its bound's slack and dual; the dual starts at the linear cost it carries at
-    // the optimum (w = sum_rows z + z_bound with inactive rows)
-    double v = 1.0, sb = 1.0, zb = SLACK ? fmax(wv_cost, 1.0) : 1.0;
-    // warm start (group-uniform): y holds the previous solution; slacks from it and the stored
-    // duals, both floored at delta (complementarity >= delta^2), CBF rows centred at delta^2
+    // warm start (group-uniform): y holds the previous solution (pdip_solve_sep_ip)
     const bool use_warm = warm != nullptr && warm_delta > 0.0;
-    const double wd = warm_delta, wd2 = warm_delta * warm_delta;
     int as_steps = 0;  // dual active-set steps before the PDIP (counted in iters)
     // ---- start: unconstrained minimiser (block-diagonal P: per-channel 2x2 solves). When it
     // satisfies every row it is the optimum (convex QP, all multipliers zero; slack mode: v = 0
@@ -985,7 +1051,7 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
                 double yg[SEP_NZ], rpg = 0.0, rdg = 0.0, tlg = 0.0;
                 const int r = sep_dual_as<G, SB, CB>(rw, has_cbf, P, Pinv, q, yu, cfg.tol, cfg.dual_as, pol, yg, rpg,
                                                      rdg, as_steps, nullptr, cfg.want_rd, tlg, dbg, das_k0, das_ids,
-                                                     das_save, nullptr, box_sc, box_w);
+                                                     das_save, nullptr, box_sc, box_w, cfg.want_rp);
                 if (r != 0) {
                     PdipOut fo{r > 0 ? ST_OPTIMAL : ST_UNKNOWN, as_steps};
 #pragma unroll
@@ -1008,6 +1074,28 @@ __device__ PdipOut pdip_solve_sep(const SepRows<SB, CB>& rw, bool has_cbf, const
             for (int j = 0; j < SEP_NZ; j++) y[j] = yu[j];
         }
     }
+    return pdip_solve_sep_ip<G, SB, CB, SLACK>(rw, has_cbf, P, Pinv, q, y, cfg, dbg, wv_cost, v_out, red, warm,
+                                               warm_delta, pol, as_steps);
+}
+
+// The Mehrotra PDIP of pdip_solve_sep from its start point (y: the unconstrained minimiser or the
+// warm start); as_steps: the dual active set's steps before it (counted in the iterations).
+template <int G, int SB, int CB, bool SLACK>
+__device__ __forceinline__ PdipOut pdip_solve_sep_ip(const SepRows<SB, CB>& rw, bool has_cbf,
+                                                     const double* __restrict__ P, const double* __restrict__ Pinv,
+                                                     const double (&q)[SEP_NZ], double (&y)[SEP_NZ],
+                                                     const PdipCfg cfg, long long* dbg, double wv_cost, double* v_out,
+                                                     double* red, SepWarm<SB>* warm, double warm_delta, double* pol,
+                                                     int as_steps) {
+    (void)dbg;
+    const bool slk = SLACK && has_cbf;  // group-uniform
+    // slack variable, its bound's slack and dual; the dual starts at the linear cost it carries at
+    // the optimum (w = sum_rows z + z_bound with inactive rows)
+    double v = 1.0, sb = 1.0, zb = SLACK ? fmax(wv_cost, 1.0) : 1.0;
+    // warm start (group-uniform): y holds the previous solution; slacks from it and the stored
+    // duals, both floored at delta (complementarity >= delta^2), CBF rows centred at delta^2
+    const bool use_warm = warm != nullptr && warm_delta > 0.0;
+    const double wd = warm_delta, wd2 = warm_delta * warm_delta;
     // slacks (s) and duals (z): box lower / upper sides, CBF upper side
     double sl[SEP_D][SB], su[SEP_D][SB], zl[SEP_D][SB], zu[SEP_D][SB], cs[CB], cz[CB];
     double pl[SEP_D][SB], pu[SEP_D][SB], pc[CB];  // relative primal-residual scales

@@ -22,9 +22,20 @@ def _torch():
     return torch
 
 
+# (first OPTIMAL -> INFEASIBLE transition of an iteration-0 QP in the 400-step runs,
+# profiles/r06_reference_instances.json: 2r/circle 11, 5r/circle 2, 6r/circle 58, 8r/diverge 194 in
+# base mode; 3r/line3 17 and 8r/circle2 19 with their own parameters — slack mode, K = 16, every
+# other robot a neighbour, which before round 6 ended in a capacity error)
+TRANSITIONS = {("2r/circle", "base"): 11, ("5r/circle", "base"): 2, ("6r/circle", "base"): 58,
+               ("8r/diverge", "base"): 194, ("3r/line3", "own"): 17, ("8r/circle2", "own"): 19}
+
+
 @pytest.mark.parametrize("name,mode,steps", [("2r/line", "base", 120), ("8r/circle", "base", 100),
                                              ("3r/line", "base", 100), ("6r/upward", "base", 100),
-                                             ("2r/line", "own", 120), ("8r/circle", "own", 100)])
+                                             ("2r/line", "own", 120), ("8r/circle", "own", 100),
+                                             ("2r/circle", "base", 24), ("5r/circle", "base", 16),
+                                             ("6r/circle", "base", 70), ("8r/diverge", "base", 200),
+                                             ("3r/line3", "own", 30), ("8r/circle2", "own", 30)])
 def test_reference_instance_gauss_seidel_matches_oracle(mpclib, name, mode, steps):
     """mode "base": the reference's run (base_config.json overlaid); "own": the instance file's own
     parameters (d_min 0.8, w_u_eff 1, ...), the keys it lacks from the base config."""
@@ -65,7 +76,12 @@ def test_reference_instance_gauss_seidel_matches_oracle(mpclib, name, mode, step
     assert (err > 1e-8).sum() <= max(2, 0.02 * err.size), np.argwhere(err > 1e-8)
     st = np.array(s.status_log)
     d0 = np.sqrt(((states[:, None, :2] - states[None, :, :2]) ** 2).sum(-1)) + np.diag(np.full(n, np.inf))
-    if mode == "base" and name in ("2r/line", "8r/circle"):
+    if (name, mode) in TRANSITIONS:
+        # the run covers an OPTIMAL -> INFEASIBLE transition (the oracle's statuses confirmed every
+        # update above); chaotic closed loops may move it by a few steps with last-bit changes
+        tr = np.argwhere((st[:-1, :, 0] == O.OPTIMAL) & (st[1:, :, 0] == O.INFEASIBLE))
+        assert len(tr) > 0 and tr[0, 0] + 1 <= TRANSITIONS[(name, mode)] + 5, tr[:3]
+    elif mode == "base" and name in ("2r/line", "8r/circle"):
         # started inside d_min = 2 of each other (1.5 / 1.53 m): a CBF row no acceleration
         # satisfies, every QP INFEASIBLE, the robots hold position (example :208-221)
         assert d0.min() < cfg["d_min"] and np.all(st[:, :, 0] == O.INFEASIBLE)

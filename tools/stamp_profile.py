@@ -53,7 +53,7 @@ PPH = ["rows+acc", "reduce acc", "rp/py/conv", "cholesky", "pred solve", "pred s
        "mua", "corr rows+vc", "corr solve", "corr steps+min", "update"]
 for v in VARIANTS:
     ctx.set_variant(v)
-    stamps = torch.zeros(N * 8 + (N * 16 if PDIP else 0) + (N * 2 * 256 if TRACE else 0), dtype=torch.int64,
+    stamps = torch.zeros(N * 8 + (N * 32 if PDIP else 0) + (N * 2 * 256 if TRACE else 0), dtype=torch.int64,
                          device=dev)
     for rep in range(3):  # last rep measured (warm caches)
         ctx.impc_solve(snap, targets=tg, knn_k=8, knn_radius=radius, stamps=stamps, cov=COV, **out)
@@ -61,7 +61,8 @@ for v in VARIANTS:
     allst = stamps.cpu().numpy()
     s = allst[:N * 8].reshape(N, 8).astype(np.float64) * 0.01  # 10 ns ticks -> us
     if PDIP and v == 0:
-        ps = allst[N * 8:].reshape(N, 16).astype(np.float64)  # shader cycles
+        # shader cycles (per agent: 32 stamps in the 16-lane kernel, 16 in the FoV kernel)
+        ps = (allst[N * 8:N * 24].reshape(N, 16) if FOV else allst[N * 8:N * 40].reshape(N, 32)[:, :16]).astype(np.float64)
         okp = ps[:, 11] > 0
         d = np.diff(ps[okp, :12], axis=1)
         tot = ps[okp, 11] - ps[okp, 0]
@@ -74,7 +75,19 @@ for v in VARIANTS:
             print(f"   {name:15s} mean {d[:, k].mean():7.0f}  p50 {np.median(d[:, k]):7.0f} cycles"
                   + (f"   critical agent {dc[k]:7.0f}" if dc is not None else ""))
     if PDIP and v == 0 and not FOV:  # dual active-set stamps (solve 0, first steps)
-        ps = allst[N * 8:].reshape(N, 16).astype(np.float64)
+        # (the 16-lane kernel: 32 stamps per agent, 16 .. 21 around the solver call)
+        ps = allst[N * 8:N * 40].reshape(N, 32).astype(np.float64)
+        its0_ = out["iters"].cpu().numpy()[:, 0]
+        for nstep in (0, 1, 2):
+            m = (ps[:, 21] > 0) & (its0_ == nstep) & (ps[:, 16] > 0) & (ps[:, 19] > 0)
+            if m.sum() == 0:
+                continue
+            print(f"variant {v}: solve phase around the solver, {nstep} step(s): {m.sum()} agents")
+            for name, a, b in [("nfin checks", 16, 17), ("to solver entry", 17, 12), ("solver", 12, 10),
+                               ("to solve exit", 10, 18), ("objective", 18, 19), ("ykeep", 19, 20),
+                               ("write_iteration", 20, 21)]:
+                d = ps[m, b] - ps[m, a]
+                print(f"   {name:17s} mean {d.mean():7.0f}  p50 {np.median(d):7.0f} cycles")
         its0 = out["iters"].cpu().numpy()[:, 0]
         # (the first scan is the fast-start test; the first side joins an empty active set
         # without substitutions, so stamps 4 and 5 belong to later steps only)
@@ -98,7 +111,7 @@ for v in VARIANTS:
                 d = ps[m, b] - ps[m, a]
                 print(f"   {name:15s} mean {d.mean():7.0f}  p50 {np.median(d):7.0f} cycles")
     if PDIP and v == 0 and FOV:  # the wave dual active set's stamps (das_wave.hpp, solve 0)
-        ps = allst[N * 8:].reshape(N, 16).astype(np.float64)
+        ps = allst[N * 8:N * 24].reshape(N, 16).astype(np.float64)
         names = [("init", 0, 1), ("scan 1", 1, 2), ("candidate P^-1 g", 2, 3), ("subst + dots", 3, 4),
                  ("step lengths", 4, 5), ("update y, u", 5, 6), ("join", 6, 7), ("scan 2", 7, 8)]
         names0 = [("init", 0, 1), ("scan", 1, 2), ("converged", 2, 9), ("dual residual", 9, 10)]
