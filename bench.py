@@ -332,9 +332,11 @@ def main():
             barrier_sync()
             t0 = time.perf_counter()
             e0.record()  # torch's current stream: the one run_steps launches on
+            # (the timed steps continue the warm-up's closed loop: its last step's neighbour table
+            # is the first timed step's, mpccbf_run::continue_tables)
             r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=log[0], iters_log=log[1],
                               timing=timing, solve_stride=1, step_index=args.warmup,
-                              kernel_clock=kclock if timing else None, **common)
+                              kernel_clock=kclock if timing else None, continue_tables=True, **common)
             e1.record()
             barrier_sync()
             return time.perf_counter() - t0, r

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPCCBF_ABI_VERSION 11
+#define MPCCBF_ABI_VERSION 12
 
 /* qpcpp::SolveStatus (Solver.h:13-21) */
 enum {
@@ -269,6 +269,13 @@ typedef struct mpccbf_run {
      * kernels only (the FoV kernels write nothing). */
     uint64_t* kernel_clock;
     int32_t kernel_clock_waves;
+    /* ABI 12: 1 = this call continues the context's previous mpccbf_run_steps call: batch->states
+     * is that call's final table, unchanged since, with the same agent range and neighbour
+     * query (knn_k, knn_radius). Its first step then reads the neighbour table the previous call's
+     * last step filled, instead of rebuilding table 0 (two memsets and an insert launch per call).
+     * The library checks pointer, range and query against the previous call and rebuilds when any
+     * differs (or when an mpccbf_impc_solve in grid mode came between); 0: always rebuild. */
+    int32_t continue_tables;
 } mpccbf_run;
 
 int mpccbf_run_steps(mpccbf_ctx* ctx, const mpccbf_batch* batch, mpccbf_run* run, void* hip_stream);

@@ -81,6 +81,14 @@ struct mpccbf_ctx {
     int defer_parity = 0;
     int variant = 0;
     int last_n = 0;  // agents of the last IMPC launch (the kernel name depends on it: share-adaptive)
+    // grid mode: where the previous mpccbf_run_steps call left the table rotation (ABI 12,
+    // mpccbf_run::continue_tables): its final state table, shape, query and the next step's table
+    struct {
+        bool valid = false;
+        const double* states = nullptr;
+        int ns = 0, first = 0, count = 0, k = 0, next = 0;
+        double radius = 0.0;
+    } gcont;
 };
 
 using namespace mpccbf;
@@ -103,6 +111,7 @@ static int grid_tables(mpccbf_ctx* c, int num_states, uint32_t* (&cnt)[3], uint3
                        double* (&sst)[3]) {
     const size_t tb = grid_table_bytes(num_states);
     if (3 * tb > c->grid_bytes) {
+        c->gcont.valid = false;
         if (c->grid_scratch) (void)hipFree(c->grid_scratch);
         c->grid_scratch = nullptr;
         c->grid_bytes = 0;
@@ -147,6 +156,7 @@ int impc_enqueue(mpccbf_ctx* c, const mpccbf_batch* b, hipStream_t stream, hipEv
         const uint32_t T = grid_table_size(b->num_states);
         int rd = 0;
         if (gstep < 0) {
+            c->gcont.valid = false;  // (table 0 rebuilt: a run_steps continuation must rebuild too)
             HIP_TRY(hipMemsetAsync(cnt[0], 0, (size_t)T * 4, stream));
             HIP_TRY(launch_grid_insert(b->states, b->num_states, 0, 0, b->knn_radius, cnt[0], slots[0], sst[0],
                                        stream));
@@ -750,15 +760,26 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
     const bool gtab = b->nb_row_ptr == nullptr && count > 0 && r->num_steps > 0;
     uint32_t *gcnt[3] = {}, *gslots[3] = {};
     double* gsst[3] = {};
+    int gbase = 0;  // the first step's table index (gstep = gbase + s)
     if (gtab) {
         if (b->knn_k < 1 || !(b->knn_radius > 0))
             return fail(MPCCBF_ERR_INVALID_ARGUMENT, "grid neighbours need knn_k >= 1 and knn_radius > 0");
         const int rc = grid_tables(c, ns, gcnt, gslots, gsst);
         if (rc != MPCCBF_OK) return rc;
-        const size_t cb = (size_t)grid_table_size(ns) * 4;
-        HIP_TRY(hipMemsetAsync(gcnt[0], 0, cb, stream));
-        HIP_TRY(hipMemsetAsync(gcnt[1], 0, cb, stream));
-        HIP_TRY(launch_grid_insert(b->states, ns, 0, 0, b->knn_radius, gcnt[0], gslots[0], gsst[0], stream));
+        const auto& g = c->gcont;
+        const bool cont = r->continue_tables && g.valid && g.states == b->states && g.ns == ns && g.first == first &&
+                          g.count == count && g.k == b->knn_k && g.radius == b->knn_radius;
+        if (cont) {
+            // the previous call's last step filled table g.next with these states and zeroed the
+            // one after it: this call's first step reads the former and fills the latter
+            gbase = g.next;
+        } else {
+            const size_t cb = (size_t)grid_table_size(ns) * 4;
+            HIP_TRY(hipMemsetAsync(gcnt[0], 0, cb, stream));
+            HIP_TRY(hipMemsetAsync(gcnt[1], 0, cb, stream));
+            HIP_TRY(launch_grid_insert(b->states, ns, 0, 0, b->knn_radius, gcnt[0], gslots[0], gsst[0], stream));
+        }
+        c->gcont.valid = false;  // (set again once every step is enqueued)
     }
     for (int s = 0; s < r->num_steps; s++) {
         double* cur = tables[s & 1];
@@ -778,7 +799,7 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
         }
         const bool tk = r->solve_ms && (r->solve_stride <= 1 || s % r->solve_stride == 0);
         const int rc = impc_enqueue(c, &sb, stream, tk ? ev[3 * s + 1] : nullptr, tk ? ev[3 * s + 2] : nullptr,
-                                    gtab ? s : -1,
+                                    gtab ? gbase + s : -1,
                                     r->kernel_clock ? (unsigned long long*)r->kernel_clock +
                                                           2 * (size_t)r->kernel_clock_waves * s
                                                     : nullptr);
@@ -803,13 +824,26 @@ int mpccbf_run_steps(mpccbf_ctx* c, const mpccbf_batch* b, mpccbf_run* r, void* 
         }
         // the rows the kernel did not insert (static rows / the other ranks' rows) join the table
         // of the next step
-        if (gtab && count < ns)
-            HIP_TRY(launch_grid_insert(nxt, ns, first, first + count, b->knn_radius, gcnt[(s + 1) % 3],
-                                       gslots[(s + 1) % 3], gsst[(s + 1) % 3], stream));
+        if (gtab && count < ns) {
+            const int t = (gbase + s + 1) % 3;
+            HIP_TRY(launch_grid_insert(nxt, ns, first, first + count, b->knn_radius, gcnt[t], gslots[t], gsst[t],
+                                       stream));
+        }
         if (r->step_ms || (timing && s == r->num_steps - 1)) HIP_TRY(hipEventRecord(ev[3 * s + 3], stream));
     }
     guard.g = nullptr;  // every barrier of the call passed: the peers no longer wait on this rank
     r->final_table = r->num_steps & 1;
+    if (gtab) {  // where a continuing call picks the rotation up (mpccbf_run::continue_tables)
+        auto& g = c->gcont;
+        g.valid = true;
+        g.states = tables[r->num_steps & 1];
+        g.ns = ns;
+        g.first = first;
+        g.count = count;
+        g.k = b->knn_k;
+        g.radius = b->knn_radius;
+        g.next = (gbase + r->num_steps) % 3;
+    }
     if (timing && r->num_steps > 0) {
         HIP_TRY(hipEventSynchronize(ev[3 * (r->num_steps - 1) + 3]));
         for (int s = 0; s < r->num_steps; s++) {

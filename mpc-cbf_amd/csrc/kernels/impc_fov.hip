@@ -94,8 +94,6 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
     double s0[6];
 #pragma unroll
     for (int k = 0; k < 6; k++) s0[k] = args.states[(size_t)self * 6 + k];
-    __shared__ double noise0[8];  // the next state's noise draws, while the state is in flight
-    early_noise(args, ai, lane, noise0);
     // grid mode: the neighbour query's loads are staged between the setup's (gq_*; the state
     // arrives before the branch, else the join waits for every load in flight)
     const bool grid_mode = args.nb_row_ptr == nullptr;
@@ -791,7 +789,7 @@ __global__ void __launch_bounds__(64) impc_fov_kernel(const DevOps op, const dou
         double yk[NZ];
 #pragma unroll
         for (int j = 0; j < NZ; j++) yk[j] = ykeep_s[j];
-        write_agent_outputs<NZ, 64, !SLACK, false>(op, buf, args, ai, lane, s0, yk, have_curve, noise0);
+        write_agent_outputs<NZ, 64, !SLACK, false>(op, buf, args, ai, lane, s0, yk, have_curve);
     }
     // (diagnostics; here, not after the query: there it pushed the kernel into scratch)
     write_nb_out(args, ai, lane, grid_mode, nb_scratch, nb0, nnb);

@@ -479,10 +479,8 @@ __device__ __forceinline__ SepRows<SB, CB>& pick_rows(SepRows<SB, CB>& reg, SepR
 
 // (force-inlined: instantiated by two kernels, an out-of-line call would copy the kernel arguments
 // to the stack at every launch's start)
-// INPL (with LEAN): an agent the lean solve does not settle is not deferred to the fallback launch;
-// the function returns true and the caller runs the full pipeline for it in place
-template <int SB, int CB, bool SLACK, bool QUEUE, bool LEAN = false, bool INPL = false>
-__device__ __forceinline__ bool impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
+template <int SB, int CB, bool SLACK, bool QUEUE, bool LEAN = false>
+__device__ __forceinline__ void impc_sep_agent(const DevOps& op, const double* __restrict__ buf, const ImpcArgs& args,
                                const int ai, const int gl, double* stage, double* red, NbScratch& nbs,
                                double* keep, SepRowsLds<SB, CB>* rows_lds = nullptr, double* bconst = nullptr) {
     constexpr int G = 16;
@@ -574,7 +572,7 @@ __device__ __forceinline__ bool impc_sep_agent(const DevOps& op, const double* _
     write_nb_out(args, ai, gl, grid_mode, nbs, nb0, nnb);
     if (SLACK && !QUEUE && nnb > G && args.defer) {  // slack mode: beyond one lane per neighbour
         defer_agent(args, agent(), gl);
-        return false;
+        return;
     }
     const bool nb_overflow = nnb < 0 || (SLACK && !QUEUE && nnb > G);
     if (nb_overflow) nnb = 0;
@@ -673,7 +671,7 @@ __device__ __forceinline__ bool impc_sep_agent(const DevOps& op, const double* _
         if (it < 2) stamp(args, ai, gl, 3 + 2 * it);
         if (count > cap && args.defer) {  // beyond this instantiation: the fallback launch solves it
             defer_agent(args, agent(), gl);
-            return false;
+            return;
         }
 #ifdef MPCCBF_PDIP_STAMPS  // (profiling build: the solve phase's parts around the solver, slots 16 ..)
         long long* const dbgs = (args.stamps && it == 0)
@@ -737,9 +735,8 @@ __device__ __forceinline__ bool impc_sep_agent(const DevOps& op, const double* _
                 prs = tl;
                 drs = __builtin_nan("");
             } else {
-                if constexpr (INPL) return true;  // (the caller's full pipeline solves it)
                 defer_agent(args, agent(), gl);
-                return false;
+                return;
             }
             if (gl == 0) res[0] = prs, res[1] = drs;
         } else {
@@ -796,7 +793,6 @@ __device__ __forceinline__ bool impc_sep_agent(const DevOps& op, const double* _
                 ca.robust = attempt == 2;
                 ca.dual_as = attempt == 0 ? op.dual_as : 0;
                 ca.want_rd = args.dual_res != nullptr;
-                ca.want_rp = args.primal_res != nullptr;
                 const int k0 = attempt == 0 ? warm_count(it) : 0;
                 po = pdip_solve_sep<G, SB, CB, SLACK>(rw, live, opp(buf, op.o_Pr), opp(buf, op.o_Pinv), q, y,
                                                       ca, dbg, wslack, &vslack, red, &warm,
@@ -905,27 +901,24 @@ __device__ __forceinline__ bool impc_sep_agent(const DevOps& op, const double* _
     load_state_lds(s0k, sx);
     write_agent_outputs<NZ, G>(op, buf, args, agent(), gl, sx, yk, have_curve, noise0);
     stamp(args, ai, gl, 7);
-    return false;
 }
 
 // QUEUE = false: one agent per 16-lane group. QUEUE = true (fallback launch): the agents the main
 // launch deferred (args.queue: [count, blocks done, agents...]), one per group (the grid covers
 // every agent of the batch); the last block to finish empties the queue for the next step.
-// INPL (with LEAN, main launch): the lean pipeline first; an agent it does not settle runs the
-// full pipeline in place after it (no fallback launch)
-template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = false, bool INPL = false>
+template <int SB, int CB, bool SLACK, int BS, bool QUEUE = false, bool LEAN = false>
 __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const double* __restrict__ buf,
                                                        const ImpcArgs args) {
     constexpr int GPB = BS / 16;
     // CBF-row staging, reused as the dual active set's scratch (sep_pol_doubles)
     // (slack mode: the slack-pattern active set's scratch + its multipliers, sep_slack_patterns)
     __shared__ double stage_all[GPB][sep_stage_doubles<SB, CB, SLACK>()];
-    __shared__ double red_all[GPB][LEAN && !INPL ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
+    __shared__ double red_all[GPB][LEAN ? 1 : 16 * (A_N + 1)];  // LDS all-reduce of the Newton sums
     __shared__ NbScratch nb_scratch[GPB];
     // kept solution | warm-start duals (not in the lean launch) | the agent's state | the dual active
     // set's warm-start side ids and their count (not in slack mode) | linear term and constant, the
     // agent index, the residuals
-    __shared__ double keep_all[GPB][sep_keep_doubles<SB, SLACK, LEAN && !INPL>()];
+    __shared__ double keep_all[GPB][sep_keep_doubles<SB, SLACK, LEAN>()];
     constexpr bool rows_lds_per_lane = QUEUE || SB > 1;
     __shared__ SepRowsLds<SB, CB> rows_lds[rows_lds_per_lane ? BS : 1];
     // the box rows' constants per agent (sep_box_consts; not in slack mode)
@@ -938,18 +931,10 @@ __global__ void __launch_bounds__(BS) impc_sep_kernel(const DevOps op, const dou
         grid_clear<BS>(args);
         const int ai = xcd_block((int)blockIdx.x, (int)gridDim.x) * GPB + gib;
         if (ai >= args.num_agents) return;
-        const bool full = impc_sep_agent<SB, CB, SLACK, false, LEAN, INPL>(
-            op, buf, args, ai, gl, stage_all[gib], red_all[gib], nb_scratch[gib], keep_all[gib],
-            rows_lds + (rows_lds_per_lane ? gib * 16 : 0), SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
-        if constexpr (INPL) {
-            if (full) {
-                wave_lds_sync();
-                impc_sep_agent<SB, CB, SLACK, false>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
-                                                     nb_scratch[gib], keep_all[gib],
-                                                     rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
-                                                     SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
-            }
-        }
+        impc_sep_agent<SB, CB, SLACK, false, LEAN>(op, buf, args, ai, gl, stage_all[gib], red_all[gib],
+                                                   nb_scratch[gib], keep_all[gib],
+                                                   rows_lds + (rows_lds_per_lane ? gib * 16 : 0),
+                                                   SLACK ? nullptr : bconst_all[SLACK ? 0 : gib]);
         kclock_end<BS>(args);
     } else {
         // one queue entry per group (no grid-stride loop: carried across iterations the agent's
@@ -1238,13 +1223,13 @@ static hipError_t launch_impc_t(const DevOps& op, const double* buf, const ImpcA
     return hipGetLastError();
 }
 
-template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false, bool LEAN = false, bool INPL = false>
+template <int SB, int CB, bool SLACK, int BS = 256, bool QUEUE = false, bool LEAN = false>
 static hipError_t launch_impc_sep_t(const DevOps& op, const double* buf, const ImpcArgs& a,
                                     hipStream_t s) {
     constexpr int GPB = BS / 16;
     int blocks = (a.num_agents + GPB - 1) / GPB;
-    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE, LEAN, INPL>), dim3(blocks), dim3(BS), 0, s, op,
-                       buf, a);
+    hipLaunchKernelGGL((dev::impc_sep_kernel<SB, CB, SLACK, BS, QUEUE, LEAN>), dim3(blocks), dim3(BS), 0, s, op, buf,
+                       a);
     return hipGetLastError();
 }
 
@@ -1267,13 +1252,12 @@ static hipError_t launch_impc_wide(const DevOps& op, const double* buf, const Im
 //       4's rank share) the one-agent-per-wave kernel (its fallback as a second launch); beyond,
 //       the 16-lane kernel (4 agents per wave: one wave per SIMD covers 4 x as many agents);
 //   VARIANT_SEP16 — the 16-lane kernel at any count (the layout of rounds 1-4);
-//   VARIANT_WIDE — the one-agent-per-wave kernel at any count;
-//   VARIANT_SEP16_INPL — the 16-lane kernel running the lean pipeline (fast start + dual active
-//       set), the full pipeline in place only for the agents it does not settle.
-constexpr int VARIANT_SEP16 = 4, VARIANT_WIDE = 5, VARIANT_SEP16_INPL = 6;
-static bool sep_variant(int variant) {
-    return variant == 0 || variant == VARIANT_SEP16 || variant == VARIANT_SEP16_INPL;
-}
+//   VARIANT_WIDE — the one-agent-per-wave kernel at any count.
+// (Round 6, measured and dropped: a lean-then-full variant — the fast start and the dual active
+// set, the full pipeline in place after the IMPC loop for the agents they do not settle — ran the
+// lean part 1.6 us slower than the lean kernel alone and 0.5 us slower than the full kernel.)
+constexpr int VARIANT_SEP16 = 4, VARIANT_WIDE = 5;
+static bool sep_variant(int variant) { return variant == 0 || variant == VARIANT_SEP16; }
 static bool use_wide(const DevOps& op, int variant, int n) {
     return impc_wide_ok(op) && (variant == VARIANT_WIDE || (variant == 0 && n <= op.wide_max));
 }
@@ -1345,8 +1329,7 @@ const char* impc_kernel_name(const DevOps& op, int variant, int n) {
     if (use_wide(op, variant, n)) return "impc_wide_kernel<256>";
     if (sep_lean(op, variant, n)) return "impc_sep_kernel<1,1,false,256,false,true>";
     if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16)
-        return variant == VARIANT_SEP16_INPL ? "impc_sep_kernel<1,1,false,256,false,true,true>"
-                                             : "impc_sep_kernel<1,1,false,256>";
+        return "impc_sep_kernel<1,1,false,256>";
     if (op.nz == 6) {
         if ((variant == 0 || variant == 3) && op.m < 64) return "impc_kernel<6,16,4>";
         if (variant == 1 && op.m < 64) return "impc_kernel<6,64,1>";
@@ -1368,7 +1351,6 @@ hipError_t launch_impc(const DevOps& op, const double* buf, const ImpcArgs& a, i
     if (use_wide(op, variant, a.num_agents)) return launch_impc_wide(op, buf, a, s);
     if (sep_lean(op, variant, a.num_agents)) return launch_impc_sep_t<1, 1, false, 256, false, true>(op, buf, a, s);
     if (sep_variant(variant) && op.sep && op.nzd == SEP_NZD_HOST && op.sep_rows_per_dim <= 16) {
-        if (variant == VARIANT_SEP16_INPL) return launch_impc_sep_t<1, 1, false, 256, false, true, true>(op, buf, a, s);
         return launch_impc_sep_t<1, 1, false>(op, buf, a, s);
     }
     if (op.nz == 6) {

@@ -428,7 +428,7 @@ __device__ __forceinline__ void sep_gram(const double* __restrict__ pol, int k, 
 // Active sides the dual active set's factor holds (L, multipliers, substitutions): DAS_K <= POL_K
 // (the staged-row layout); a QP that needs more gives up to the PDIP. (MPCCBF_DAS_K: A/B builds)
 #ifndef MPCCBF_DAS_K
-#define MPCCBF_DAS_K 4
+#define MPCCBF_DAS_K 5
 #endif
 constexpr int DK = MPCCBF_DAS_K;
 static_assert(DK >= 1 && DK <= POL_K, "the factor holds at most POL_K staged rows");

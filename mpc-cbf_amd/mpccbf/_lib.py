@@ -101,7 +101,7 @@ class Run(C.Structure):
                 ("iters_log", C.c_void_p), ("step_ms", C.c_void_p), ("solve_ms", C.c_void_p),
                 ("comm", C.c_void_p), ("reserve_steps", C.c_int32), ("solve_stride", C.c_int32),
                 ("final_table", C.c_int32), ("kernel_clock", C.c_void_p),
-                ("kernel_clock_waves", C.c_int32)]
+                ("kernel_clock_waves", C.c_int32), ("continue_tables", C.c_int32)]
 
 
 class DenseQP(C.Structure):
@@ -268,7 +268,7 @@ class Context:
                   status=None, obj=None, iters=None, status_log=None, iters_log=None,
                   timing=False, comm=None, reserve_steps=0, solve_stride=1, step_timing=True,
                   stream=None, traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0,
-                  cov=None, kernel_clock=None, stamps=None):
+                  cov=None, kernel_clock=None, stamps=None, continue_tables=False):
         """Closed-loop control steps on the device (mpccbf_run_steps). Returns a dict with the
         table holding the final states ('final', a tensor) and, with timing=True, per-step
         device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms). kernel_clock: a
@@ -300,7 +300,8 @@ class Context:
                 solve_ms=None if solve_ms is None else solve_ms.ctypes.data,
                 comm=None if comm is None else comm.handle, reserve_steps=reserve_steps,
                 solve_stride=solve_stride, kernel_clock=_ptr(kernel_clock),
-                kernel_clock_waves=0 if kernel_clock is None else int(kernel_clock.shape[1]))
+                kernel_clock_waves=0 if kernel_clock is None else int(kernel_clock.shape[1]),
+                continue_tables=int(bool(continue_tables)))
         _check(load().mpccbf_run_steps(self._h, C.byref(b), C.byref(r), _stream(stream)))
         out = {"final": states if r.final_table == 0 else states_alt}
         if timing:

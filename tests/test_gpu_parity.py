@@ -314,6 +314,46 @@ def test_run_steps_matches_step_by_step(mpclib, first, count):
         np.testing.assert_array_equal(ref_states[keep], states[keep])
 
 
+@pytest.mark.parametrize("first,count", [(0, 512), (12, 488)])
+def test_run_steps_continuation_matches_one_call(mpclib, first, count):
+    """mpccbf_run::continue_tables (ABI 12): 3 + 4 + 5 steps in three calls, each continuing the
+    previous call's neighbour-table rotation, == 12 steps in one call (bit-identical states and
+    statuses); a continuation whose states are not the previous call's final table, or after an
+    mpccbf_impc_solve in grid mode, rebuilds the table and gives the same result."""
+    torch = _torch()
+    cfg = swarm.config(15)
+    states, targets = swarm.lattice_swarm(512, seed=6)
+    states[:, :2] *= 0.6
+    dev = torch.device("cuda", 0)
+    st0 = torch.tensor(states, device=dev)
+    tg = torch.tensor(targets[first:first + count], device=dev)
+    common = dict(targets=tg, agent_first=first, num_agents=count, knn_k=8, knn_radius=6.0)
+    ctx = mpclib.Context(cfg)
+    out = ctx.alloc_outputs(count)
+    a, b = st0.clone(), torch.empty_like(st0)
+    log1 = torch.empty((12, count, 2), dtype=torch.int32, device=dev)
+    r = ctx.run_steps(a, b, 12, x=out["x"], obj=out["obj"], status_log=log1, **common)
+    torch.cuda.synchronize()
+    ref, ref_log = r["final"].cpu().numpy(), log1.cpu().numpy()
+    for mode in ("continue", "interrupted"):
+        c = mpclib.Context(cfg)
+        o = c.alloc_outputs(count)
+        a, b = st0.clone(), torch.empty_like(st0)
+        log2 = torch.empty((12, count, 2), dtype=torch.int32, device=dev)
+        s = 0
+        for k in (3, 4, 5):
+            if mode == "interrupted" and s == 7:  # a grid-mode solve between the calls
+                c.impc_solve(a, **common)
+            r = c.run_steps(a, b, k, x=o["x"], obj=o["obj"], status_log=log2[s:s + k], step_index=s,
+                            continue_tables=s > 0, **common)
+            if r["final"] is not a:
+                a, b = b, a
+            s += k
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(a.cpu().numpy(), ref)
+        np.testing.assert_array_equal(log2.cpu().numpy(), ref_log)
+
+
 def test_run_steps_with_single_rank_communicator(mpclib):
     """The RCCL exchange path (in-place all-gather after every step) with one rank equals the
     single-process loop."""

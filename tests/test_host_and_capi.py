@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol(mpclib):
 
 def test_abi_version_and_status_strings(mpclib):
     L = mpclib.load()
-    assert L.mpccbf_abi_version() == 11
+    assert L.mpccbf_abi_version() == 12
     assert [L.mpccbf_status_string(i).decode() for i in range(7)] == mpclib.STATUS_NAMES
 
 
