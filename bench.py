@@ -329,14 +329,18 @@ def main():
                               iters=out["iters"], reserve_steps=nsteps, **common)
             if r["final"] is not tables[0]:
                 tables.reverse()
+            # (the timed steps continue the warm-up's closed loop: its last step's neighbour table
+            # is the first timed step's, mpccbf_run::continue_tables). Their arguments are
+            # marshalled here, before the timed region, which holds the C call alone — the
+            # library's own host work (checks, table setup, launches) and the steps
+            run = ctx.prepare_run_steps(tables[0], tables[1], nsteps, status_log=log[0], iters_log=log[1],
+                                        timing=timing, solve_stride=1, step_index=args.warmup,
+                                        kernel_clock=kclock if timing else None, continue_tables=True,
+                                        **common)
             barrier_sync()
             t0 = time.perf_counter()
             e0.record()  # torch's current stream: the one run_steps launches on
-            # (the timed steps continue the warm-up's closed loop: its last step's neighbour table
-            # is the first timed step's, mpccbf_run::continue_tables)
-            r = ctx.run_steps(tables[0], tables[1], nsteps, status_log=log[0], iters_log=log[1],
-                              timing=timing, solve_stride=1, step_index=args.warmup,
-                              kernel_clock=kclock if timing else None, continue_tables=True, **common)
+            r = run()
             e1.record()
             barrier_sync()
             return time.perf_counter() - t0, r

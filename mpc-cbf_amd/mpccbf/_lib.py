@@ -190,6 +190,26 @@ def _stream(stream):
     return getattr(stream, "cuda_stream", stream)
 
 
+class PreparedRun:
+    """One marshalled mpccbf_run_steps call (Context.prepare_run_steps): calling it runs the steps
+    (the C call alone); it holds the tensors its pointers refer to."""
+
+    def __init__(self, ctx, batch, run, stream, states, states_alt, num_steps, step_ms, solve_ms, keep):
+        self._ctx, self._b, self._r, self._s = ctx, batch, run, stream
+        self._fn = load().mpccbf_run_steps
+        self._tables = (states, states_alt)
+        self._n, self._step_ms, self._solve_ms, self._keep = num_steps, step_ms, solve_ms, keep
+
+    def __call__(self):
+        _check(self._fn(self._ctx._h, C.byref(self._b), C.byref(self._r), self._s))
+        out = {"final": self._tables[0] if self._r.final_table == 0 else self._tables[1]}
+        if self._solve_ms is not None:
+            out["step_ms"] = None if self._step_ms is None else self._step_ms[:self._n]
+            sm = self._solve_ms[:self._n]
+            out["solve_ms"] = sm[sm >= 0]
+        return out
+
+
 class Context:
     """One controller configuration on one device (mpccbf_create / mpccbf_destroy)."""
 
@@ -263,13 +283,20 @@ class Context:
                   substeps=_ptr(substeps), nb_out=_ptr(nb_out))
         _check(load().mpccbf_impc_solve(self._h, C.byref(b), _stream(stream)))
 
-    def run_steps(self, states, states_alt, num_steps, targets=None, refs=None, agent_first=0,
+    def run_steps(self, *args, **kw):
+        """Closed-loop control steps on the device (mpccbf_run_steps): prepare_run_steps(...)()
+        in one call; see prepare_run_steps for the arguments and the returned dict."""
+        return self.prepare_run_steps(*args, **kw)()
+
+    def prepare_run_steps(self, states, states_alt, num_steps, targets=None, refs=None, agent_first=0,
                   num_agents=None, knn_k=0, knn_radius=0.0, nb_row_ptr=None, nb_col=None, x=None,
                   status=None, obj=None, iters=None, status_log=None, iters_log=None,
                   timing=False, comm=None, reserve_steps=0, solve_stride=1, step_timing=True,
                   stream=None, traj_t=None, pos_std=0.0, vel_std=0.0, noise_seed=0, step_index=0,
                   cov=None, kernel_clock=None, stamps=None, continue_tables=False):
-        """Closed-loop control steps on the device (mpccbf_run_steps). Returns a dict with the
+        """The arguments of one mpccbf_run_steps call, marshalled once (checks, ctypes structures,
+        the stream handle): returns a PreparedRun whose call () runs the steps — a caller that
+        times the steps prepares them outside its timed region. The call returns a dict with the
         table holding the final states ('final', a tensor) and, with timing=True, per-step
         device times 'step_ms' and IMPC-kernel times 'solve_ms' (numpy, ms). kernel_clock: a
         (num_steps, W, 2) device tensor (torch.int64, W >= launch_waves(num_agents)) for every
@@ -302,13 +329,9 @@ class Context:
                 solve_stride=solve_stride, kernel_clock=_ptr(kernel_clock),
                 kernel_clock_waves=0 if kernel_clock is None else int(kernel_clock.shape[1]),
                 continue_tables=int(bool(continue_tables)))
-        _check(load().mpccbf_run_steps(self._h, C.byref(b), C.byref(r), _stream(stream)))
-        out = {"final": states if r.final_table == 0 else states_alt}
-        if timing:
-            out["step_ms"] = None if step_ms is None else step_ms[:num_steps]
-            sm = solve_ms[:num_steps]
-            out["solve_ms"] = sm[sm >= 0]
-        return out
+        return PreparedRun(self, b, r, _stream(stream), states, states_alt, num_steps, step_ms, solve_ms,
+                           keep=(targets, refs, nb_row_ptr, nb_col, x, status, obj, iters, status_log,
+                                 iters_log, traj_t, cov, kernel_clock, stamps))
 
     def launch_waves(self, num_agents: int) -> int:
         """Waves of the IMPC launch for num_agents that write the launch clock (0: no clock)."""
