@@ -161,12 +161,6 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
     const int gl = lane_bits_opaque<63>();
     double pi[SEP_D][3];
     sep_pinv(Pinv, pi);
-    double pb[SEP_NZ][2];
-#pragma unroll
-    for (int o = 0; o < SEP_NZ; o++) {
-        pb[o][0] = P[o * 6 + 2 * (o / 2)];
-        pb[o][1] = P[o * 6 + 2 * (o / 2) + 1];
-    }
     // violation scales 1 / (1 + |bound|) and the candidate weight 1 / sqrt(g P^-1 g): the row's
     // (formed where the row is)
     const double sl = rw.sl, su = rw.su;
@@ -429,6 +423,14 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
         for (int j = 0; j < SEP_NZ; j++) nf = nf || !isfinite(y[j]);
         if (__ballot(nf) != 0ull) return 0;
     }
+    // P's blocks loaded here, where they are used (not live across the steps), and the active rows
+    // read without a branch per row (as sep_dual_as)
+    double pb[SEP_NZ][2];
+#pragma unroll
+    for (int o = 0; o < SEP_NZ; o++) {
+        pb[o][0] = P[o * 6 + 2 * (o / 2)];
+        pb[o][1] = P[o * 6 + 2 * (o / 2) + 1];
+    }
     double rd = 0.0, qn = 0.0;
     if (k == 0) {
 #pragma unroll
@@ -444,14 +446,19 @@ __device__ int wide_dual_as(const WRow& rw, const double* __restrict__ P, const 
             const int d = o / 2;
             r[o] = fma(pb[o][0], y[2 * d], fma(pb[o][1], y[2 * d + 1], q[o]));
         }
+        double g[WK][SEP_NZ + 1];
 #pragma unroll
         for (int i = 0; i < WK; i++) {
-            if (i < k) {
-                const double* ri = pol + i * 16;
-                const double li = ri[POL_SGN] * u[i];
+            const double* ri = pol + (i < k ? i : 0) * 16;  // (rows past k: row 0, weight 0)
 #pragma unroll
-                for (int o = 0; o < SEP_NZ; o++) r[o] = fma(li, ri[o], r[o]);
-            }
+            for (int o = 0; o < SEP_NZ; o++) g[i][o] = ri[o];
+            g[i][SEP_NZ] = ri[POL_SGN];
+        }
+#pragma unroll
+        for (int i = 0; i < WK; i++) {
+            const double li = i < k ? g[i][SEP_NZ] * u[i] : 0.0;
+#pragma unroll
+            for (int o = 0; o < SEP_NZ; o++) r[o] = fma(li, g[i][o], r[o]);
         }
 #pragma unroll
         for (int o = 0; o < SEP_NZ; o++) {

@@ -450,14 +450,6 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
     const int gl = lane_bits_opaque<G - 1>();
     double pi[SEP_D][3];
     sep_pinv(Pinv, pi);
-    // P's 2x2 channel blocks for the dual residual at the end, loaded here (uniform: scalar
-    // registers) so the loads are not on the converged solve's critical path
-    double pb[SEP_NZ][2];
-#pragma unroll
-    for (int o = 0; o < SEP_NZ; o++) {
-        pb[o][0] = P[o * 6 + 2 * (o / 2)];
-        pb[o][1] = P[o * 6 + 2 * (o / 2) + 1];
-    }
     constexpr int NS = 2 * SEP_D * SB + CB;
     double sc[NS];  // violation scale 1 / (1 + |bound|) per side
     {
@@ -865,6 +857,15 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
         for (int j = 0; j < SEP_NZ; j++) nf = nf || !isfinite(y[j]);
         if (grp_ballot<G>(nf) != 0ull) return 0;
     }
+    // P's 2x2 channel blocks (uniform), loaded here where the dual residual uses them: loaded at
+    // the solve's start, their 24 scalar registers stayed live across every step (round 6: with
+    // the branch-free row reads below, 29.3 -> 28.7 us per config-3 launch)
+    double pb[SEP_NZ][2];
+#pragma unroll
+    for (int o = 0; o < SEP_NZ; o++) {
+        pb[o][0] = P[o * 6 + 2 * (o / 2)];
+        pb[o][1] = P[o * 6 + 2 * (o / 2) + 1];
+    }
     double rd = 0.0, qn = 0.0;
     if (k == 0 && !want_rd) {
         // (rd = 0: not stored, and below the tolerance by construction)
@@ -876,24 +877,28 @@ __device__ int sep_dual_as(const SepRows<SB, CB>& rw, bool has_cbf, const double
             qn = fmax(qn, fabs(q[o]));
         }
     } else {
-        // G_A^T lam over the wave's largest active count only (scalar loop bound), each active
-        // row's entries read once
-        int kw = 0;
-#pragma unroll
-        for (int i = 1; i <= DK; i++) kw += __ballot(k >= i) != 0ull ? 1 : 0;
         double r[SEP_NZ];
 #pragma unroll
         for (int o = 0; o < SEP_NZ; o++) {
             const int d = o / 2;
             r[o] = fma(pb[o][0], y[2 * d], fma(pb[o][1], y[2 * d + 1], q[o]));
         }
+        // G_A^T lam: every staged row's entries loaded first, no per-row branch (rows past k read
+        // row 0 and weigh 0: the same sums as over the active rows alone)
+        {
+            double g[DK][SEP_NZ + 1];
 #pragma unroll
-        for (int i = 0; i < DK; i++) {
-            if (i < kw) {
-                const double* ri = pol + (i < k ? i : 0) * 16;
-                const double li = i < k ? ri[POL_SGN] * u[i] : 0.0;
+            for (int i = 0; i < DK; i++) {
+                const double* ri = pol + (i < k ? i : 0) * 16;  // (rows past k: row 0, weight 0)
 #pragma unroll
-                for (int o = 0; o < SEP_NZ; o++) r[o] = fma(li, ri[o], r[o]);
+                for (int o = 0; o < SEP_NZ; o++) g[i][o] = ri[o];
+                g[i][SEP_NZ] = ri[POL_SGN];
+            }
+#pragma unroll
+            for (int i = 0; i < DK; i++) {
+                const double li = i < k ? g[i][SEP_NZ] * u[i] : 0.0;
+#pragma unroll
+                for (int o = 0; o < SEP_NZ; o++) r[o] = fma(li, g[i][o], r[o]);
             }
         }
 #pragma unroll
