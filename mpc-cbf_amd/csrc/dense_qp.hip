@@ -84,6 +84,7 @@ struct DenseBatch {
     // count flags: 1 = reduced on the host (beyond the device elimination's 64 variables / 64
     // equalities; host/dense_qp.cpp), its reduced QP, status, m and pd uploaded, x expanded on the host
     const int32_t* hostred;  // (NULL: none)
+    const int32_t* psize;    // count x 2: the packed form's doubles and ints (its slot, off_d / off_i, is a bound)
     int32_t lds_rows, lds_stride;  // the reduce kernel's E^T image (reduce_stride)
     // the packed input (dbl, ints, off_*, red_off, hostred) lives in pinned host memory and is read
     // by the kernels over the bus (no copy); the reduce kernel first stages its QP's packed words
@@ -167,7 +168,7 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
         // 8 per lane in flight, so the bus latency is paid a few times instead of once per read
         double* sd = et + (size_t)(NROWS + ET_PAD) * LDS_S;
         int32_t* si = (int32_t*)(sd + a.stage_d);
-        const int nd = (int)(a.off_d[qi + 1] - a.off_d[qi]), ni = (int)(a.off_i[qi + 1] - a.off_i[qi]);
+        const int nd = a.psize[2 * qi], ni = a.psize[2 * qi + 1];  // (the packed sizes: the slot is a bound)
         // (doubles and ints in the same pass, 512 of each: 16 loads per lane in flight — two bus
         // round trips for a typical QP where separate passes took three)
         for (int e0 = 0; e0 < nd || e0 < ni; e0 += 8 * 64) {
@@ -746,66 +747,48 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     if (count < 0 || (count > 0 && (!qps || !status_out)))
         return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "dense QP batch: null argument");
     if (count == 0) return MPCCBF_OK;
-    // ---- host: validate and size every QP (worker pool), then pack each straight into the pinned
-    // input at its offset (worker pool). The kernels read it there over the bus: no copy
-    std::vector<PackPlan> plan(count);
-    parallel_for(count, [&](int k0, int k1) {
-        for (int k = k0; k < k1; k++) plan[k] = plan_qp(qps[k]);
-    });
-    for (int k = 0; k < count; k++)  // the first bad QP's error, as a serial pass would report
-        if (!plan[k].err.empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + plan[k].err);
-    // QPs beyond the device elimination (more than 64 variables or 64 equality rows): the equality
-    // elimination on the host (host/dense_qp.cpp), the reduced QP solved on the device like the rest
-    std::vector<int> big;
-    std::vector<ReducedQP> hred;
-    for (int k = 0; k < count; k++)
-        if (plan[k].cap) big.push_back(k);
-    hred.resize(big.size());
-    for (size_t b = 0; b < big.size(); b++) {
-        try {
-            hred[b] = reduce_dense_qp(qps[big[b]]);
-        } catch (const std::exception& ex) {
-            return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(big[b]) + ": " + ex.what());
-        }
-    }
-    // offsets (+ totals), reduced-QP blocks sized by their inequality rows (the reduced rows are a
-    // subset of them; a QP with more than DENSE_ROWS is a capacity error before its rows are read),
-    // the batch maxima that size the kernels (PDIP row slots, the reduction's LDS image and staging)
+    // ---- host, one pass per QP (worker pool, slice by slice ahead of each slice's reduction):
+    // validation, row classification and the packed form written straight into the pinned input,
+    // at an offset sized beforehand from n and m alone (an upper bound of the packed size: no
+    // separate sizing pass over H and A). The kernels read it there over the bus: no copy
     std::vector<int64_t> off_d(count + 1), off_i(count + 1), red_off(count);
     size_t nd = 0, ni = 0, nred = 0;
-    int rows_max = 1, nmax = 1, emax = 1, sd_max = 0, si_max = 0;
-    for (int k = 0, b = 0; k < count; k++) {
+    for (int k = 0; k < count; k++) {
         off_d[k] = (int64_t)nd;
         off_i[k] = (int64_t)ni;
-        nd += plan[k].nd + 1;  // (+1: the spare word pack_qp's compaction may write past the QP)
-        ni += plan[k].ni + 1;
         red_off[k] = (int64_t)nred;
-        int rows_k;
-        if (plan[k].cap) {
-            rows_k = std::min(hred[b++].m, DENSE_ROWS);
-        } else {
-            rows_k = std::min(plan[k].mi, DENSE_ROWS);
-            nmax = std::max(nmax, plan[k].n);
-            emax = std::max(emax, plan[k].me);
-            sd_max = std::max(sd_max, (int)plan[k].nd + 1);
-            si_max = std::max(si_max, (int)plan[k].ni + 1);
+        const int64_t n = qps[k].n, m = qps[k].m;
+        const bool packable = n >= 1 && n <= DENSE_NMAX && m >= 0;
+        if (packable) {  // (the sizes of pack_qp with nh <= n (n + 1) / 2, me + mi <= m + n, enz + inz <= m n + n)
+            const int64_t hmax = n * (n + 1) / 2, rows = m + n, nzmax = m * n + n;
+            nd += (size_t)(n + 1 + hmax + 2 * rows + nzmax) + 1;  // (+1: the spare word of pack_qp's compaction)
+            ni += (size_t)(4 + (rows + 1) + (2 * (rows + 1) + 2 * hmax + nzmax + 3) / 4) + 1;
         }
-        rows_max = std::max(rows_max, rows_k);
-        nred += (size_t)DQ_HDR + (size_t)std::max(rows_k, 1) * DQ_ROW;  // (>= 1 row: the kernel reads row 0)
+        // reduced-QP block: its reduced rows are a subset of the inequality rows (<= m + n); a QP
+        // with more than DENSE_ROWS is a capacity error before its rows are read
+        const int64_t rows_k = (n >= 1 && m >= 0) ? std::min<int64_t>(m + n, DENSE_ROWS) : 1;
+        nred += (size_t)DQ_HDR + (size_t)std::max<int64_t>(rows_k, 1) * DQ_ROW;  // (>= 1 row: the kernel reads row 0)
     }
     off_d[count] = (int64_t)nd;
     off_i[count] = (int64_t)ni;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_error(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        // (no device: the QPs' own argument errors still take precedence, as a host-side check)
+        for (int k = 0; k < count; k++) {
+            const PackPlan pl = plan_qp(qps[k]);
+            if (!pl.err.empty()) return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + pl.err);
+        }
+        return set_error(MPCCBF_ERR_NO_DEVICE, "no HIP device visible");
+    }
     int device = 0;
     hipError_t e = hipGetDevice(&device);
     // ---- pinned input: packed doubles | packed ints | off_d | off_i | red_off | host-reduced
-    // flags (only when there are host-reduced QPs); pinned output: x | obj | status
+    // flags | packed sizes (2 per QP); pinned output: x | obj | status
     const size_t b_d = align16(nd * sizeof(double)), b_i = align16(ni * sizeof(int32_t));
     const size_t b_off = align16((size_t)(count + 1) * sizeof(int64_t));
     const size_t b_int = align16((size_t)count * sizeof(int32_t));
-    const size_t b_hr = big.empty() ? 0 : b_int;
-    const size_t in_bytes = b_d + b_i + 3 * b_off + b_hr;
+    const size_t b_ps = align16((size_t)count * 2 * sizeof(int32_t));
+    const size_t in_bytes = b_d + b_i + 3 * b_off + b_int + b_ps;
     const size_t b_x = align16((size_t)count * DENSE_NMAX * sizeof(double));
     const size_t b_obj = align16((size_t)count * sizeof(double));
     if (e == hipSuccess) e = g_dense_host.reserve(in_bytes);
@@ -818,11 +801,10 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     int64_t* h_offi = (int64_t*)(hb + b_d + b_i + b_off);
     int64_t* h_redoff = (int64_t*)(hb + b_d + b_i + 2 * b_off);
     int32_t* h_hr = (int32_t*)(hb + b_d + b_i + 3 * b_off);
+    int32_t* h_ps = (int32_t*)(hb + b_d + b_i + 3 * b_off + b_int);
     std::memcpy(h_offd, off_d.data(), (count + 1) * sizeof(int64_t));
     std::memcpy(h_offi, off_i.data(), (count + 1) * sizeof(int64_t));
     std::memcpy(h_redoff, red_off.data(), count * sizeof(int64_t));
-    if (b_hr)
-        for (int k = 0; k < count; k++) h_hr[k] = plan[k].cap ? 1 : 0;
     // ---- device buffers: reduced QPs | Z, xp | y | status | m | pd | iters
     const size_t b_red = align16(nred * sizeof(double));
     const size_t b_zx = align16((size_t)count * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX) * sizeof(double));
@@ -836,7 +818,8 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     a.off_d = g_dense_host.dev<const int64_t>(h_offd);
     a.off_i = g_dense_host.dev<const int64_t>(h_offi);
     a.red_off = g_dense_host.dev<const int64_t>(h_redoff);
-    a.hostred = b_hr ? g_dense_host.dev<const int32_t>(h_hr) : nullptr;
+    a.hostred = g_dense_host.dev<const int32_t>(h_hr);
+    a.psize = g_dense_host.dev<const int32_t>(h_ps);
     a.count = count;
     a.red = (double*)p;
     p += b_red;
@@ -855,11 +838,6 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     a.maxit = 100;
     a.tol = 1e-9;
     a.feas_tol = 1e-6;
-    a.lds_rows = nmax;
-    a.lds_stride = dev::reduce_stride(nmax, emax);
-    size_t lds = (size_t)(a.lds_rows + dev::ET_PAD) * a.lds_stride * sizeof(double);
-    const size_t stage = (size_t)sd_max * sizeof(double) + (size_t)si_max * sizeof(int32_t);
-    a.stage_d = a.stage_i = 0;
     a.dstamps = nullptr;
 #ifdef MPCCBF_PDIP_STAMPS
     // profiling build: QP 0's reduction phases, printed to stderr with MPCCBF_DENSE_STAMPS=1
@@ -871,24 +849,70 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         a.dstamps = d_stamps;
     }
 #endif
-    if (lds + stage <= 48 * 1024) {  // (beyond: the kernel reads its QP over the bus where it uses it)
-        a.stage_d = sd_max;
-        a.stage_i = si_max;
-        lds += stage;
-    }
     hipStream_t s = nullptr;
-    // pack a slice (worker pool), launch its reduction, pack the next meanwhile
+    std::vector<PackPlan> plan(count);
+    // QPs beyond the device elimination (more than 64 variables or 64 equality rows): the equality
+    // elimination on the host (host/dense_qp.cpp, after the slices), the reduced QP solved on the
+    // device like the rest
+    std::vector<int> big;
+    int rows_max = 1;
+    // validate + pack a slice (worker pool), launch its reduction (sized by the slice's own
+    // largest QP), pack the next meanwhile; the first bad QP's error as a serial pass would report
+    // it (the slices before it are finished first: the pinned input stays theirs until then)
     const int nslice = count >= 1024 ? 4 : 1;
     const int slice = (count + nslice - 1) / nslice;
     for (int q0 = 0; q0 < count && e == hipSuccess; q0 += slice) {
         const int q1 = std::min(count, q0 + slice);
         parallel_for(q1 - q0, [&](int k0, int k1) {
-            for (int k = q0 + k0; k < q0 + k1; k++)
-                if (!plan[k].cap) pack_qp(qps[k], plan[k], h_d + off_d[k], h_i + off_i[k]);
+            for (int k = q0 + k0; k < q0 + k1; k++) {
+                plan[k] = plan_qp(qps[k]);
+                const PackPlan& pl = plan[k];
+                const bool packed = pl.err.empty() && !pl.cap;
+                if (packed) pack_qp(qps[k], pl, h_d + off_d[k], h_i + off_i[k]);
+                h_hr[k] = pl.cap ? 1 : 0;
+                h_ps[2 * k] = packed ? (int32_t)pl.nd + 1 : 0;  // (+1: the spare word, staged as before)
+                h_ps[2 * k + 1] = packed ? (int32_t)pl.ni + 1 : 0;
+            }
         });
+        int nmax = 1, emax = 1, sd_max = 0, si_max = 0;
+        for (int k = q0; k < q1; k++) {
+            if (!plan[k].err.empty()) {
+                (void)hipStreamSynchronize(s);
+                return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(k) + ": " + plan[k].err);
+            }
+            if (plan[k].cap) {
+                big.push_back(k);
+                continue;
+            }
+            rows_max = std::max(rows_max, std::min(plan[k].mi, DENSE_ROWS));
+            nmax = std::max(nmax, plan[k].n);
+            emax = std::max(emax, plan[k].me);
+            sd_max = std::max(sd_max, (int)plan[k].nd + 1);
+            si_max = std::max(si_max, (int)plan[k].ni + 1);
+        }
+        a.lds_rows = nmax;
+        a.lds_stride = dev::reduce_stride(nmax, emax);
+        size_t lds = (size_t)(a.lds_rows + dev::ET_PAD) * a.lds_stride * sizeof(double);
+        const size_t stage = (size_t)sd_max * sizeof(double) + (size_t)si_max * sizeof(int32_t);
+        a.stage_d = a.stage_i = 0;
+        if (lds + stage <= 48 * 1024) {  // (beyond: the kernel reads its QP over the bus where it uses it)
+            a.stage_d = sd_max;
+            a.stage_i = si_max;
+            lds += stage;
+        }
         a.first = q0;
         hipLaunchKernelGGL(dev::dense_reduce_kernel, dim3(q1 - q0), dim3(64), lds, s, a);
         e = hipGetLastError();
+    }
+    std::vector<ReducedQP> hred(big.size());
+    for (size_t b = 0; b < big.size() && e == hipSuccess; b++) {
+        try {
+            hred[b] = reduce_dense_qp(qps[big[b]]);
+        } catch (const std::exception& ex) {
+            (void)hipStreamSynchronize(s);
+            return set_error(MPCCBF_ERR_INVALID_ARGUMENT, "QP " + std::to_string(big[b]) + ": " + ex.what());
+        }
+        rows_max = std::max(rows_max, std::min(hred[b].m, DENSE_ROWS));
     }
     a.first = 0;
     // host-reduced QPs: their reduced form in the device layout (P, LP padded with the identity, q,
