@@ -657,7 +657,6 @@ static_assert(dense_pack::DENSE_NMAX == DENSE_NMAX && dense_pack::DENSE_EMAX == 
 using dense_pack::finite_bound;
 using dense_pack::PackPlan;
 using dense_pack::plan_qp;
-using dense_pack::pack_qp;
 
 // Host worker pool for the per-QP validation and packing: created on first use (up to 15 workers
 // beside the calling thread), kept for the process (a thread spawn per call cost more than the
@@ -864,11 +863,11 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     for (int q0 = 0; q0 < count && e == hipSuccess; q0 += slice) {
         const int q1 = std::min(count, q0 + slice);
         parallel_for(q1 - q0, [&](int k0, int k1) {
+            thread_local dense_pack::PackScratch scratch;
             for (int k = q0 + k0; k < q0 + k1; k++) {
-                plan[k] = plan_qp(qps[k]);
+                plan[k] = dense_pack::pack_qp_once(qps[k], h_d + off_d[k], h_i + off_i[k], scratch);
                 const PackPlan& pl = plan[k];
                 const bool packed = pl.err.empty() && !pl.cap;
-                if (packed) pack_qp(qps[k], pl, h_d + off_d[k], h_i + off_i[k]);
                 h_hr[k] = pl.cap ? 1 : 0;
                 h_ps[2 * k] = packed ? (int32_t)pl.nd + 1 : 0;  // (+1: the spare word, staged as before)
                 h_ps[2 * k + 1] = packed ? (int32_t)pl.ni + 1 : 0;

@@ -22,6 +22,21 @@ def toy():
                 hi=np.array([INF]))
 
 
+def test_one_scan_packer_matches_two_pass_form(tmp_path):
+    """The host's one-scan packer (dense_pack.hpp pack_qp_once, the product path) gives the plan,
+    the first error and the packed words of the two-pass form (plan_qp, then pack_qp) on seeded
+    random QPs covering every branch of the packer (tests/cpp/dense_pack_check.cpp). CPU only."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "dense_pack_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I" + repo, "-I" + os.path.join(repo, "include"),
+                    os.path.join(repo, "tests", "cpp", "dense_pack_check.cpp"), "-o", exe],
+                   check=True, capture_output=True, timeout=300)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "identical" in out.stdout
+
+
 def test_dense_invalid_arguments_rejected_on_host(mpclib):
     bad = dict(H=np.eye(2), c=np.array([0.0, np.nan]))
     with pytest.raises(mpclib.MpccbfError, match="non-finite"):

@@ -1,6 +1,7 @@
 // Host cost of the generic dense path's validation + packing (csrc/host/dense_pack.hpp) per QP,
 // one thread, on the golden MPC-CBF QPs replicated (tools/dense_pack_bench.py writes them):
-//   g++ -O3 -std=c++17 -I. tools/dense_pack_bench.cpp -o /tmp/dpb && /tmp/dpb /tmp/golden.bin
+//   g++ -O3 -std=c++17 -I. tools/dense_pack_bench.cpp -o /tmp/dpb && /tmp/dpb /tmp/golden.bin [once]
+// (plan_qp + pack_qp, the two-pass form; with a second argument pack_qp_once, the product's)
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -29,6 +30,8 @@ int main(int argc, char** argv) {
     }
     std::fclose(f);
     const int reps = 4096;
+    const bool once = argc > 2;  // (second argument: pack_qp_once)
+    PackScratch w;
     std::vector<double> d;
     std::vector<int32_t> ii;
     double best = 1e30;
@@ -38,13 +41,22 @@ int main(int argc, char** argv) {
         auto t0 = std::chrono::steady_clock::now();
         for (int r = 0; r < reps; r++) {
             const mpccbf_dense_qp& q = qps[r % count];
-            const PackPlan pl = plan_qp(q);
             const size_t od = d.size(), oi = ii.size();
-            d.resize(od + pl.nd + 1);
-            ii.resize(oi + pl.ni + 1);
-            pack_qp(q, pl, d.data() + od, ii.data() + oi);
-            d.pop_back();
-            ii.pop_back();
+            if (once) {  // one scan into a slot sized from n and m (dense_qp.hip)
+                const size_t n = q.n, m = q.m, hmax = n * (n + 1) / 2, rows = m + n, nz = m * n + n;
+                d.resize(od + n + 1 + hmax + 2 * rows + nz + 1);
+                ii.resize(oi + 4 + (rows + 1) + (2 * (rows + 1) + 2 * hmax + nz + 3) / 4 + 1);
+                const PackPlan pl = pack_qp_once(q, d.data() + od, ii.data() + oi, w);
+                d.resize(od + pl.nd);
+                ii.resize(oi + pl.ni);
+            } else {
+                const PackPlan pl = plan_qp(q);
+                d.resize(od + pl.nd + 1);
+                ii.resize(oi + pl.ni + 1);
+                pack_qp(q, pl, d.data() + od, ii.data() + oi);
+                d.pop_back();
+                ii.pop_back();
+            }
         }
         const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
         best = us < best ? us : best;
