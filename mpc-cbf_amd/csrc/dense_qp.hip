@@ -41,6 +41,7 @@
 #include "host/dense_qp.hpp"
 #include "host/errors.hpp"
 #include "kernels/group.hpp"
+#include "kernels/das_wave.hpp"
 #include "kernels/pdip.hpp"
 
 namespace mpccbf {
@@ -91,6 +92,7 @@ struct DenseBatch {
     // into LDS with one batch of loads: stage_d / stage_i words (the batch's largest QP; 0: direct)
     int32_t stage_d, stage_i;
     int32_t first;  // dense_reduce_kernel: the slice's first QP (block b reduces QP first + b)
+    int32_t das_steps;  // dense_qp_kernel: dual active-set steps before the PDIP (0: the PDIP alone)
     long long* dstamps;  // profiling build: QP 0's reduction phase stamps (24 words), else NULL
 };
 
@@ -530,6 +532,106 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
 }
 #undef DSTAMP
 
+// The dual active set (das_wave.hpp, the FoV controller's) on the reduced QP's row image, before
+// the PDIP: a QP with P positive definite whose rows fit the image. An optimum it returns is the
+// QP's exact optimum (primal and dual residuals checked): status OPTIMAL, y, its steps. Anything
+// else (no feasible point in sight, the step limit, a breakdown) stays RS_SOLVE for
+// dense_qp_kernel's PDIP and phase 1, as before. (Its own launch: inlined into the PDIP kernel
+// its state pushed that kernel into scratch.)
+template <int NZ>
+__global__ void __launch_bounds__(64) dense_das_kernel(const DenseBatch a) {
+    const int qi = blockIdx.x;
+    const int gl = threadIdx.x;
+    if (qi >= a.count || a.status[qi] != RS_SOLVE) return;  // decided by the reduction
+    const double* base = a.red + a.red_off[qi];
+    const double* P = base;
+    const double* LP = base + NZ * NZ;
+    const double* qv = base + 2 * NZ * NZ;
+    const double* rows = base + DQ_HDR;
+    const int m = a.m[qi];
+    const bool pd = a.pd[qi] != 0;
+    double q[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; i++) q[i] = qv[i];
+    // first: the dual active set (das_wave.hpp, the FoV controller's) on the row image, when P is
+    // positive definite and the rows fit its image; an optimum it returns is the QP's exact
+    // optimum (primal and dual residuals checked); anything else (no feasible point found, a
+    // step limit, a breakdown) goes to the PDIP below as before
+    if (pd && m <= WROWS && __builtin_amdgcn_readfirstlane(a.das_steps) > 0) {
+        static_assert(NZ <= WNZ, "the reduced dimension fits the 16-wide image");
+        __shared__ double Gimg[(WROWS + 1) * WNZ];  // (rows 0 .. m - 1, then row m all zero)
+        __shared__ double Pi8[NZ * NZ];             // P^-1 (from its Cholesky factor LP)
+        __shared__ WaveScratch sc;
+        __shared__ WaveAS ws;
+        // image rows: g (NZ) then zeros to WNZ; row m all zero (the unused slots' row)
+        for (int e = gl; e < (m + 1) * WNZ; e += 64) {
+            const int r = e / WNZ, j = e - r * WNZ;
+            Gimg[e] = (r < m && j < NZ) ? rows[(size_t)r * DQ_ROW + j] : 0.0;
+        }
+        // P^-1 column j = LP^-T LP^-1 e_j (lane j < NZ; LP lower triangular, row-major)
+        if (gl < NZ) {
+            double z[NZ];
+#pragma unroll
+            for (int i = 0; i < NZ; i++) {
+                double v = i == gl ? 1.0 : 0.0;
+#pragma unroll
+                for (int k = 0; k < i; k++) v = fma(-LP[i * NZ + k], z[k], v);
+                z[i] = v / LP[i * NZ + i];
+            }
+#pragma unroll
+            for (int i = NZ - 1; i >= 0; i--) {
+                double v = z[i];
+#pragma unroll
+                for (int k = i + 1; k < NZ; k++) v = fma(-LP[k * NZ + i], z[k], v);
+                z[i] = v / LP[i * NZ + i];
+            }
+#pragma unroll
+            for (int i = 0; i < NZ; i++) Pi8[i * NZ + gl] = z[i];
+        }
+        if (gl < WNZ) sc.q[gl] = gl < NZ ? q[gl < NZ ? gl : 0] : 0.0;
+        wave_lds_sync();
+        {
+            // the operators padded to 16 x 16 with the identity (das_store_operators' entries)
+            constexpr int NE = WNZ * WNZ / 64;
+            double pi[NE], pp[NE];
+#pragma unroll
+            for (int k = 0; k < NE; k++) {
+                const int e = gl + 64 * k, i = e >> 4, j = e & 15;
+                const bool in = i < NZ && j < NZ;
+                pi[k] = in ? Pi8[(in ? i : 0) * NZ + (in ? j : 0)] : (i == j ? 1.0 : 0.0);
+                pp[k] = in ? P[(in ? i : 0) * NZ + (in ? j : 0)] : (i == j ? 1.0 : 0.0);
+            }
+            das_store_operators(ws, pi, pp, gl);
+        }
+        WaveRows wr;
+#pragma unroll
+        for (int sl = 0; sl < WR; sl++) {
+            const int r = wave_owner_row(gl, sl);
+            const bool on = r < m;
+            const double* src = rows + (size_t)(on ? r : 0) * DQ_ROW;
+            const double l = on ? src[NZ] : -1e300, h = on ? src[NZ + 1] : 1e300;
+            wr.g[sl] = &Gimg[(on ? r : m) * WNZ];  // (row m: the zeroed row after the image)
+            // (every row has an upper side: a row without one gets an unreachable bound)
+            wr.hi[sl] = on ? (h < 1e300 ? h : 1e300) : 1.0;
+            wr.lo[sl] = on ? (l > -1e300 ? l : 0.0) : -1.0;
+            wr.ml[sl] = on ? (l > -1e300 ? 1.0 : 0.0) : 1.0;
+        }
+        double drp = 0.0, drd = 0.0, tlow = 0.0;
+        int dsteps = 0;
+        const int r = das_solve_wave(wr, Gimg, sc, ws, nullptr, nullptr, a.tol, a.das_steps, false, gl, drp, drd,
+                                     dsteps, tlow, nullptr, 0, m, nullptr, false);
+        if (r == 1) {
+            if (gl == 0) {
+                a.status[qi] = ST_OPTIMAL;
+                a.iters[qi] = dsteps;
+#pragma unroll
+                for (int i = 0; i < NZ; i++) a.y[(size_t)qi * NZ + i] = sc.y[i];
+            }
+            return;
+        }
+    }
+}
+
 template <int NZ, int R>
 __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
@@ -544,6 +646,9 @@ __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
     const int m = a.m[qi];
     const bool pd = a.pd[qi] != 0;
 
+    double q[NZ], y[NZ];
+#pragma unroll
+    for (int i = 0; i < NZ; i++) q[i] = qv[i];
     Rows<NZ, R> rw;
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -559,9 +664,6 @@ __global__ void __launch_bounds__(64) dense_qp_kernel(const DenseBatch a) {
         rw.lo[r] = hl ? l : 0.0;
         rw.hi[r] = hu ? h : 0.0;
     }
-    double q[NZ], y[NZ];
-#pragma unroll
-    for (int i = 0; i < NZ; i++) q[i] = qv[i];
     PdipCfg cfg{a.maxit, a.tol};
     cfg.reg = reg;
     const PdipOut po = pdip_solve<NZ, 64, R>(rw, P, pd ? LP : nullptr, q, y, cfg);
@@ -835,6 +937,7 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
     a.obj = g_dense_out.dev<double>(ho + b_x);
     a.status_out = g_dense_out.dev<int32_t>(ho + b_x + b_obj);
     a.maxit = 100;
+    a.das_steps = 48;
     a.tol = 1e-9;
     a.feas_tol = 1e-6;
     a.dstamps = nullptr;
@@ -956,6 +1059,10 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         if (e == hipSuccess) e = hipMemcpyAsync(a.status + k, &hst[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(a.m + k, &hm[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(a.pd + k, &hpd[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
+    }
+    if (e == hipSuccess && a.das_steps > 0 && rows_max <= dev::WROWS) {
+        hipLaunchKernelGGL((dev::dense_das_kernel<DENSE_NZ>), dim3(count), dim3(64), 0, s, a);
+        e = hipGetLastError();
     }
     if (e == hipSuccess) {
         if (rows_max <= 64) hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, 1>), dim3(count), dim3(64), 0, s, a);
