@@ -59,7 +59,12 @@ def gi(P, q, N, b, rule, tol=1e-6, maxstep=64):
         m = (v * sc).max()
         if m <= 0.1 * tol:
             return steps, len(A), y
-        sel = v * sc if rule == "scaled" else (v / nrm**2 if rule == "normal2" else v / nrm)
+        if rule == "scaled":
+            sel = v * sc
+        elif rule.startswith("pow"):  # v / |g|^e, e = the digits / 100 (pow150: 1.5)
+            sel = v / nrm ** (int(rule[3:]) / 100.0)
+        else:
+            sel = v / nrm**2 if rule == "normal2" else v / nrm
         p = int(np.argmax(np.where(v * sc > 0.1 * tol, sel, -np.inf)))
         up = 0.0
         while True:
@@ -115,7 +120,7 @@ def main():
     p = O.make_params(cfg)
     refs = swarm.refs_from_targets(targets, cfg["k_hor"])
     rng = np.random.default_rng(0)
-    tot = {"scaled": [], "normal": [], "diag": [], "euclid": []}
+    tot = {r: [] for r in (os.environ.get("DAS_RULES") or "scaled,normal,normal2,diag,euclid").split(",")}
     for s in range(iters.shape[0]):
         ags = list(np.where(iters[s, :, 1 if it1 else 0] >= min_steps)[0])
         if sample:
