@@ -532,6 +532,26 @@ __global__ void __launch_bounds__(64) dense_reduce_kernel(const DenseBatch a) {
 }
 #undef DSTAMP
 
+// x = xp + Z y and the objective of OPTIMAL QP qi (y: the reduced solution, global or LDS), its
+// final status into the pinned output (one wave)
+__device__ __forceinline__ void dense_expand_qp(const DenseBatch& a, int qi, int st, const double* yq, int l) {
+    if (l == 0) a.status_out[qi] = st;
+    if (st != ST_OPTIMAL || (a.hostred && a.hostred[qi])) return;  // (host-reduced: host expands)
+    // x = xp + Z y; the objective from the reduced QP, k0 + q^T y + 1/2 y^T P y (P, q, k0 in the
+    // device block the reduction wrote: nothing read from the host input)
+    const double* zx = a.zx + (size_t)qi * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX);
+    const double* red = a.red + a.red_off[qi];
+    double xv = zx[DENSE_NMAX * DENSE_NZ + l];
+#pragma unroll
+    for (int b = 0; b < DENSE_NZ; b++) xv = fma(zx[l * DENSE_NZ + b], yq[b], xv);
+    const int pa = l >> 3, pb = l & 7;  // lane (a, b): 1/2 P_ab y_a y_b; lanes 0..7 also q_l y_l
+    double f = 0.5 * red[l] * yq[pa] * yq[pb];
+    if (l < DENSE_NZ) f = fma(red[2 * DENSE_NZ * DENSE_NZ + l], yq[l], f);
+    f = grp_sum<64>(f);
+    a.x[(size_t)qi * DENSE_NMAX + l] = xv;  // (beyond n: 0; the host copies n)
+    if (l == 0) a.obj[qi] = f + red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 1];
+}
+
 // The dual active set (das_wave.hpp, the FoV controller's) on the reduced QP's row image, before
 // the PDIP: a QP with P positive definite whose rows fit the image. An optimum it returns is the
 // QP's exact optimum (primal and dual residuals checked): status OPTIMAL, y, its steps. Anything
@@ -542,7 +562,14 @@ template <int NZ>
 __global__ void __launch_bounds__(64) dense_das_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int gl = threadIdx.x;
-    if (qi >= a.count || a.status[qi] != RS_SOLVE) return;  // decided by the reduction
+    if (qi >= a.count) return;
+    {
+        const int st0 = a.status[qi];
+        if (st0 != RS_SOLVE) {  // decided by the reduction: its final status (and x) now
+            dense_expand_qp(a, qi, st0, a.y + (size_t)qi * NZ, gl);
+            return;
+        }
+    }
     const double* base = a.red + a.red_off[qi];
     const double* P = base;
     const double* LP = base + NZ * NZ;
@@ -550,6 +577,7 @@ __global__ void __launch_bounds__(64) dense_das_kernel(const DenseBatch a) {
     const double* rows = base + DQ_HDR;
     const int m = a.m[qi];
     const bool pd = a.pd[qi] != 0;
+    if (gl == 0) a.status_out[qi] = RS_SOLVE;  // (unsettled so far: the host's check, small batches)
     double q[NZ];
 #pragma unroll
     for (int i = 0; i < NZ; i++) q[i] = qv[i];
@@ -627,6 +655,7 @@ __global__ void __launch_bounds__(64) dense_das_kernel(const DenseBatch a) {
 #pragma unroll
                 for (int i = 0; i < NZ; i++) a.y[(size_t)qi * NZ + i] = sc.y[i];
             }
+            dense_expand_qp(a, qi, ST_OPTIMAL, sc.y, gl);  // (x, objective, the final status)
             return;
         }
     }
@@ -689,23 +718,7 @@ __global__ void __launch_bounds__(64) dense_expand_kernel(const DenseBatch a) {
     const int qi = blockIdx.x;
     const int l = threadIdx.x;
     if (qi >= a.count) return;
-    const int st = a.status[qi];
-    if (l == 0) a.status_out[qi] = st;
-    if (st != ST_OPTIMAL || (a.hostred && a.hostred[qi])) return;  // (host-reduced: host expands)
-    // x = xp + Z y; the objective from the reduced QP, k0 + q^T y + 1/2 y^T P y (P, q, k0 in the
-    // device block the reduction wrote: nothing read from the host input)
-    const double* zx = a.zx + (size_t)qi * (DENSE_NMAX * DENSE_NZ + DENSE_NMAX);
-    const double* red = a.red + a.red_off[qi];
-    const double* yq = a.y + (size_t)qi * DENSE_NZ;
-    double xv = zx[DENSE_NMAX * DENSE_NZ + l];
-#pragma unroll
-    for (int b = 0; b < DENSE_NZ; b++) xv = fma(zx[l * DENSE_NZ + b], yq[b], xv);
-    const int pa = l >> 3, pb = l & 7;  // lane (a, b): 1/2 P_ab y_a y_b; lanes 0..7 also q_l y_l
-    double f = 0.5 * red[l] * yq[pa] * yq[pb];
-    if (l < DENSE_NZ) f = fma(red[2 * DENSE_NZ * DENSE_NZ + l], yq[l], f);
-    f = grp_sum<64>(f);
-    a.x[(size_t)qi * DENSE_NMAX + l] = xv;  // (beyond n: 0; the host copies n)
-    if (l == 0) a.obj[qi] = f + red[2 * DENSE_NZ * DENSE_NZ + DENSE_NZ + 1];
+    dense_expand_qp(a, qi, a.status[qi], a.y + (size_t)qi * DENSE_NZ, l);
 }
 
 }  // namespace dev
@@ -1060,17 +1073,27 @@ int mpccbf_qp_solve_dense_batch(int32_t count, const mpccbf_dense_qp* qps, doubl
         if (e == hipSuccess) e = hipMemcpyAsync(a.m + k, &hm[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(a.pd + k, &hpd[b], sizeof(int32_t), hipMemcpyHostToDevice, s);
     }
+    // the active-set launch settles most QPs and writes their final outputs (and those of the QPs
+    // the reduction decided); a small batch whose QPs it all settled needs no PDIP and no
+    // expansion launch (the host checks the pinned statuses after one synchronisation)
+    bool settled = false;
     if (e == hipSuccess && a.das_steps > 0 && rows_max <= dev::WROWS) {
         hipLaunchKernelGGL((dev::dense_das_kernel<DENSE_NZ>), dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
+        if (e == hipSuccess && count <= 64 && big.empty()) {
+            e = hipStreamSynchronize(s);
+            const int32_t* so = (const int32_t*)(ho + b_x + b_obj);
+            settled = e == hipSuccess;
+            for (int k = 0; k < count && settled; k++) settled = so[k] != RS_SOLVE;
+        }
     }
-    if (e == hipSuccess) {
+    if (e == hipSuccess && !settled) {
         if (rows_max <= 64) hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, 1>), dim3(count), dim3(64), 0, s, a);
         else if (rows_max <= 128) hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, 2>), dim3(count), dim3(64), 0, s, a);
         else hipLaunchKernelGGL((dev::dense_qp_kernel<DENSE_NZ, DQ_R>), dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) {
+    if (e == hipSuccess && !settled) {
         hipLaunchKernelGGL(dev::dense_expand_kernel, dim3(count), dim3(64), 0, s, a);
         e = hipGetLastError();
     }
