@@ -331,7 +331,8 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
         // the candidate's P^-1 g on the row layout, published
         const double wi = rowdot17(ws.Pi, i, gp);
         publish16(ws.w, wi, lane);
-        const double nw = dotl_b<BOUND>(gp, ws.w);
+        // n_p^T P^-1 n_p from the lanes' own products (a 16-lane sum), not read back from ws.w
+        const double nw = grp_sum<16>(gp[i] * wi);
         WSTAMP(3, steps == 0);
         double up = 0.0;  // the candidate's multiplier
         for (;;) {
