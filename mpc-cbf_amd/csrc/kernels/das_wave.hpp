@@ -351,7 +351,7 @@ __device__ __forceinline__ int das_solve_wave(const WaveRows& rw, const double* 
             const double vi = fwd_rows(L, inv_i, ci, i, kk);
             const double rhoi = bwd_rows(sc.M, inv_i, vi, i, kk);
             const double zn = nw - grp_sum<16>(vi * vi);
-            const double vp = sp * (dotl_b<BOUND>(gp, sc.y) - bp);
+            const double vp = sp * (grp_sum<16>(gp[i] * yi) - bp);  // (y's lanes in registers, as nw)
             WSTAMP(4, steps == 1);
             // dual step: the first active multiplier to reach zero
             const double r_i = sgi * rhoi;
